@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Headline benchmark: remote one-sided put/get GiB/s + p50 ocm_alloc latency.
+
+BASELINE.json metric: "remote put/get GiB/s + p50 ocm_alloc latency, 4 KiB-1 GiB,
+1/2/4/8 MI355X". The workload is the reference's R/W sweep (`ocm_test 4`,
+reference test/ocm_test.c:323-425): a 2 GiB+1 remote pair, one-sided reads and
+writes of every power-of-two size — here 4 KiB .. 1 GiB — each op blocking, as
+in the reference. The reference never timed it; we do.
+
+One step = for every size s: get(s) then put(s), on every rank concurrently.
+Each rank is one app process on its own MI355X with its own ocmd daemon; the
+daemons form one mesh (rank0 = master/placement). Remote halves are placed by
+the governor:
+  pattern "stripe" (default): striped over every peer GPU (all xGMI links),
+  pattern "ring": reference placement (orig_rank + 1) % N, one peer per rank.
+With a single GPU there is no peer HBM: the remote half lives in the daemon's
+pinned host tier (PCIe), like the reference's single-node coercion to host
+memory (src/alloc.c:82-83).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+Rank 0 prints ONE JSON line. value = total bytes moved by all ranks per
+second (GiB/s) over the K timed steps, timed max-over-ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "remote put/get GiB/s + p50 ocm_alloc latency, 4 KiB-1 GiB, 1/2/4/8 MI355X"
+GiB = float(1 << 30)
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--device", choices=["auto", "gpu", "cpu"], default="auto")
+    ap.add_argument("--min-bytes", type=int, default=4096)
+    ap.add_argument("--max-bytes", type=int, default=None, help="largest transfer (default 1 GiB; 16 MiB on CPU)")
+    ap.add_argument("--pattern", choices=["stripe", "ring"], default="stripe")
+    ap.add_argument("--alloc-samples", type=int, default=200)
+    ap.add_argument("--no-characterize", action="store_true")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def coord_init(world: int):
+    """gloo group for coordination only: touches no GPU, so every rank can
+    start its daemon before HIP is initialised in this process."""
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    return dist
+
+
+def gather_obj(dist, obj, world):
+    if dist is None:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def main() -> int:
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = args.gpus if args.gpus is not None else world
+    if n_gpus != world:
+        print(f"--gpus {n_gpus} but WORLD_SIZE={world}; launch with torch.distributed.run for N>1", file=sys.stderr)
+        return 2
+
+    import torch  # noqa: F401  (device count without HIP init)
+
+    ndev = torch.cuda.device_count()
+    use_gpu = args.device == "gpu" or (args.device == "auto" and ndev > 0)
+    if use_gpu and local_rank >= ndev:
+        print(f"rank {rank}: LOCAL_RANK {local_rank} but only {ndev} GPUs", file=sys.stderr)
+        return 2
+    max_bytes = args.max_bytes or ((1 << 30) if use_gpu else (16 << 20))
+
+    from oncilla_amd import api
+    from oncilla_amd.models import workloads as wl
+    from oncilla_amd.parallel.mesh import Mesh, free_ports
+    from oncilla_amd.utils.paths import is_built
+
+    if not is_built():
+        if rank == 0:
+            from oncilla_amd.utils.build import build
+
+            build()
+    dist = coord_init(world)
+    if dist is not None:
+        dist.barrier()
+
+    # ---- daemon mesh: one ocmd per rank / GPU ----
+    my_port = free_ports(1)[0]
+    ports = gather_obj(dist, my_port, world)
+    ns = f"bench{os.environ.get('MASTER_PORT', '0')}_{ports[0]}"
+    workdir = os.path.join("/tmp", f"ocm_{ns}")
+    os.makedirs(workdir, exist_ok=True)
+    gpus = [(local_rank if use_gpu else None) for _ in range(world)]
+    if use_gpu:
+        # every rank's GPU ordinal (single node: LOCAL_RANK == RANK)
+        gpus = gather_obj(dist, local_rank, world)
+    policy = "stripe" if args.pattern == "stripe" else "ring"
+    mesh = Mesh(world, gpus=gpus, ns=ns, policy=policy, workdir=workdir, ports=ports, ranks=[rank])
+    mesh.start(timeout=120)
+    if dist is not None:
+        dist.barrier()
+
+    result = {}
+    client = None
+    try:
+        client = api.Client(daemon_rank=rank, gpu=(local_rank if use_gpu else None), ns=ns)
+        if not use_gpu:
+            os.environ["OCM_NO_GPU"] = "1"
+        client.init()
+        remote_kind = api.OCM_REMOTE_GPU if use_gpu else api.OCM_REMOTE_RDMA
+
+        # ---- p50 ocm_alloc latency (remote pair, and the local malloc path) ----
+        lat_remote = wl.alloc_latency(client, remote_kind, args.alloc_samples, local_bytes=64 << 10,
+                                      remote_bytes=1 << 20)
+        lat_local = wl.alloc_latency(client, api.OCM_LOCAL_HOST, args.alloc_samples, local_bytes=1 << 20)
+        if dist is not None:
+            dist.barrier()
+
+        # ---- the sweep pair: 2 x max + 1 bytes each side (reference: 2 GiB + 1) ----
+        pair_bytes = 2 * max_bytes + 1
+        pair = client.alloc(remote_kind, local_bytes=pair_bytes, remote_bytes=pair_bytes)
+        info = pair.remote_info()
+
+        # verify: pattern -> put -> clobber -> get -> check
+        pair.fill(seed=1234 + rank, nbytes=max_bytes)
+        pair.put(0, 0, max_bytes)
+        pair.fill(seed=0, nbytes=max_bytes)
+        pair.get(0, 0, max_bytes)
+        bad = pair.check(seed=1234 + rank, nbytes=max_bytes)
+        if bad:
+            raise RuntimeError(f"rank {rank}: {bad} words differ after put/get round trip")
+
+        sizes = wl.sweep_sizes(args.min_bytes, max_bytes)
+        for _ in range(args.warmup):
+            wl.rw_sweep_step(pair, sizes)
+
+        def sync():
+            if use_gpu:
+                torch.cuda.synchronize(local_rank)
+
+        if dist is not None:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        moved = 0
+        for _ in range(args.steps):
+            moved += wl.rw_sweep_step(pair, sizes)
+        sync()
+        t1 = time.perf_counter()
+        if dist is not None:
+            dist.barrier()
+        elapsed = t1 - t0
+
+        # max over ranks of elapsed, sum of bytes
+        stats = gather_obj(dist, {"elapsed": elapsed, "moved": moved, "lat": lat_remote, "lat_local": lat_local,
+                                  "extents": info["extents"]}, world)
+        t_max = max(s["elapsed"] for s in stats)
+        total = sum(s["moved"] for s in stats)
+
+        sweep = {}
+        if not args.no_characterize:
+            ch = wl.characterize(pair, sizes)
+            chs = gather_obj(dist, ch, world)
+            for s in sizes:
+                g = max(c[s]["get_s"] for c in chs)
+                p = max(c[s]["put_s"] for c in chs)
+                sweep[str(s)] = {"get_GiBps": round(world * s / g / GiB, 3), "put_GiBps": round(world * s / p / GiB, 3),
+                                 "get_us": round(g * 1e6, 2), "put_us": round(p * 1e6, 2)}
+        pair.free()
+        if dist is not None:
+            dist.barrier()  # every rank is done with every owner before daemons stop
+
+        value = total / t_max / GiB
+        tiers = sorted({e["tier"] for s in stats for e in s["extents"]})
+        result = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "uint8",
+            "data": "synthetic (hash-pattern fill, put/get round trip verified on device)",
+            "config": {
+                "model": "ocm_test-4 R/W sweep, 2x1GiB+1 remote pair per rank" if max_bytes == 1 << 30
+                else f"ocm_test-4 R/W sweep, max {max_bytes} B",
+                "global_batch": world,
+                "seq_len": max_bytes,
+                "parallelism": f"{args.pattern}{world}",
+                "pattern": args.pattern,
+                "remote_tier": "+".join({1: "host", 2: "hbm"}[t] for t in tiers),
+                "extents_per_pair": len(stats[0]["extents"]),
+                "sizes": f"{args.min_bytes}..{max_bytes} x2",
+                "device": "gpu" if use_gpu else "cpu",
+            },
+            "alloc_p50_us": round(max(s["lat"]["alloc_p50_us"] for s in stats), 2),
+            "alloc_p99_us": round(max(s["lat"]["alloc_p99_us"] for s in stats), 2),
+            "free_p50_us": round(max(s["lat"]["free_p50_us"] for s in stats), 2),
+            "local_alloc_p50_us": round(max(s["lat_local"]["alloc_p50_us"] for s in stats), 2),
+            "sweep": sweep,
+        }
+    finally:
+        if client is not None:
+            client.close()
+        mesh.stop()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        line = json.dumps(result)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

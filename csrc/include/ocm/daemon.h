@@ -1,0 +1,169 @@
+// ocmd: one daemon per MI355X (or per host when CPU-only).
+//
+// Parity with reference src/main.c + src/mem.c (daemon entry, app registry,
+// mailbox poller, inter-daemon protocol, listener/inbound/request threads) and
+// src/alloc.c (owner-side alloc/free). Re-designed as ONE epoll event loop:
+//   * app mailbox (POSIX mqueue fd), mesh sockets, app pidfds (crash reclaim),
+//     signalfd — no thread per request, no usleep(500) poll, no busy spin;
+//   * persistent mesh links instead of a TCP connection per RPC;
+//   * rank0 owns the Governor (directory + placement);
+//   * owners serve DO_ALLOC from a registered Arena (HBM slabs exported with
+//     hipIpcGetMemHandle, pinned host-tier slabs);
+//   * requests are asynchronous state machines keyed by a sequence number.
+#pragma once
+#include <sys/types.h>
+
+#include <cstdint>
+#include <deque>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "ocm/arena.h"
+#include "ocm/governor.h"
+#include "ocm/msg.h"
+#include "ocm/nodefile.h"
+#include "ocm/pmsg.h"
+#include "ocm/sock.h"
+
+namespace ocm {
+
+struct DaemonConfig {
+    std::string nodefile;
+    int rank = -1;
+    int gpu = -2;                    // -2 auto, -1 CPU-only, >=0 explicit
+    std::string ns;
+    Policy policy = Policy::Ring;
+    uint64_t stripe_unit = 1ull << 20;
+    uint64_t slab_bytes = 1ull << 30;
+    uint64_t gpu_capacity = 0;       // 0: fraction of free HBM
+    double gpu_fraction = 0.75;
+    uint64_t host_capacity = 0;      // 0: fraction of MemAvailable
+    double host_fraction = 0.25;
+    int join_timeout_ms = 60000;
+    bool zero_on_alloc = false;
+    std::string ready_file;
+    std::string bind_ip;             // default: 0.0.0.0
+};
+
+int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err);
+
+class Daemon {
+public:
+    explicit Daemon(const DaemonConfig &cfg);
+    ~Daemon();
+    int run();           // blocks until shutdown; returns exit code
+    void request_stop() { stop_ = true; }
+
+private:
+    struct App {
+        pid_t pid = 0;
+        std::string mbox;
+        int pidfd = -1;
+        int mqfd = -1;
+        std::deque<Msg> backlog;
+        bool watching_out = false;
+    };
+    struct Pending {
+        uint64_t seq = 0;
+        uint64_t app_seq = 0;     // the app's correlation id, echoed in the reply
+        long t0_ms = 0;           // for the request timeout sweep
+        pid_t pid = 0;            // 0: internal (reclaim), no app reply
+        uint32_t type = 0;        // MSG_REQ_ALLOC / MSG_REQ_FREE / MSG_STATS
+        int expect = 0, got = 0;
+        int err = 0;
+        uint64_t alloc_id = 0;
+        uint64_t stripe_unit = 0;
+        uint64_t total_bytes = 0;
+        uint32_t kind = 0;
+        std::vector<Region> extents;
+        std::vector<bool> have;
+        std::set<int> awaiting;   // ranks we wait on (peer death fails the request)
+    };
+    struct OriginAlloc {
+        pid_t pid = 0;
+        bool remote = false;
+        uint64_t bytes = 0;
+        std::vector<Region> extents;
+    };
+    struct OwnedExtent {
+        uint32_t slab_id = 0;
+        uint64_t offset = 0;
+        uint32_t tier = 0;
+        int orig_rank = -1;
+        uint64_t bytes = 0;
+    };
+
+    int init();
+    void shutdown();
+    int loop();
+    void ep_add(int fd, uint32_t events, uint64_t tag);
+    void ep_mod(int fd, uint32_t events, uint64_t tag);
+    void ep_del(int fd);
+
+    // sources
+    void on_mailbox();
+    void on_accept();
+    void on_conn_readable(int fd);
+    void on_conn_writable(int fd);
+    void on_pidfd(pid_t pid);
+    void on_app_writable(pid_t pid);
+    void on_signal();
+    void drop_conn(int fd);
+
+    // dispatch
+    void handle_app_msg(Msg &m);
+    void handle_mesh_msg(Msg &m, int from_fd);
+    void send_rank(int r, Msg &m);      // to a daemon (self = local queue)
+    void send_app(pid_t pid, const Msg &m);
+
+    // protocol steps
+    void app_connect(const Msg &m);
+    void app_disconnect(pid_t pid, bool crashed);
+    void app_req_alloc(Msg &m);
+    void app_req_free(Msg &m);
+    void app_stats(Msg &m);
+    void r0_add_node(const NodeConfig &cfg);
+    void r0_req_alloc(Msg &m);
+    void r0_place_fail(Msg &m);
+    void owner_do_alloc(Msg &m);
+    void owner_do_free(Msg &m);
+    void origin_do_alloc_resp(Msg &m);
+    void origin_do_free_resp(Msg &m);
+    void finish_alloc(Pending &p);
+    void start_free(uint64_t alloc_id, pid_t reply_pid, uint64_t reply_seq);
+    void fail_pending_on(int rank);
+    void peer_lost(int rank);
+    void sweep_timeouts();
+
+    NodeConfig my_config() const;
+    void check_ready();
+    uint64_t next_seq() { return ++seq_; }
+
+    DaemonConfig cfg_;
+    NodeFile nf_;
+    int rank_ = -1, n_ = 0, gpu_ = -1, num_gpu_ = 0;
+    uint64_t gpu_total_ = 0;
+    std::string ns_;
+    Mailbox box_;
+    int ep_ = -1, listen_fd_ = -1, sig_fd_ = -1;
+    bool stop_ = false, ready_ = false;
+    std::unique_ptr<Arena> arena_;
+    std::unique_ptr<Governor> gov_;
+    std::map<int, std::unique_ptr<Conn>> conns_;   // fd -> connection
+    std::vector<int> peer_fd_;                     // rank -> fd (-1 none)
+    std::vector<NodeConfig> table_;
+    std::vector<bool> joined_;
+    std::deque<Msg> self_q_;
+    std::map<pid_t, App> apps_;
+    std::map<uint64_t, Pending> pending_;
+    std::map<uint64_t, OriginAlloc> origin_allocs_;
+    std::map<std::pair<uint64_t, int>, OwnedExtent> owned_;
+    uint64_t seq_ = 0, local_ids_ = 0;
+    int request_timeout_ms_ = 30000;
+    uint64_t n_alloc_ = 0, n_free_ = 0, n_reclaimed_ = 0, n_spilled_ = 0;
+};
+
+}  // namespace ocm

@@ -1,0 +1,114 @@
+// Allocation governor: rank0's directory and placement policy.
+//
+// Parity with reference src/alloc.c:59-140 (alloc_add_node, alloc_find): rank0
+// records joining nodes and decides where a request lands; HOST/GPU kinds stay
+// on the origin, remote kinds go to (orig_rank + 1) % N. Extended MI355X-first:
+//   * capacity accounting per daemon for HBM and the pinned host tier, fed by
+//     hipMemGetInfo at join (the reference's get_free_mem check was commented out);
+//   * an explicit remote_rank is honoured (reference field "not yet used");
+//   * policies: ring (reference), least_loaded, stripe (one allocation spread
+//     over several peers so put/get use several xGMI links), loopback;
+//   * spill to the host tier when HBM is exhausted, ENOMEM when both are;
+//   * an allocation table keyed by alloc_id for free/crash reclaim.
+// Pure logic (no I/O) so it is unit-tested on CPU.
+#pragma once
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "ocm/msg.h"
+
+namespace ocm {
+
+enum class Policy { Ring, LeastLoaded, Stripe, Loopback };
+Policy parse_policy(const std::string &s, Policy dflt);
+const char *policy_name(Policy p);
+
+struct NodeState {
+    int rank = -1;
+    bool joined = false;
+    bool alive = false;
+    int gpu = -1;
+    uint64_t gpu_capacity = 0, gpu_reserved = 0;
+    uint64_t host_capacity = 0, host_reserved = 0;
+    std::string host;
+};
+
+struct PlacedExtent {
+    int owner = -1;
+    uint32_t tier = TIER_NONE;
+    uint64_t bytes = 0;
+    bool spilled = false;
+};
+
+struct PlaceRequest {
+    int orig_rank = 0;
+    int remote_rank = -1;
+    uint64_t bytes = 0;
+    uint32_t flags = 0;         // ocm_alloc_flags
+    uint32_t stripe_width = 0;  // 0 = all peers
+    uint64_t stripe_unit = 0;
+    bool remote = true;         // false: local kind (owner = orig)
+    uint32_t local_tier = TIER_HOST;
+    int app_pid = 0;
+};
+
+struct Placement {
+    uint64_t alloc_id = 0;
+    uint64_t stripe_unit = 0;   // 0: single extent
+    std::vector<PlacedExtent> extents;
+    int err = 0;                // errno (ENOMEM, EINVAL, EHOSTDOWN)
+};
+
+class Governor {
+public:
+    Governor(int num_nodes, Policy policy, uint64_t default_stripe_unit);
+    void add_node(const NodeConfig &cfg);       // ADD_NODE
+    void mark_dead(int rank);
+    const NodeState &node(int rank) const { return nodes_.at(rank); }
+    int num_nodes() const { return static_cast<int>(nodes_.size()); }
+    int num_alive() const;
+    Policy policy() const { return policy_; }
+
+    // Decide owners for a request, reserve capacity, assign an alloc_id.
+    Placement place(const PlaceRequest &r);
+    // Re-place one extent of a live allocation after its owner failed DO_ALLOC.
+    // Returns false when nothing fits.
+    bool replace_extent(uint64_t alloc_id, int extent_idx, int failed_owner, PlacedExtent *out);
+    // Release an allocation (all extents). Returns false when unknown.
+    bool release(uint64_t alloc_id);
+    // Drop every allocation of an app (crash reclaim) or whose origin died.
+    std::vector<uint64_t> allocations_of_app(int orig_rank, int pid) const;
+    std::vector<uint64_t> allocations_from(int orig_rank) const;
+    size_t live_allocations() const { return table_.size(); }
+    uint64_t spilled_count() const { return n_spilled_; }
+
+    struct Entry {
+        int orig_rank;
+        int pid;
+        Placement placement;
+    };
+    const Entry *find(uint64_t id) const;
+
+private:
+    bool fits(const NodeState &n, uint32_t tier, uint64_t bytes) const;
+    void reserve(int rank, uint32_t tier, uint64_t bytes, int sign);
+    std::vector<int> candidates(const PlaceRequest &r) const;
+    bool place_one(int preferred, uint64_t bytes, uint32_t want_tier, bool allow_spill,
+                   const std::vector<int> &fallback, const std::vector<int> &spill_to, PlacedExtent *out);
+
+    std::vector<NodeState> nodes_;
+    Policy policy_;
+    uint64_t default_stripe_unit_;
+    uint64_t next_id_ = 1;
+    uint64_t n_spilled_ = 0;
+    std::map<uint64_t, Entry> table_;
+};
+
+// Stripe geometry shared by the governor, daemon and data plane: an allocation
+// of `total` bytes striped over `n` extents in units of `unit` bytes puts unit
+// u on extent u % n at extent offset (u / n) * unit.
+uint64_t stripe_extent_bytes(uint64_t total, uint64_t unit, int n, int idx);
+
+}  // namespace ocm

@@ -1,0 +1,130 @@
+// Wire record shared by app<->daemon (mailbox) and daemon<->daemon (mesh).
+//
+// Parity: reference inc/msg.h:24-73 defines one fixed 160-byte `struct message`
+// with {type, status, pid, rank, union{request, allocation, node config}} and the
+// CONNECT/ADD_NODE/REQ_ALLOC/DO_ALLOC/REQ_FREE/DO_FREE/RELEASE_APP states. This
+// record keeps that size and those states, and adds what an asynchronous
+// event-loop daemon needs: a correlation sequence number, an explicit sender
+// rank and an error code. The allocation body carries the peer-memory export
+// handle (hipIpcMemHandle_t, 64 B) where the reference carried ib_ip[64].
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+namespace ocm {
+
+constexpr size_t kMsgBytes = 160;
+constexpr size_t kHandleBytes = 64;  // == sizeof(hipIpcMemHandle_t)
+constexpr int kMaxExtents = 8;       // == OCM_MAX_EXTENTS
+
+enum MsgType : uint32_t {
+    MSG_INVALID = 0,
+    MSG_CONNECT,          // app -> daemon
+    MSG_CONNECT_CONFIRM,  // daemon -> app (carries node config of the daemon)
+    MSG_DISCONNECT,       // app -> daemon
+    MSG_ADD_NODE,         // daemon -> rank0 on boot (node config)
+    MSG_REQ_ALLOC,        // app -> daemon -> rank0
+    MSG_DO_ALLOC,         // rank0 -> owner; owner -> origin daemon (response)
+    MSG_REQ_FREE,         // app -> daemon
+    MSG_DO_FREE,          // origin daemon -> owner; owner -> origin (response)
+    MSG_RELEASE_APP,      // daemon -> app: request finished (header of a reply)
+    // --- additions ---
+    MSG_EXTENT,           // daemon -> app: one extent of a multi-extent reply
+    MSG_HELLO,            // mesh link handshake
+    MSG_NODE_TABLE,       // rank0 -> all: one node config per message
+    MSG_PLACE_FAIL,       // owner -> rank0: DO_ALLOC failed, re-place
+    MSG_FREED,            // owner -> rank0: capacity returned
+    MSG_STATS,            // app -> daemon (-> peer): statistics query
+    MSG_APP_DEAD,         // origin daemon -> rank0: app crashed, drop its directory entries
+    MSG_SHUTDOWN,         // any -> daemon: orderly exit
+    MSG_PING,             // liveness / latency probe
+    MSG_MAX
+};
+
+enum MsgStatus : uint32_t { MSG_NO_STATUS = 0, MSG_REQUEST, MSG_RESPONSE };
+
+enum Tier : uint32_t { TIER_NONE = 0, TIER_HOST = 1, TIER_GPU = 2 };
+
+// Request body (REQ_ALLOC / REQ_FREE / STATS).
+struct AllocReq {
+    int32_t orig_rank;     // daemon the app is attached to
+    int32_t remote_rank;   // requested owner, -1 = rank0 decides
+    uint64_t bytes;        // remote bytes (pairs) or local bytes (local kinds)
+    uint32_t kind;         // enum ocm_kind of the app request
+    uint32_t flags;        // enum ocm_alloc_flags
+    uint32_t stripe_width;
+    uint32_t tier;         // requested tier (TIER_GPU unless HOST_TIER flag)
+    uint64_t stripe_unit;
+    uint64_t alloc_id;     // REQ_FREE: the allocation to free
+    int32_t app_pid;
+    int32_t n_extents;     // REQ_FREE: extents the app holds
+    uint8_t pad[72];
+};
+
+// One placed extent (DO_ALLOC response, EXTENT, DO_FREE).
+enum RegionFlags : uint16_t {
+    REGION_DEDICATED = 1u << 0,  // slab holds only this extent: importer unmaps it on free
+    REGION_SPILLED = 1u << 1,    // placed in the host tier because HBM was exhausted
+};
+
+struct Region {
+    uint64_t alloc_id;
+    uint64_t bytes;        // bytes of this extent
+    uint64_t offset;       // offset of the extent inside its slab
+    uint64_t slab_bytes;
+    uint64_t stripe_unit;  // 0 when the allocation is a single extent
+    uint32_t slab_id;
+    int32_t owner_rank;
+    int32_t orig_rank;
+    int32_t owner_gpu;     // node-local device ordinal, -1 for host tier
+    uint16_t tier;         // enum Tier
+    uint16_t flags;        // enum RegionFlags
+    uint16_t extent_idx;
+    uint16_t n_extents;
+    uint8_t handle[kHandleBytes];  // hipIpcMemHandle_t (GPU) or "/proc/<pid>/fd/<n>" (host)
+};
+
+// Node description (ADD_NODE / NODE_TABLE / CONNECT_CONFIRM / STATS reply).
+struct NodeConfig {
+    char host[40];
+    int32_t rank;
+    int32_t gpu;           // device ordinal, -1 = CPU-only daemon
+    int32_t num_gpu;       // GPUs visible on the node
+    int32_t pid;
+    uint64_t gpu_total;    // bytes of HBM on `gpu`
+    uint64_t gpu_capacity; // bytes this daemon may hand out
+    uint64_t host_capacity;
+    uint64_t gpu_used;
+    uint64_t host_used;
+    uint32_t num_nodes;
+    uint32_t num_apps;
+    uint32_t n_alloc, n_free, n_reclaimed, n_spilled, n_slabs;
+    uint32_t pad;
+};
+
+struct Msg {
+    uint32_t type;     // MsgType
+    uint32_t status;   // MsgStatus
+    int32_t pid;       // app which made the request
+    int32_t rank;      // rank of the daemon that originated the request
+    uint64_t seq;      // correlation id (origin daemon scope)
+    int32_t src_rank;  // rank of the sender of this record (-1 = app)
+    int32_t err;       // 0 or a positive errno
+    union {
+        AllocReq req;
+        Region region;
+        NodeConfig node;
+        uint8_t raw[128];
+    } u;
+};
+
+static_assert(sizeof(AllocReq) == 128, "AllocReq must be 128 bytes");
+static_assert(sizeof(Region) == 128, "Region must be 128 bytes");
+static_assert(sizeof(NodeConfig) == 128, "NodeConfig must be 128 bytes");
+static_assert(sizeof(Msg) == kMsgBytes, "wire record must stay 160 bytes");
+static_assert(offsetof(Msg, u) == 32, "union must start at byte 32");
+
+const char *msg_type_str(uint32_t t);
+const char *msg_status_str(uint32_t s);
+
+}  // namespace ocm

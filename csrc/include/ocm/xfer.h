@@ -1,0 +1,61 @@
+// Data-plane transfer engine: one-sided put/get between a linear buffer and a
+// (possibly striped) remote buffer, as hand-written gfx950 kernels.
+//
+// Replaces the reference's one-sided fabric operations:
+//   ib_write/ib_read  (RDMA WRITE/READ, src/rdma.c:46-85,240-263)
+//   extoll_write/read (RMA2 put/get in 8 MiB chunks x 2 in flight, src/extoll.c:40-173)
+// On MI355X the "NIC" is the GPU itself: a kernel on the initiating GPU streams
+// 16-byte vectors between its HBM and peer HBM mapped over xGMI (IPC import).
+// A put pushes (local loads, remote stores); a get pulls (remote loads).
+// A remote buffer can be striped over several owners: unit u of the striped
+// address space lives on extent u % n at extent offset (u / n) * unit, so one
+// launch drives several xGMI links at once.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+namespace ocm {
+
+constexpr int kXferMaxExtents = 8;
+
+struct XferArgs {
+    char *lin;                       // linear side, already offset to the first byte
+    char *ext[kXferMaxExtents];      // extent bases of the striped side
+    uint64_t rem_off;                // first byte in striped coordinates
+    uint64_t len;                    // bytes
+    uint32_t unit_shift;             // log2(stripe unit); ignored when n_ext == 1
+    uint32_t n_ext;                  // 1..8
+    uint32_t tile_shift;             // log2(tile bytes), tile <= unit
+    uint32_t put;                    // 1: lin -> striped, 0: striped -> lin
+};
+
+enum XferVariant : int {
+    XFER_AUTO = 0,
+    XFER_REG = 1,    // register-staged, 8 x 16 B loads in flight per lane
+    XFER_LDS = 2,    // LDS-DMA (global_load_lds_dwordx4) staged, wave-private double buffer
+};
+
+struct XferTuning {
+    int variant = XFER_AUTO;
+    int max_blocks = 0;      // 0: per-path default
+    bool nontemporal = true; // nt stores on the destination
+};
+
+// Launch one transfer on `stream`. Returns hipSuccess or the launch error.
+hipError_t xfer_launch(const XferArgs &a, const XferTuning &t, hipStream_t stream);
+
+// Plain device copy dst <- src (both device-accessible), via the same kernel.
+hipError_t xfer_copy(void *dst, const void *src, uint64_t bytes, const XferTuning &t, hipStream_t stream);
+
+// Default tuning from the environment (OCM_XFER_VARIANT, OCM_XFER_BLOCKS, OCM_XFER_NT).
+XferTuning xfer_tuning_from_env();
+
+// Deterministic 32-bit word pattern (word i of a buffer) for data verification.
+hipError_t pattern_fill(void *p, uint64_t words, uint64_t first_word, uint32_t seed, hipStream_t stream);
+// Adds the number of mismatching words to *bad_dev (device memory).
+hipError_t pattern_check(const void *p, uint64_t words, uint64_t first_word, uint32_t seed, unsigned long long *bad_dev,
+                         hipStream_t stream);
+uint32_t pattern_word_host(uint64_t i, uint32_t seed);
+
+}  // namespace ocm

@@ -1,0 +1,146 @@
+/*
+ * oncillamem.h — public C ABI of libocm (MI355X-native OncillaMem).
+ *
+ * Parity: same entry points, enum values and struct layouts as the reference
+ * app interface (reference inc/oncillamem.h:24-89):
+ *   - enum ocm_kind values OCM_LOCAL_HOST=1 .. OCM_REMOTE_GPU=7
+ *   - struct ocm_params       (48 B)  src/dest offsets, *_2 offsets, bytes, op_flag
+ *   - struct ocm_alloc_params (24 B)  local_alloc_bytes, rem_alloc_bytes, kind
+ *
+ * What the kinds mean on MI355X (one backend, not a dispatch layer):
+ *   OCM_LOCAL_HOST   page-aligned host memory of the calling process
+ *   OCM_LOCAL_GPU    HBM of the calling process' GPU
+ *   OCM_REMOTE_GPU   pair: local half in the app GPU's HBM, remote half in the
+ *                    HBM of a peer MI355X (placed by rank0) reached over xGMI,
+ *                    or in a daemon's pinned host tier when HBM is exhausted
+ *   OCM_REMOTE_RDMA  pair whose local half is pinned host memory (CPU-visible,
+ *   OCM_REMOTE_RMA   like the reference's malloc'd IB/EXTOLL bounce buffer);
+ *                    remote half placed exactly like OCM_REMOTE_GPU
+ *   OCM_LOCAL_RDMA / OCM_LOCAL_RMA  accepted as OCM_LOCAL_HOST (the reference
+ *                    never implemented them).
+ *
+ * Functions added for MI355X (async put/get, striping, explicit placement,
+ * daemon statistics) are declared after the reference block.
+ */
+#ifndef ONCILLAMEM_H
+#define ONCILLAMEM_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lib_alloc *ocm_alloc_t;
+
+enum ocm_kind {
+    OCM_LOCAL_HOST = 1,
+    OCM_LOCAL_RMA,
+    OCM_REMOTE_RMA,
+    OCM_LOCAL_RDMA,
+    OCM_REMOTE_RDMA,
+    OCM_LOCAL_GPU,
+    OCM_REMOTE_GPU,
+};
+
+/* General parameters for one-sided / two-sided copies.
+ * op_flag: read = 0, write = 1. */
+struct ocm_params {
+    uint64_t src_offset;
+    uint64_t dest_offset;
+    uint64_t src_offset_2;
+    uint64_t dest_offset_2;
+    uint64_t bytes;
+    int op_flag;
+};
+typedef struct ocm_params *ocm_param_t;
+
+struct ocm_alloc_params {
+    uint64_t local_alloc_bytes;
+    uint64_t rem_alloc_bytes;
+    enum ocm_kind kind;
+};
+typedef struct ocm_alloc_params *ocm_alloc_param_t;
+
+/* ---------------- reference API (inc/oncillamem.h:69-89) ---------------- */
+int ocm_init(void);
+int ocm_tini(void);
+ocm_alloc_t ocm_alloc(ocm_alloc_param_t alloc_param);
+int ocm_free(ocm_alloc_t a);
+int ocm_localbuf(ocm_alloc_t a, void **buf, size_t *len);
+bool ocm_is_remote(ocm_alloc_t a);
+enum ocm_kind ocm_alloc_kind(ocm_alloc_t a);
+int ocm_remote_sz(ocm_alloc_t a, size_t *len);
+/* Implemented (stubs in the reference, src/lib.c:491-499):
+ * copy_in  writes min(local,remote) bytes from `src` into the allocation
+ *          (remote half for pairs, the buffer itself for local kinds);
+ * copy_out reads them back into `dst`. Host or device pointers accepted. */
+int ocm_copy_out(void *dst, ocm_alloc_t src);
+int ocm_copy_in(ocm_alloc_t dst, void *src);
+int ocm_copy(ocm_alloc_t dst, ocm_alloc_t src, ocm_param_t options);
+int ocm_copy_onesided(ocm_alloc_t src, ocm_param_t options);
+
+/* ---------------- MI355X extensions ---------------- */
+
+enum ocm_alloc_flags {
+    OCM_ALLOC_STRIPE      = 1u << 0, /* stripe the remote half over several peers (xGMI links) */
+    OCM_ALLOC_HOST_TIER   = 1u << 1, /* place the remote half in a daemon's pinned host tier */
+    OCM_ALLOC_NO_SPILL    = 1u << 2, /* fail instead of spilling to the host tier */
+    OCM_ALLOC_ZERO        = 1u << 3, /* zero the remote half before returning */
+    OCM_ALLOC_LOOPBACK    = 1u << 4, /* remote half in the origin daemon's own HBM */
+};
+
+struct ocm_alloc_ex_params {
+    int32_t  remote_rank;   /* -1: rank0 places; >=0: honour this owner (reference field was unused) */
+    uint32_t flags;         /* enum ocm_alloc_flags */
+    uint32_t stripe_width;  /* 0: all peers; else max number of owners */
+    uint32_t reserved;
+    uint64_t stripe_unit;   /* bytes per stripe unit, 0: default (OCM_STRIPE_UNIT or 1 MiB) */
+};
+
+enum ocm_tier { OCM_TIER_NONE = 0, OCM_TIER_HOST = 1, OCM_TIER_GPU = 2 };
+
+#define OCM_MAX_EXTENTS 8
+
+struct ocm_remote_info {
+    uint32_t n_extents;
+    uint32_t tier[OCM_MAX_EXTENTS];       /* enum ocm_tier per extent */
+    int32_t  owner_rank[OCM_MAX_EXTENTS];
+    int32_t  owner_gpu[OCM_MAX_EXTENTS];  /* device ordinal on the node, -1 for host */
+    uint64_t extent_bytes[OCM_MAX_EXTENTS];
+    uint64_t stripe_unit;
+    uint64_t alloc_id;
+    uint64_t remote_bytes;
+};
+
+struct ocm_daemon_stats {
+    int32_t  rank;
+    int32_t  gpu;
+    int32_t  num_nodes;
+    int32_t  num_apps;
+    uint64_t gpu_capacity, gpu_used;
+    uint64_t host_capacity, host_used;
+    uint64_t n_alloc, n_free, n_reclaimed, n_spilled;
+    uint64_t n_slabs;
+    uint64_t reserved[4];
+};
+
+ocm_alloc_t ocm_alloc_ex(ocm_alloc_param_t alloc_param, const struct ocm_alloc_ex_params *ex);
+/* Non-blocking variants: enqueue on the allocation's stream; ocm_wait() completes them. */
+int ocm_copy_onesided_async(ocm_alloc_t a, ocm_param_t options);
+int ocm_wait(ocm_alloc_t a);
+int ocm_remote_info(ocm_alloc_t a, struct ocm_remote_info *info);
+/* Device pointer of the remote half when it is a single extent (NULL if striped). */
+void *ocm_remotebuf(ocm_alloc_t a);
+int ocm_stats(int rank, struct ocm_daemon_stats *out); /* rank -1: local daemon */
+int ocm_rank(void);        /* rank of the daemon this process is attached to */
+int ocm_num_nodes(void);   /* daemons in the mesh */
+int ocm_device(void);      /* HIP device the library copies on, -1 when CPU-only */
+const char *ocm_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ONCILLAMEM_H */

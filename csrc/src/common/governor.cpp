@@ -1,0 +1,290 @@
+#include "ocm/governor.h"
+
+#include <algorithm>
+#include <cerrno>
+
+#include "../../include/oncillamem.h"
+#include "ocm/log.h"
+
+namespace ocm {
+
+Policy parse_policy(const std::string &s, Policy dflt) {
+    if (s == "ring") return Policy::Ring;
+    if (s == "least_loaded" || s == "least-loaded") return Policy::LeastLoaded;
+    if (s == "stripe") return Policy::Stripe;
+    if (s == "loopback" || s == "local") return Policy::Loopback;
+    return dflt;
+}
+
+const char *policy_name(Policy p) {
+    switch (p) {
+    case Policy::Ring: return "ring";
+    case Policy::LeastLoaded: return "least_loaded";
+    case Policy::Stripe: return "stripe";
+    case Policy::Loopback: return "loopback";
+    }
+    return "?";
+}
+
+uint64_t stripe_extent_bytes(uint64_t total, uint64_t unit, int n, int idx) {
+    if (n <= 1 || unit == 0) return idx == 0 ? total : 0;
+    const uint64_t units = (total + unit - 1) / unit;
+    if ((uint64_t)idx >= units) return 0;
+    const uint64_t cnt = (units - (uint64_t)idx + (uint64_t)n - 1) / (uint64_t)n;
+    const uint64_t last = units - 1;
+    if (last % (uint64_t)n == (uint64_t)idx) return (cnt - 1) * unit + (total - last * unit);
+    return cnt * unit;
+}
+
+Governor::Governor(int num_nodes, Policy policy, uint64_t default_stripe_unit)
+    : nodes_(num_nodes), policy_(policy), default_stripe_unit_(default_stripe_unit ? default_stripe_unit : (1ull << 20)) {
+    for (int i = 0; i < num_nodes; i++) nodes_[i].rank = i;
+}
+
+void Governor::add_node(const NodeConfig &cfg) {
+    if (cfg.rank < 0 || cfg.rank >= (int)nodes_.size()) {
+        OCM_WARN("ADD_NODE for rank %d outside nodefile (%zu nodes)", cfg.rank, nodes_.size());
+        return;
+    }
+    NodeState &n = nodes_[cfg.rank];
+    if (n.joined) {
+        // A restarted daemon lost its memory: forget what it owned.
+        OCM_WARN("rank %d re-joined; dropping its previous allocations", cfg.rank);
+        for (auto it = table_.begin(); it != table_.end();) {
+            bool owned = false;
+            for (auto &e : it->second.placement.extents) owned |= e.owner == cfg.rank;
+            if (owned) {
+                for (auto &e : it->second.placement.extents)
+                    if (e.owner != cfg.rank) reserve(e.owner, e.tier, e.bytes, -1);
+                it = table_.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        n.gpu_reserved = n.host_reserved = 0;
+    }
+    n.joined = true;
+    n.alive = true;
+    n.gpu = cfg.gpu;
+    n.gpu_capacity = cfg.gpu_capacity;
+    n.host_capacity = cfg.host_capacity;
+    n.host = std::string(cfg.host, strnlen(cfg.host, sizeof(cfg.host)));
+}
+
+void Governor::mark_dead(int rank) {
+    if (rank >= 0 && rank < (int)nodes_.size()) nodes_[rank].alive = false;
+}
+
+int Governor::num_alive() const {
+    int c = 0;
+    for (auto &n : nodes_) c += n.alive && n.joined;
+    return c;
+}
+
+bool Governor::fits(const NodeState &n, uint32_t tier, uint64_t bytes) const {
+    if (!n.alive || !n.joined) return false;
+    if (tier == TIER_GPU) return n.gpu >= 0 && n.gpu_reserved + bytes <= n.gpu_capacity;
+    if (tier == TIER_HOST) return n.host_reserved + bytes <= n.host_capacity;
+    return false;
+}
+
+void Governor::reserve(int rank, uint32_t tier, uint64_t bytes, int sign) {
+    if (rank < 0 || rank >= (int)nodes_.size()) return;
+    NodeState &n = nodes_[rank];
+    uint64_t &slot = tier == TIER_GPU ? n.gpu_reserved : n.host_reserved;
+    if (sign > 0)
+        slot += bytes;
+    else
+        slot = slot >= bytes ? slot - bytes : 0;
+}
+
+std::vector<int> Governor::candidates(const PlaceRequest &r) const {
+    std::vector<int> out;
+    const int n = (int)nodes_.size();
+    for (int d = 1; d < n; d++) {
+        int k = (r.orig_rank + d) % n;
+        if (nodes_[k].alive && nodes_[k].joined) out.push_back(k);
+    }
+    return out;
+}
+
+bool Governor::place_one(int preferred, uint64_t bytes, uint32_t want_tier, bool allow_spill,
+                         const std::vector<int> &fallback, const std::vector<int> &spill_to, PlacedExtent *out) {
+    auto take = [&](int rank, uint32_t tier, bool spilled) {
+        reserve(rank, tier, bytes, +1);
+        out->owner = rank;
+        out->tier = tier;
+        out->bytes = bytes;
+        out->spilled = spilled;
+        if (spilled) n_spilled_++;
+        return true;
+    };
+    if (fits(nodes_[preferred], want_tier, bytes)) return take(preferred, want_tier, false);
+    for (int k : fallback)
+        if (k != preferred && fits(nodes_[k], want_tier, bytes)) return take(k, want_tier, false);
+    if (allow_spill && want_tier == TIER_GPU) {
+        if (fits(nodes_[preferred], TIER_HOST, bytes)) return take(preferred, TIER_HOST, true);
+        for (int k : spill_to)
+            if (k != preferred && fits(nodes_[k], TIER_HOST, bytes)) return take(k, TIER_HOST, true);
+    }
+    return false;
+}
+
+Placement Governor::place(const PlaceRequest &r) {
+    Placement p;
+    const int n = (int)nodes_.size();
+    if (r.bytes == 0 || r.orig_rank < 0 || r.orig_rank >= n) {
+        p.err = EINVAL;
+        return p;
+    }
+    if (!r.remote) {
+        // Local kinds: the app allocates the memory itself; rank0 only records it.
+        PlacedExtent e;
+        e.owner = r.orig_rank;
+        e.tier = r.local_tier;
+        e.bytes = r.bytes;
+        p.extents.push_back(e);
+        p.alloc_id = next_id_++;
+        table_[p.alloc_id] = Entry{r.orig_rank, r.app_pid, p};
+        table_[p.alloc_id].placement.extents[0].tier = TIER_NONE;  // nothing reserved
+        return p;
+    }
+    uint32_t want_tier = (r.flags & OCM_ALLOC_HOST_TIER) ? TIER_HOST : TIER_GPU;
+    const bool allow_spill = !(r.flags & OCM_ALLOC_NO_SPILL);
+    std::vector<int> peers = candidates(r);
+    std::vector<int> owners;
+    bool explicit_owner = false;
+    if (r.remote_rank >= 0) {
+        if (r.remote_rank >= n || !nodes_[r.remote_rank].alive) {
+            p.err = r.remote_rank >= n ? EINVAL : EHOSTDOWN;
+            return p;
+        }
+        owners.push_back(r.remote_rank);
+        explicit_owner = true;
+    } else if ((r.flags & OCM_ALLOC_LOOPBACK) || policy_ == Policy::Loopback) {
+        owners.push_back(r.orig_rank);
+        explicit_owner = true;
+    } else if (peers.empty()) {
+        // Single daemon: no peer HBM exists, the remote half lives in the host tier
+        // (the reference coerced every request to host memory here, src/alloc.c:82-83).
+        owners.push_back(r.orig_rank);
+        want_tier = TIER_HOST;
+    } else if ((r.flags & OCM_ALLOC_STRIPE) || policy_ == Policy::Stripe) {
+        owners = peers;
+        size_t width = r.stripe_width ? r.stripe_width : owners.size();
+        width = std::min<size_t>({width, owners.size(), (size_t)kMaxExtents});
+        owners.resize(width);
+    } else if (policy_ == Policy::LeastLoaded) {
+        int best = peers[0];
+        uint64_t best_free = 0;
+        for (int k : peers) {
+            const NodeState &s = nodes_[k];
+            uint64_t f = s.gpu_capacity > s.gpu_reserved ? s.gpu_capacity - s.gpu_reserved : 0;
+            if (f > best_free) {
+                best_free = f;
+                best = k;
+            }
+        }
+        owners.push_back(best);
+    } else {
+        owners.push_back(peers[0]);  // ring: (orig + 1) % N, skipping dead nodes
+    }
+
+    uint64_t unit = r.stripe_unit ? r.stripe_unit : default_stripe_unit_;
+    int nx = (int)owners.size();
+    if (nx > 1) {
+        const uint64_t units = (r.bytes + unit - 1) / unit;
+        if (units < (uint64_t)nx) nx = (int)units;
+    }
+    if (nx <= 1) unit = 0;
+
+    std::vector<int> fallback = explicit_owner ? std::vector<int>{} : peers;
+    if (!explicit_owner && want_tier == TIER_HOST) fallback.push_back(r.orig_rank);
+    // HBM exhausted: spill to a host tier, peers first, then the origin node's own.
+    std::vector<int> spill_to = explicit_owner ? std::vector<int>{} : peers;
+    if (!explicit_owner) spill_to.push_back(r.orig_rank);
+    for (int i = 0; i < nx; i++) {
+        PlacedExtent e;
+        const uint64_t b = stripe_extent_bytes(r.bytes, unit, nx, i);
+        if (!place_one(owners[i], b, want_tier, allow_spill, fallback, spill_to, &e)) {
+            for (auto &done : p.extents) reserve(done.owner, done.tier, done.bytes, -1);
+            p.extents.clear();
+            p.err = ENOMEM;
+            return p;
+        }
+        p.extents.push_back(e);
+    }
+    p.stripe_unit = unit;
+    p.alloc_id = next_id_++;
+    table_[p.alloc_id] = Entry{r.orig_rank, r.app_pid, p};
+    return p;
+}
+
+bool Governor::replace_extent(uint64_t alloc_id, int idx, int failed_owner, PlacedExtent *out) {
+    auto it = table_.find(alloc_id);
+    if (it == table_.end() || idx < 0 || idx >= (int)it->second.placement.extents.size()) return false;
+    PlacedExtent &old = it->second.placement.extents[idx];
+    reserve(old.owner, old.tier, old.bytes, -1);
+    std::vector<int> order;
+    const int n = (int)nodes_.size();
+    for (int d = 1; d <= n; d++) {
+        int k = (failed_owner + d) % n;
+        if (k != failed_owner) order.push_back(k);
+    }
+    PlacedExtent e;
+    // Try HBM elsewhere first, then any host tier (including the failed owner's).
+    bool ok = false;
+    for (int k : order)
+        if (!ok && fits(nodes_[k], TIER_GPU, old.bytes) && old.tier == TIER_GPU) {
+            reserve(k, TIER_GPU, old.bytes, +1);
+            e = PlacedExtent{k, TIER_GPU, old.bytes, false};
+            ok = true;
+        }
+    if (!ok) {
+        order.insert(order.begin(), failed_owner);
+        for (int k : order)
+            if (!ok && fits(nodes_[k], TIER_HOST, old.bytes)) {
+                reserve(k, TIER_HOST, old.bytes, +1);
+                e = PlacedExtent{k, TIER_HOST, old.bytes, old.tier == TIER_GPU};
+                ok = true;
+            }
+    }
+    if (!ok) {
+        old.owner = -1;
+        return false;
+    }
+    if (e.spilled) n_spilled_++;
+    old = e;
+    *out = e;
+    return true;
+}
+
+bool Governor::release(uint64_t alloc_id) {
+    auto it = table_.find(alloc_id);
+    if (it == table_.end()) return false;
+    for (auto &e : it->second.placement.extents)
+        if (e.owner >= 0 && e.tier != TIER_NONE) reserve(e.owner, e.tier, e.bytes, -1);
+    table_.erase(it);
+    return true;
+}
+
+std::vector<uint64_t> Governor::allocations_of_app(int orig_rank, int pid) const {
+    std::vector<uint64_t> v;
+    for (auto &kv : table_)
+        if (kv.second.orig_rank == orig_rank && kv.second.pid == pid) v.push_back(kv.first);
+    return v;
+}
+
+std::vector<uint64_t> Governor::allocations_from(int orig_rank) const {
+    std::vector<uint64_t> v;
+    for (auto &kv : table_)
+        if (kv.second.orig_rank == orig_rank) v.push_back(kv.first);
+    return v;
+}
+
+const Governor::Entry *Governor::find(uint64_t id) const {
+    auto it = table_.find(id);
+    return it == table_.end() ? nullptr : &it->second;
+}
+
+}  // namespace ocm

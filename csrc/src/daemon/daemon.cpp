@@ -1,0 +1,1206 @@
+#include "ocm/daemon.h"
+
+#include <fcntl.h>
+#include <hip/hip_runtime_api.h>
+#include <signal.h>
+#include <sys/epoll.h>
+#include <sys/signalfd.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+
+#include "../../include/oncillamem.h"
+#include "ocm/log.h"
+
+namespace ocm {
+
+namespace {
+
+enum Tag : uint64_t { T_MBOX = 1, T_LISTEN, T_CONN, T_PIDFD, T_APPMQ, T_SIGNAL };
+inline uint64_t tag(Tag k, uint64_t id) { return (static_cast<uint64_t>(k) << 56) | (id & 0x00ffffffffffffffull); }
+inline Tag tag_kind(uint64_t t) { return static_cast<Tag>(t >> 56); }
+inline uint64_t tag_id(uint64_t t) { return t & 0x00ffffffffffffffull; }
+
+long now_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1000L + ts.tv_nsec / 1000000L;
+}
+
+int pidfd_open_compat(pid_t pid) { return (int)syscall(SYS_pidfd_open, pid, 0); }
+
+bool is_remote_kind(uint32_t kind) {
+    return kind == OCM_REMOTE_GPU || kind == OCM_REMOTE_RDMA || kind == OCM_REMOTE_RMA;
+}
+
+uint64_t parse_bytes(const std::string &s) {
+    char *end = nullptr;
+    double v = std::strtod(s.c_str(), &end);
+    std::string suf = end ? end : "";
+    uint64_t mul = 1;
+    if (suf == "K" || suf == "KiB" || suf == "k") mul = 1ull << 10;
+    else if (suf == "M" || suf == "MiB") mul = 1ull << 20;
+    else if (suf == "G" || suf == "GiB") mul = 1ull << 30;
+    else if (suf == "T" || suf == "TiB") mul = 1ull << 40;
+    return (uint64_t)(v * (double)mul);
+}
+
+uint64_t mem_available() {
+    std::ifstream f("/proc/meminfo");
+    std::string k;
+    uint64_t v;
+    std::string unit;
+    while (f >> k >> v >> unit)
+        if (k == "MemAvailable:") return v * 1024ull;
+    return 0;
+}
+
+}  // namespace
+
+int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err) {
+    auto env = [](const char *k) -> const char * {
+        const char *v = std::getenv(k);
+        return (v && *v) ? v : nullptr;
+    };
+    if (const char *v = env("OCM_NODEFILE")) cfg->nodefile = v;
+    if (const char *v = env("OCM_PLACEMENT")) cfg->policy = parse_policy(v, cfg->policy);
+    if (const char *v = env("OCM_STRIPE_UNIT")) cfg->stripe_unit = parse_bytes(v);
+    if (const char *v = env("OCM_SLAB_BYTES")) cfg->slab_bytes = parse_bytes(v);
+    if (const char *v = env("OCM_GPU_CAPACITY")) cfg->gpu_capacity = parse_bytes(v);
+    if (const char *v = env("OCM_HOST_CAPACITY")) cfg->host_capacity = parse_bytes(v);
+    if (const char *v = env("OCM_GPU_FRACTION")) cfg->gpu_fraction = std::atof(v);
+    if (const char *v = env("OCM_HOST_FRACTION")) cfg->host_fraction = std::atof(v);
+    if (env("OCM_ZERO_ON_ALLOC")) cfg->zero_on_alloc = true;
+    if (env("OCM_NO_GPU")) cfg->gpu = -1;
+    for (int i = 1; i < argc; i++) {
+        std::string a = argv[i];
+        auto val = [&](std::string *out) {
+            if (i + 1 >= argc) {
+                *err = "missing value for " + a;
+                return false;
+            }
+            *out = argv[++i];
+            return true;
+        };
+        std::string v;
+        if (a == "--rank") {
+            if (!val(&v)) return -1;
+            cfg->rank = std::atoi(v.c_str());
+        } else if (a == "--gpu") {
+            if (!val(&v)) return -1;
+            cfg->gpu = (v == "none" || v == "cpu") ? -1 : std::atoi(v.c_str());
+        } else if (a == "--ns") {
+            if (!val(&cfg->ns)) return -1;
+        } else if (a == "--policy") {
+            if (!val(&v)) return -1;
+            cfg->policy = parse_policy(v, cfg->policy);
+        } else if (a == "--stripe-unit") {
+            if (!val(&v)) return -1;
+            cfg->stripe_unit = parse_bytes(v);
+        } else if (a == "--slab-bytes") {
+            if (!val(&v)) return -1;
+            cfg->slab_bytes = parse_bytes(v);
+        } else if (a == "--gpu-capacity") {
+            if (!val(&v)) return -1;
+            cfg->gpu_capacity = parse_bytes(v);
+        } else if (a == "--host-capacity") {
+            if (!val(&v)) return -1;
+            cfg->host_capacity = parse_bytes(v);
+        } else if (a == "--join-timeout-ms") {
+            if (!val(&v)) return -1;
+            cfg->join_timeout_ms = std::atoi(v.c_str());
+        } else if (a == "--ready-file") {
+            if (!val(&cfg->ready_file)) return -1;
+        } else if (a == "--bind") {
+            if (!val(&cfg->bind_ip)) return -1;
+        } else if (a == "--zero") {
+            cfg->zero_on_alloc = true;
+        } else if (!a.empty() && a[0] == '-') {
+            *err = "unknown option " + a;
+            return -1;
+        } else {
+            cfg->nodefile = a;
+        }
+    }
+    if (cfg->nodefile.empty()) {
+        *err = "usage: ocmd <nodefile> [--rank R] [--gpu G|none] [--ns NS] [--policy ring|least_loaded|stripe|loopback]";
+        return -1;
+    }
+    if (cfg->ns.empty()) cfg->ns = pmsg_namespace();
+    return 0;
+}
+
+Daemon::Daemon(const DaemonConfig &cfg) : cfg_(cfg) {}
+
+Daemon::~Daemon() { shutdown(); }
+
+void Daemon::ep_add(int fd, uint32_t events, uint64_t t) {
+    struct epoll_event ev;
+    std::memset(&ev, 0, sizeof(ev));
+    ev.events = events;
+    ev.data.u64 = t;
+    if (epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &ev) != 0) OCM_WARN("epoll add fd %d: %s", fd, strerror(errno));
+}
+
+void Daemon::ep_mod(int fd, uint32_t events, uint64_t t) {
+    struct epoll_event ev;
+    std::memset(&ev, 0, sizeof(ev));
+    ev.events = events;
+    ev.data.u64 = t;
+    epoll_ctl(ep_, EPOLL_CTL_MOD, fd, &ev);
+}
+
+void Daemon::ep_del(int fd) { epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr); }
+
+NodeConfig Daemon::my_config() const {
+    NodeConfig c;
+    std::memset(&c, 0, sizeof(c));
+    gethostname(c.host, sizeof(c.host) - 1);
+    c.rank = rank_;
+    c.gpu = gpu_;
+    c.num_gpu = num_gpu_;
+    c.pid = (int32_t)getpid();
+    c.gpu_total = gpu_total_;
+    c.gpu_capacity = arena_ ? arena_->capacity(TIER_GPU) : 0;
+    c.host_capacity = arena_ ? arena_->capacity(TIER_HOST) : 0;
+    c.gpu_used = arena_ ? arena_->used(TIER_GPU) : 0;
+    c.host_used = arena_ ? arena_->used(TIER_HOST) : 0;
+    c.num_nodes = (uint32_t)n_;
+    c.num_apps = (uint32_t)apps_.size();
+    c.n_alloc = (uint32_t)n_alloc_;
+    c.n_free = (uint32_t)n_free_;
+    c.n_reclaimed = (uint32_t)n_reclaimed_;
+    c.n_spilled = (uint32_t)(gov_ ? gov_->spilled_count() : n_spilled_);
+    c.n_slabs = (uint32_t)(arena_ ? arena_->num_slabs() : 0);
+    return c;
+}
+
+int Daemon::init() {
+    std::string err;
+    if (parse_nodefile(cfg_.nodefile, &nf_, &err) != 0) {
+        OCM_ERR("%s", err.c_str());
+        return -1;
+    }
+    rank_ = resolve_rank(nf_, cfg_.rank, &err);
+    if (rank_ < 0) {
+        OCM_ERR("%s", err.c_str());
+        return -1;
+    }
+    n_ = nf_.size();
+    ns_ = cfg_.ns;
+    const NodeEntry &me = nf_.nodes[rank_];
+
+    // ---- GPU discovery ----
+    int ndev = 0;
+    if (cfg_.gpu != -1) {
+        if (hipGetDeviceCount(&ndev) != hipSuccess) {
+            (void)hipGetLastError();
+            ndev = 0;
+        }
+    }
+    num_gpu_ = ndev;
+    if (cfg_.gpu >= 0)
+        gpu_ = cfg_.gpu;
+    else if (cfg_.gpu == -2 && me.gpu >= 0)
+        gpu_ = me.gpu;
+    else if (cfg_.gpu == -2 && ndev > 0)
+        gpu_ = rank_ % ndev;
+    else
+        gpu_ = -1;
+    if (gpu_ >= ndev) {
+        OCM_ERR("gpu %d requested but only %d visible", gpu_, ndev);
+        return -1;
+    }
+    ArenaConfig ac;
+    ac.gpu = gpu_;
+    ac.slab_bytes = cfg_.slab_bytes;
+    ac.zero_on_alloc = cfg_.zero_on_alloc;
+    if (gpu_ >= 0) {
+        size_t free_b = 0, total_b = 0;
+        (void)hipSetDevice(gpu_);
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+            OCM_ERR("hipMemGetInfo failed on gpu %d", gpu_);
+            return -1;
+        }
+        gpu_total_ = total_b;
+        ac.gpu_capacity = cfg_.gpu_capacity ? cfg_.gpu_capacity : (uint64_t)((double)free_b * cfg_.gpu_fraction);
+    }
+    int local_daemons = 0;
+    for (auto &e : nf_.nodes) local_daemons += (e.dns == me.dns);
+    ac.host_capacity = cfg_.host_capacity
+                           ? cfg_.host_capacity
+                           : (uint64_t)((double)mem_available() * cfg_.host_fraction / std::max(1, local_daemons));
+    arena_ = std::make_unique<Arena>(ac);
+    if (rank_ == 0) gov_ = std::make_unique<Governor>(n_, cfg_.policy, cfg_.stripe_unit);
+    table_.assign(n_, NodeConfig{});
+    joined_.assign(n_, false);
+    peer_fd_.assign(n_, -1);
+
+    // ---- event loop plumbing ----
+    ep_ = epoll_create1(EPOLL_CLOEXEC);
+    sigset_t mask;
+    sigemptyset(&mask);
+    sigaddset(&mask, SIGINT);
+    sigaddset(&mask, SIGTERM);
+    sigprocmask(SIG_BLOCK, &mask, nullptr);
+    signal(SIGPIPE, SIG_IGN);
+    sig_fd_ = signalfd(-1, &mask, SFD_CLOEXEC | SFD_NONBLOCK);
+    ep_add(sig_fd_, EPOLLIN, tag(T_SIGNAL, 0));
+
+    pmsg_cleanup(ns_);
+    if (box_.open_self(daemon_mailbox_name(rank_, ns_), kMsgBytes, 8, true) != 0) {
+        OCM_ERR("cannot open daemon mailbox: %s", last_error());
+        return -1;
+    }
+    ep_add(box_.fd(), EPOLLIN, tag(T_MBOX, 0));
+
+    listen_fd_ = tcp_listen(cfg_.bind_ip.empty() ? "0.0.0.0" : cfg_.bind_ip, me.ocm_port, 64);
+    if (listen_fd_ < 0) {
+        OCM_ERR("%s", last_error());
+        return -1;
+    }
+    set_nonblocking(listen_fd_, true);
+    ep_add(listen_fd_, EPOLLIN, tag(T_LISTEN, 0));
+
+    // Mesh: connect to every lower rank; higher ranks connect to us.
+    for (int r = 0; r < rank_; r++) {
+        const NodeEntry &ne = nf_.nodes[r];
+        int fd = tcp_connect(ne.ip, ne.ocm_port, cfg_.join_timeout_ms);
+        if (fd < 0) {
+            if (r == 0) {
+                OCM_ERR("cannot reach rank0 at %s:%d (start the master first)", ne.ip.c_str(), ne.ocm_port);
+                return -1;
+            }
+            OCM_WARN("rank %d unreachable; continuing without it", r);
+            continue;
+        }
+        Msg hello;
+        std::memset(&hello, 0, sizeof(hello));
+        hello.type = MSG_HELLO;
+        hello.src_rank = rank_;
+        hello.rank = rank_;
+        send_all(fd, &hello, sizeof(hello));
+        set_nonblocking(fd, true);
+        auto c = std::make_unique<Conn>();
+        c->fd = fd;
+        c->peer_rank = r;
+        peer_fd_[r] = fd;
+        ep_add(fd, EPOLLIN, tag(T_CONN, (uint64_t)fd));
+        conns_[fd] = std::move(c);
+    }
+    // Join: report our configuration to rank0 (reference notify_rank0, src/main.c:143-160).
+    Msg add;
+    std::memset(&add, 0, sizeof(add));
+    add.type = MSG_ADD_NODE;
+    add.status = MSG_REQUEST;
+    add.rank = rank_;
+    add.u.node = my_config();
+    send_rank(0, add);
+    OCM_INFO("ocmd rank %d/%d up: gpu %d (%d visible), hbm capacity %.1f GiB, host tier %.1f GiB, policy %s, ns %s",
+             rank_, n_, gpu_, num_gpu_, (double)arena_->capacity(TIER_GPU) / (1 << 30),
+             (double)arena_->capacity(TIER_HOST) / (1 << 30), policy_name(cfg_.policy), ns_.c_str());
+    return 0;
+}
+
+void Daemon::check_ready() {
+    if (ready_) return;
+    for (int r = 0; r < n_; r++)
+        if (!joined_[r]) return;
+    ready_ = true;
+    OCM_LOG("rank %d: mesh complete (%d nodes)", rank_, n_);
+    if (!cfg_.ready_file.empty()) {
+        std::string tmp = cfg_.ready_file + ".tmp";
+        std::ofstream f(tmp);
+        f << "{\"rank\": " << rank_ << ", \"gpu\": " << gpu_ << ", \"pid\": " << getpid() << ", \"nodes\": " << n_
+          << "}\n";
+        f.close();
+        rename(tmp.c_str(), cfg_.ready_file.c_str());
+    }
+}
+
+void Daemon::shutdown() {
+    if (ep_ < 0) return;
+    for (auto &kv : apps_) {
+        if (kv.second.pidfd >= 0) close(kv.second.pidfd);
+    }
+    apps_.clear();
+    for (auto &kv : conns_) close(kv.first);
+    conns_.clear();
+    if (listen_fd_ >= 0) close(listen_fd_);
+    listen_fd_ = -1;
+    box_.close_self(true);
+    arena_.reset();
+    if (sig_fd_ >= 0) close(sig_fd_);
+    sig_fd_ = -1;
+    close(ep_);
+    ep_ = -1;
+    if (!cfg_.ready_file.empty()) unlink(cfg_.ready_file.c_str());
+}
+
+int Daemon::run() {
+    if (init() != 0) {
+        shutdown();
+        return 1;
+    }
+    int rc = loop();
+    OCM_INFO("ocmd rank %d exiting (allocs %llu, frees %llu, reclaimed %llu)", rank_,
+             (unsigned long long)n_alloc_, (unsigned long long)n_free_, (unsigned long long)n_reclaimed_);
+    shutdown();
+    return rc;
+}
+
+int Daemon::loop() {
+    struct epoll_event evs[64];
+    while (!stop_) {
+        while (!self_q_.empty() && !stop_) {
+            Msg m = self_q_.front();
+            self_q_.pop_front();
+            handle_mesh_msg(m, -1);
+        }
+        if (stop_) break;
+        int n = epoll_wait(ep_, evs, 64, self_q_.empty() ? 1000 : 0);
+        sweep_timeouts();
+        if (n < 0) {
+            if (errno == EINTR) continue;
+            OCM_ERR("epoll_wait: %s", strerror(errno));
+            return 1;
+        }
+        for (int i = 0; i < n && !stop_; i++) {
+            const uint64_t t = evs[i].data.u64;
+            const uint32_t e = evs[i].events;
+            switch (tag_kind(t)) {
+            case T_MBOX: on_mailbox(); break;
+            case T_LISTEN: on_accept(); break;
+            case T_CONN:
+                if (e & (EPOLLIN | EPOLLHUP | EPOLLERR)) on_conn_readable((int)tag_id(t));
+                if ((e & EPOLLOUT) && conns_.count((int)tag_id(t))) on_conn_writable((int)tag_id(t));
+                break;
+            case T_PIDFD: on_pidfd((pid_t)tag_id(t)); break;
+            case T_APPMQ: on_app_writable((pid_t)tag_id(t)); break;
+            case T_SIGNAL: on_signal(); break;
+            default: break;
+            }
+        }
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------- sources
+
+void Daemon::on_signal() {
+    struct signalfd_siginfo si;
+    while (read(sig_fd_, &si, sizeof(si)) == (ssize_t)sizeof(si)) {
+        OCM_INFO("rank %d: signal %u, shutting down", rank_, si.ssi_signo);
+        stop_ = true;
+    }
+}
+
+void Daemon::on_mailbox() {
+    Msg m;
+    // Drain everything queued (the queue is small; senders block when it is full).
+    for (int i = 0; i < 64; i++) {
+        int rc = box_.recv(&m, 0);
+        if (rc != 1) break;
+        handle_app_msg(m);
+    }
+}
+
+void Daemon::on_accept() {
+    for (;;) {
+        int fd = tcp_accept(listen_fd_);
+        if (fd < 0) break;
+        set_nonblocking(fd, true);
+        auto c = std::make_unique<Conn>();
+        c->fd = fd;
+        ep_add(fd, EPOLLIN, tag(T_CONN, (uint64_t)fd));
+        conns_[fd] = std::move(c);
+    }
+}
+
+void Daemon::drop_conn(int fd) {
+    auto it = conns_.find(fd);
+    if (it == conns_.end()) return;
+    int r = it->second->peer_rank;
+    ep_del(fd);
+    close(fd);
+    conns_.erase(it);
+    if (r >= 0 && r < n_ && peer_fd_[r] == fd) {
+        peer_fd_[r] = -1;
+        peer_lost(r);
+    }
+}
+
+void Daemon::on_conn_readable(int fd) {
+    auto it = conns_.find(fd);
+    if (it == conns_.end()) return;
+    std::vector<std::vector<uint8_t>> recs;
+    int rc = conn_read_records(*it->second, kMsgBytes, recs);
+    for (auto &r : recs) {
+        Msg m;
+        std::memcpy(&m, r.data(), kMsgBytes);
+        handle_mesh_msg(m, fd);
+    }
+    if (rc != 0) drop_conn(fd);
+}
+
+void Daemon::on_conn_writable(int fd) {
+    auto it = conns_.find(fd);
+    if (it == conns_.end()) return;
+    if (conn_flush(*it->second) != 0) {
+        drop_conn(fd);
+        return;
+    }
+    if (!it->second->want_write) ep_mod(fd, EPOLLIN, tag(T_CONN, (uint64_t)fd));
+}
+
+void Daemon::on_pidfd(pid_t pid) {
+    OCM_INFO("rank %d: app %d exited without ocm_tini; reclaiming its memory", rank_, (int)pid);
+    app_disconnect(pid, true);
+}
+
+void Daemon::on_app_writable(pid_t pid) {
+    auto it = apps_.find(pid);
+    if (it == apps_.end()) return;
+    App &a = it->second;
+    while (!a.backlog.empty()) {
+        int rc = box_.send(a.mbox, &a.backlog.front(), 0);
+        if (rc != 1) break;
+        a.backlog.pop_front();
+    }
+    if (a.backlog.empty() && a.watching_out) {
+        ep_del(a.mqfd);
+        a.watching_out = false;
+    }
+}
+
+// ---------------------------------------------------------------- routing
+
+void Daemon::send_rank(int r, Msg &m) {
+    m.src_rank = rank_;
+    if (r == rank_) {
+        self_q_.push_back(m);
+        return;
+    }
+    if (r < 0 || r >= n_ || peer_fd_[r] < 0) {
+        OCM_WARN("rank %d: no link to rank %d for %s", rank_, r, msg_type_str(m.type));
+        // Bounce the request back as a local failure so the origin can answer the app.
+        if (m.status == MSG_REQUEST && (m.type == MSG_REQ_ALLOC || m.type == MSG_DO_ALLOC || m.type == MSG_DO_FREE ||
+                                        m.type == MSG_STATS)) {
+            Msg f = m;
+            f.status = MSG_RESPONSE;
+            f.err = EHOSTDOWN;
+            f.src_rank = r;
+            if (f.type == MSG_DO_ALLOC && rank_ == 0 && f.rank != rank_) {
+                send_rank(f.rank, f);
+                return;
+            }
+            if (f.type == MSG_REQ_ALLOC) f.type = MSG_DO_ALLOC;
+            self_q_.push_back(f);
+        }
+        return;
+    }
+    int fd = peer_fd_[r];
+    Conn &c = *conns_[fd];
+    if (conn_write(c, &m, sizeof(m)) != 0) {
+        drop_conn(fd);
+        return;
+    }
+    if (c.want_write) ep_mod(fd, EPOLLIN | EPOLLOUT, tag(T_CONN, (uint64_t)fd));
+}
+
+void Daemon::send_app(pid_t pid, const Msg &m) {
+    auto it = apps_.find(pid);
+    if (it == apps_.end()) return;
+    App &a = it->second;
+    if (a.backlog.empty()) {
+        int rc = box_.send(a.mbox, &m, 0);
+        if (rc == 1) return;
+        if (rc < 0) {
+            OCM_WARN("send to app %d failed: %s", (int)pid, last_error());
+            return;
+        }
+    }
+    a.backlog.push_back(m);
+    if (!a.watching_out && a.mqfd >= 0) {
+        ep_add(a.mqfd, EPOLLOUT, tag(T_APPMQ, (uint64_t)pid));
+        a.watching_out = true;
+    }
+}
+
+// ---------------------------------------------------------------- app messages
+
+void Daemon::handle_app_msg(Msg &m) {
+    OCM_LOG("rank %d <- app %d: %s", rank_, m.pid, msg_type_str(m.type));
+    if (m.type != MSG_CONNECT && m.type != MSG_SHUTDOWN && !apps_.count(m.pid)) {
+        OCM_WARN("rank %d: %s from unknown app %d ignored", rank_, msg_type_str(m.type), m.pid);
+        return;
+    }
+    switch (m.type) {
+    case MSG_CONNECT: app_connect(m); break;
+    case MSG_DISCONNECT: app_disconnect(m.pid, false); break;
+    case MSG_REQ_ALLOC: app_req_alloc(m); break;
+    case MSG_REQ_FREE: app_req_free(m); break;
+    case MSG_STATS: app_stats(m); break;
+    case MSG_PING: {
+        Msg r = m;
+        r.status = MSG_RESPONSE;
+        r.type = MSG_RELEASE_APP;
+        send_app(m.pid, r);
+        break;
+    }
+    case MSG_SHUTDOWN: stop_ = true; break;
+    default: OCM_WARN("rank %d: unexpected app message %s", rank_, msg_type_str(m.type)); break;
+    }
+}
+
+void Daemon::app_connect(const Msg &m) {
+    pid_t pid = m.pid;
+    if (apps_.count(pid)) app_disconnect(pid, false);
+    App a;
+    a.pid = pid;
+    a.mbox = app_mailbox_name(pid, ns_);
+    if (box_.attach(a.mbox, true) != 0) {
+        OCM_WARN("rank %d: cannot attach mailbox of app %d: %s", rank_, (int)pid, last_error());
+        return;
+    }
+    a.mqfd = box_.peer_fd(a.mbox);
+    a.pidfd = pidfd_open_compat(pid);
+    if (a.pidfd >= 0) ep_add(a.pidfd, EPOLLIN, tag(T_PIDFD, (uint64_t)pid));
+    apps_[pid] = std::move(a);
+    Msg r;
+    std::memset(&r, 0, sizeof(r));
+    r.type = MSG_CONNECT_CONFIRM;
+    r.status = MSG_RESPONSE;
+    r.pid = pid;
+    r.rank = rank_;
+    r.seq = m.seq;
+    r.u.node = my_config();
+    r.err = ready_ ? 0 : EAGAIN;
+    send_app(pid, r);
+}
+
+void Daemon::app_disconnect(pid_t pid, bool crashed) {
+    auto it = apps_.find(pid);
+    if (it == apps_.end()) return;
+    // Reclaim whatever the app still holds (reference README:68-69 left this a TODO).
+    std::vector<uint64_t> mine;
+    for (auto &kv : origin_allocs_)
+        if (kv.second.pid == pid) mine.push_back(kv.first);
+    for (uint64_t id : mine) {
+        start_free(id, 0, 0);
+        n_reclaimed_++;
+    }
+    for (auto &kv : pending_)
+        if (kv.second.pid == pid) kv.second.pid = 0;  // finish silently, then reclaim
+    App &a = it->second;
+    if (a.watching_out && a.mqfd >= 0) ep_del(a.mqfd);
+    if (a.pidfd >= 0) {
+        ep_del(a.pidfd);
+        close(a.pidfd);
+    }
+    box_.detach(a.mbox);
+    if (crashed) mq_unlink(a.mbox.c_str());
+    apps_.erase(it);
+    OCM_LOG("rank %d: app %d detached (%zu allocations reclaimed)", rank_, (int)pid, mine.size());
+}
+
+void Daemon::app_req_alloc(Msg &m) {
+    const AllocReq &req = m.u.req;
+    if (req.bytes == 0) {
+        Msg r = m;
+        r.type = MSG_RELEASE_APP;
+        r.status = MSG_RESPONSE;
+        r.err = EINVAL;
+        send_app(m.pid, r);
+        return;
+    }
+    if (!is_remote_kind(req.kind)) {
+        // Local kinds: the app allocates the memory itself (malloc / hipMalloc);
+        // the daemon only records it. No rank0 round trip on this path.
+        uint64_t id = (1ull << 63) | ((uint64_t)rank_ << 40) | (++local_ids_);
+        OriginAlloc oa;
+        oa.pid = m.pid;
+        oa.remote = false;
+        oa.bytes = req.bytes;
+        origin_allocs_[id] = oa;
+        n_alloc_++;
+        Msg r;
+        std::memset(&r, 0, sizeof(r));
+        r.type = MSG_RELEASE_APP;
+        r.status = MSG_RESPONSE;
+        r.pid = m.pid;
+        r.rank = rank_;
+        r.seq = m.seq;
+        r.u.region.alloc_id = id;
+        r.u.region.bytes = req.bytes;
+        r.u.region.tier = (uint16_t)(req.kind == OCM_LOCAL_GPU ? TIER_GPU : TIER_HOST);
+        r.u.region.owner_rank = rank_;
+        r.u.region.orig_rank = rank_;
+        r.u.region.owner_gpu = gpu_;
+        r.u.region.n_extents = 0;
+        send_app(m.pid, r);
+        return;
+    }
+    Pending p;
+    p.seq = next_seq();
+    p.pid = m.pid;
+    p.type = MSG_REQ_ALLOC;
+    p.kind = req.kind;
+    p.total_bytes = req.bytes;
+    p.awaiting.insert(0);
+    p.app_seq = m.seq;
+    p.t0_ms = now_ms();
+    pending_[p.seq] = p;
+    Msg f = m;
+    f.type = MSG_REQ_ALLOC;
+    f.status = MSG_REQUEST;
+    f.rank = rank_;
+    f.seq = p.seq;
+    f.u.req.orig_rank = rank_;
+    f.u.req.app_pid = m.pid;
+    send_rank(0, f);
+}
+
+void Daemon::app_req_free(Msg &m) {
+    const uint64_t id = m.u.req.alloc_id;
+    auto it = origin_allocs_.find(id);
+    if (it == origin_allocs_.end() || it->second.pid != m.pid) {
+        Msg r = m;
+        r.type = MSG_RELEASE_APP;
+        r.status = MSG_RESPONSE;
+        r.err = ENOENT;
+        send_app(m.pid, r);
+        return;
+    }
+    if (!it->second.remote) {
+        origin_allocs_.erase(it);
+        n_free_++;
+        Msg r = m;
+        r.type = MSG_RELEASE_APP;
+        r.status = MSG_RESPONSE;
+        r.err = 0;
+        send_app(m.pid, r);
+        return;
+    }
+    start_free(id, m.pid, m.seq);
+}
+
+void Daemon::app_stats(Msg &m) {
+    const int target = m.u.req.remote_rank;
+    if (target >= 0 && target != rank_) {
+        Pending p;
+        p.seq = next_seq();
+        p.pid = m.pid;
+        p.type = MSG_STATS;
+        p.app_seq = m.seq;
+        p.t0_ms = now_ms();
+        p.awaiting.insert(target);
+        pending_[p.seq] = p;
+        Msg f = m;
+        f.status = MSG_REQUEST;
+        f.rank = rank_;
+        f.seq = p.seq;
+        send_rank(target, f);
+        return;
+    }
+    Msg r;
+    std::memset(&r, 0, sizeof(r));
+    r.type = MSG_RELEASE_APP;
+    r.status = MSG_RESPONSE;
+    r.pid = m.pid;
+    r.rank = rank_;
+    r.seq = m.seq;
+    r.u.node = my_config();
+    send_app(m.pid, r);
+}
+
+// ---------------------------------------------------------------- mesh messages
+
+void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
+    OCM_LOG("rank %d <- rank %d: %s/%s seq %llu", rank_, m.src_rank, msg_type_str(m.type), msg_status_str(m.status),
+            (unsigned long long)m.seq);
+    switch (m.type) {
+    case MSG_HELLO: {
+        auto it = conns_.find(from_fd);
+        if (it != conns_.end() && m.src_rank >= 0 && m.src_rank < n_) {
+            it->second->peer_rank = m.src_rank;
+            if (peer_fd_[m.src_rank] >= 0 && peer_fd_[m.src_rank] != from_fd) drop_conn(peer_fd_[m.src_rank]);
+            peer_fd_[m.src_rank] = from_fd;
+        }
+        break;
+    }
+    case MSG_ADD_NODE:
+        if (rank_ == 0) r0_add_node(m.u.node);
+        break;
+    case MSG_NODE_TABLE: {
+        const NodeConfig &c = m.u.node;
+        if (c.rank >= 0 && c.rank < n_) {
+            table_[c.rank] = c;
+            joined_[c.rank] = true;
+            check_ready();
+        }
+        break;
+    }
+    case MSG_REQ_ALLOC:
+        if (rank_ == 0) r0_req_alloc(m);
+        break;
+    case MSG_PLACE_FAIL:
+        if (rank_ == 0) r0_place_fail(m);
+        break;
+    case MSG_DO_ALLOC:
+        if (m.status == MSG_REQUEST)
+            owner_do_alloc(m);
+        else
+            origin_do_alloc_resp(m);
+        break;
+    case MSG_DO_FREE:
+        if (m.status == MSG_REQUEST)
+            owner_do_free(m);
+        else
+            origin_do_free_resp(m);
+        break;
+    case MSG_FREED:
+        if (rank_ == 0 && gov_) gov_->release(m.u.region.alloc_id);
+        break;
+    case MSG_STATS:
+        if (m.status == MSG_REQUEST) {
+            Msg r = m;
+            r.status = MSG_RESPONSE;
+            r.u.node = my_config();
+            send_rank(m.rank, r);
+        } else {
+            auto it = pending_.find(m.seq);
+            if (it == pending_.end()) break;
+            Msg r = m;
+            r.type = MSG_RELEASE_APP;
+            r.status = MSG_RESPONSE;
+            r.pid = it->second.pid;
+            r.seq = it->second.app_seq;
+            if (it->second.pid) send_app(it->second.pid, r);
+            pending_.erase(it);
+        }
+        break;
+    case MSG_SHUTDOWN: stop_ = true; break;
+    case MSG_PING:
+        if (m.status == MSG_REQUEST) {
+            Msg r = m;
+            r.status = MSG_RESPONSE;
+            send_rank(m.src_rank, r);
+        }
+        break;
+    default: OCM_WARN("rank %d: unexpected mesh message %s", rank_, msg_type_str(m.type)); break;
+    }
+}
+
+void Daemon::r0_add_node(const NodeConfig &cfg) {
+    if (cfg.rank < 0 || cfg.rank >= n_) return;
+    gov_->add_node(cfg);
+    table_[cfg.rank] = cfg;
+    joined_[cfg.rank] = true;
+    // Fan the directory out: the newcomer gets the whole table, everybody else the newcomer.
+    for (int r = 0; r < n_; r++) {
+        if (!joined_[r]) continue;
+        Msg t;
+        std::memset(&t, 0, sizeof(t));
+        t.type = MSG_NODE_TABLE;
+        t.status = MSG_RESPONSE;
+        t.rank = 0;
+        if (r == cfg.rank) {
+            for (int k = 0; k < n_; k++) {
+                if (!joined_[k] || k == 0) continue;  // rank0 learns from itself below
+                t.u.node = table_[k];
+                if (r != 0) send_rank(r, t);
+            }
+            if (r != 0) {
+                t.u.node = my_config();
+                send_rank(r, t);
+            }
+        } else if (r != 0) {
+            t.u.node = cfg;
+            send_rank(r, t);
+        }
+    }
+    if (cfg.rank == 0) table_[0] = my_config();
+    check_ready();
+}
+
+void Daemon::r0_req_alloc(Msg &m) {
+    PlaceRequest pr;
+    pr.orig_rank = m.u.req.orig_rank;
+    pr.remote_rank = m.u.req.remote_rank;
+    pr.bytes = m.u.req.bytes;
+    pr.flags = m.u.req.flags;
+    pr.stripe_width = m.u.req.stripe_width;
+    pr.stripe_unit = m.u.req.stripe_unit;
+    pr.remote = true;
+    pr.app_pid = m.u.req.app_pid;
+    Placement p = gov_->place(pr);
+    if (p.err) {
+        Msg r;
+        std::memset(&r, 0, sizeof(r));
+        r.type = MSG_DO_ALLOC;
+        r.status = MSG_RESPONSE;
+        r.rank = m.rank;
+        r.seq = m.seq;
+        r.err = p.err;
+        r.u.region.n_extents = 0;
+        send_rank(m.rank, r);
+        return;
+    }
+    for (size_t i = 0; i < p.extents.size(); i++) {
+        const PlacedExtent &e = p.extents[i];
+        Msg d;
+        std::memset(&d, 0, sizeof(d));
+        d.type = MSG_DO_ALLOC;
+        d.status = MSG_REQUEST;
+        d.pid = m.pid;
+        d.rank = m.rank;  // origin daemon: responses go there
+        d.seq = m.seq;
+        Region &rg = d.u.region;
+        rg.alloc_id = p.alloc_id;
+        rg.bytes = e.bytes;
+        rg.stripe_unit = p.stripe_unit;
+        rg.owner_rank = e.owner;
+        rg.orig_rank = m.rank;
+        rg.tier = (uint16_t)e.tier;
+        rg.flags = e.spilled ? REGION_SPILLED : 0;
+        rg.extent_idx = (uint16_t)i;
+        rg.n_extents = (uint16_t)p.extents.size();
+        send_rank(e.owner, d);
+    }
+}
+
+void Daemon::r0_place_fail(Msg &m) {
+    Region rg = m.u.region;
+    PlacedExtent e;
+    if (gov_->replace_extent(rg.alloc_id, rg.extent_idx, rg.owner_rank, &e)) {
+        Msg d = m;
+        d.type = MSG_DO_ALLOC;
+        d.status = MSG_REQUEST;
+        d.err = 0;
+        d.u.region.owner_rank = e.owner;
+        d.u.region.tier = (uint16_t)e.tier;
+        d.u.region.flags = e.spilled ? REGION_SPILLED : 0;
+        OCM_LOG("re-placing alloc %llu extent %d on rank %d tier %u", (unsigned long long)rg.alloc_id,
+                rg.extent_idx, e.owner, e.tier);
+        send_rank(e.owner, d);
+        return;
+    }
+    Msg r = m;
+    r.type = MSG_DO_ALLOC;
+    r.status = MSG_RESPONSE;
+    r.err = ENOMEM;
+    send_rank(m.rank, r);
+}
+
+void Daemon::owner_do_alloc(Msg &m) {
+    Region rg = m.u.region;
+    int err = arena_->alloc(rg.tier, rg.bytes, &rg);
+    if (err) {
+        OCM_LOG("rank %d: DO_ALLOC %llu bytes tier %u failed (%d)", rank_, (unsigned long long)rg.bytes, rg.tier, err);
+        Msg f = m;
+        f.type = MSG_PLACE_FAIL;
+        f.status = MSG_REQUEST;
+        f.err = err;
+        f.u.region.owner_rank = rank_;
+        send_rank(0, f);
+        return;
+    }
+    rg.owner_rank = rank_;
+    OwnedExtent oe;
+    oe.slab_id = rg.slab_id;
+    oe.offset = rg.offset;
+    oe.tier = rg.tier;
+    oe.orig_rank = rg.orig_rank;
+    oe.bytes = rg.bytes;
+    owned_[{rg.alloc_id, (int)rg.extent_idx}] = oe;
+    if (rg.flags & REGION_SPILLED) n_spilled_++;
+    Msg r = m;
+    r.status = MSG_RESPONSE;
+    r.err = 0;
+    r.u.region = rg;
+    send_rank(m.rank, r);
+}
+
+void Daemon::owner_do_free(Msg &m) {
+    const Region &rg = m.u.region;
+    auto it = owned_.find({rg.alloc_id, (int)rg.extent_idx});
+    int err = ENOENT;
+    if (it != owned_.end()) {
+        err = arena_->free(it->second.slab_id, it->second.offset);
+        owned_.erase(it);
+    }
+    Msg r = m;
+    r.status = MSG_RESPONSE;
+    r.err = err;
+    send_rank(m.rank, r);
+}
+
+void Daemon::origin_do_alloc_resp(Msg &m) {
+    auto it = pending_.find(m.seq);
+    if (it == pending_.end()) {
+        // Origin gave up (e.g. peer loss) but the owner allocated: give it back.
+        if (!m.err && m.u.region.alloc_id) {
+            Msg f;
+            std::memset(&f, 0, sizeof(f));
+            f.type = MSG_DO_FREE;
+            f.status = MSG_REQUEST;
+            f.rank = rank_;
+            f.seq = 0;
+            f.u.region = m.u.region;
+            send_rank(m.u.region.owner_rank, f);
+        }
+        return;
+    }
+    Pending &p = it->second;
+    const Region &rg = m.u.region;
+    if (p.expect == 0) {
+        // First response fixes the extent count (0 when rank0 refused the request).
+        p.expect = rg.n_extents ? rg.n_extents : 1;
+        p.extents.assign(p.expect, Region{});
+        p.have.assign(p.expect, false);
+        p.awaiting.clear();
+    }
+    if (m.err) p.err = p.err ? p.err : m.err;
+    if (rg.n_extents == 0) {
+        // rank0 refused: nothing was placed.
+        p.got = p.expect;
+    } else if (rg.extent_idx < p.expect && !p.have[rg.extent_idx]) {
+        p.have[rg.extent_idx] = true;
+        p.got++;
+        if (!m.err) p.extents[rg.extent_idx] = rg;
+        p.alloc_id = rg.alloc_id;
+    }
+    if (p.got >= p.expect) finish_alloc(p);
+}
+
+void Daemon::finish_alloc(Pending &p) {
+    const uint64_t seq = p.seq;
+    const uint64_t app_seq = p.app_seq;
+    const pid_t pid = p.pid;
+    if (p.err) {
+        // Roll back the extents that did get memory.
+        for (int i = 0; i < p.expect; i++) {
+            if (!p.have[i] || p.extents[i].alloc_id == 0) continue;
+            Msg f;
+            std::memset(&f, 0, sizeof(f));
+            f.type = MSG_DO_FREE;
+            f.status = MSG_REQUEST;
+            f.rank = rank_;
+            f.seq = 0;
+            f.u.region = p.extents[i];
+            send_rank(p.extents[i].owner_rank, f);
+        }
+        if (p.alloc_id) {
+            Msg fr;
+            std::memset(&fr, 0, sizeof(fr));
+            fr.type = MSG_FREED;
+            fr.u.region.alloc_id = p.alloc_id;
+            send_rank(0, fr);
+        }
+        if (pid && apps_.count(pid)) {
+            Msg r;
+            std::memset(&r, 0, sizeof(r));
+            r.type = MSG_RELEASE_APP;
+            r.status = MSG_RESPONSE;
+            r.pid = pid;
+            r.rank = rank_;
+            r.seq = app_seq;
+            r.err = p.err;
+            send_app(pid, r);
+        }
+        pending_.erase(seq);
+        return;
+    }
+    OriginAlloc oa;
+    oa.pid = pid;
+    oa.remote = true;
+    oa.bytes = p.total_bytes;
+    oa.extents = p.extents;
+    const uint64_t id = p.alloc_id;
+    origin_allocs_[id] = oa;
+    n_alloc_++;
+    pending_.erase(seq);
+    if (!pid || !apps_.count(pid)) {
+        // The app vanished while we were allocating.
+        start_free(id, 0, 0);
+        n_reclaimed_++;
+        return;
+    }
+    // Header + one EXTENT record per extent (a 160-byte record holds one region).
+    Msg h;
+    std::memset(&h, 0, sizeof(h));
+    h.type = MSG_RELEASE_APP;
+    h.status = MSG_RESPONSE;
+    h.pid = pid;
+    h.rank = rank_;
+    h.seq = app_seq;
+    h.u.region = oa.extents[0];
+    h.u.region.bytes = oa.bytes;  // header carries the total
+    send_app(pid, h);
+    for (size_t i = 0; i < oa.extents.size(); i++) {
+        Msg e;
+        std::memset(&e, 0, sizeof(e));
+        e.type = MSG_EXTENT;
+        e.status = MSG_RESPONSE;
+        e.pid = pid;
+        e.rank = rank_;
+        e.seq = app_seq;
+        e.u.region = oa.extents[i];
+        send_app(pid, e);
+    }
+}
+
+void Daemon::start_free(uint64_t alloc_id, pid_t reply_pid, uint64_t reply_seq) {
+    auto it = origin_allocs_.find(alloc_id);
+    if (it == origin_allocs_.end()) return;
+    OriginAlloc oa = it->second;
+    origin_allocs_.erase(it);
+    if (!oa.remote) {
+        n_free_++;
+        return;
+    }
+    Pending p;
+    p.seq = next_seq();
+    p.pid = reply_pid;
+    p.type = MSG_REQ_FREE;
+    p.alloc_id = alloc_id;
+    p.app_seq = reply_seq;
+    p.t0_ms = now_ms();
+    p.expect = (int)oa.extents.size();
+    for (auto &e : oa.extents) p.awaiting.insert(e.owner_rank);
+    pending_[p.seq] = p;
+    for (auto &e : oa.extents) {
+        Msg f;
+        std::memset(&f, 0, sizeof(f));
+        f.type = MSG_DO_FREE;
+        f.status = MSG_REQUEST;
+        f.rank = rank_;
+        f.seq = p.seq;
+        f.u.region = e;
+        send_rank(e.owner_rank, f);
+    }
+}
+
+void Daemon::origin_do_free_resp(Msg &m) {
+    if (m.seq == 0) return;  // rollback frees need no answer
+    auto it = pending_.find(m.seq);
+    if (it == pending_.end()) return;
+    Pending &p = it->second;
+    p.got++;
+    // A dead owner's memory is gone already: count it as freed.
+    if (m.err && m.err != ENOENT && m.err != EHOSTDOWN) p.err = m.err;
+    if (p.got < p.expect) return;
+    n_free_++;
+    Msg fr;
+    std::memset(&fr, 0, sizeof(fr));
+    fr.type = MSG_FREED;
+    fr.u.region.alloc_id = p.alloc_id;
+    send_rank(0, fr);
+    if (p.pid && apps_.count(p.pid)) {
+        Msg r;
+        std::memset(&r, 0, sizeof(r));
+        r.type = MSG_RELEASE_APP;
+        r.status = MSG_RESPONSE;
+        r.pid = p.pid;
+        r.rank = rank_;
+        r.seq = p.app_seq;
+        r.err = p.err;
+        send_app(p.pid, r);
+    }
+    pending_.erase(it);
+}
+
+void Daemon::fail_pending_on(int rank) {
+    std::vector<uint64_t> dead;
+    for (auto &kv : pending_)
+        if (kv.second.awaiting.count(rank)) dead.push_back(kv.first);
+    for (uint64_t s : dead) {
+        auto it = pending_.find(s);
+        if (it == pending_.end()) continue;
+        Pending &p = it->second;
+        if (p.type == MSG_REQ_ALLOC) {
+            p.err = EHOSTDOWN;
+            if (p.expect == 0) {
+                p.expect = 1;
+                p.have.assign(1, false);
+                p.extents.assign(1, Region{});
+            }
+            finish_alloc(p);
+        } else {
+            if (p.pid && apps_.count(p.pid)) {
+                Msg r;
+                std::memset(&r, 0, sizeof(r));
+                r.type = MSG_RELEASE_APP;
+                r.status = MSG_RESPONSE;
+                r.pid = p.pid;
+                r.rank = rank_;
+                r.seq = p.app_seq;
+                r.err = EHOSTDOWN;
+                send_app(p.pid, r);
+            }
+            pending_.erase(it);
+        }
+    }
+}
+
+void Daemon::peer_lost(int rank) {
+    OCM_WARN("rank %d: lost link to rank %d", rank_, rank);
+    if (gov_) gov_->mark_dead(rank);
+    fail_pending_on(rank);
+    // Extents we own for allocations that originated at the dead daemon stay
+    // mapped by its apps; keep them until those apps' reclaim would have
+    // happened, i.e. reclaim now only when no app can still reach them.
+    std::vector<std::pair<uint64_t, int>> orphan;
+    for (auto &kv : owned_)
+        if (kv.second.orig_rank == rank) orphan.push_back(kv.first);
+    for (auto &k : orphan) {
+        arena_->free(owned_[k].slab_id, owned_[k].offset);
+        owned_.erase(k);
+        n_reclaimed_++;
+    }
+}
+
+void Daemon::sweep_timeouts() {
+    if (pending_.empty()) return;
+    const long now = now_ms();
+    std::vector<uint64_t> late;
+    for (auto &kv : pending_)
+        if (kv.second.t0_ms && now - kv.second.t0_ms > request_timeout_ms_) late.push_back(kv.first);
+    for (uint64_t s : late) {
+        auto it = pending_.find(s);
+        if (it == pending_.end()) continue;
+        Pending &p = it->second;
+        OCM_WARN("rank %d: request seq %llu (%s) timed out", rank_, (unsigned long long)s, msg_type_str(p.type));
+        if (p.type == MSG_REQ_ALLOC) {
+            p.err = ETIMEDOUT;
+            if (p.expect == 0) {
+                p.expect = 1;
+                p.have.assign(1, false);
+                p.extents.assign(1, Region{});
+            }
+            finish_alloc(p);
+        } else {
+            if (p.pid && apps_.count(p.pid)) {
+                Msg r;
+                std::memset(&r, 0, sizeof(r));
+                r.type = MSG_RELEASE_APP;
+                r.status = MSG_RESPONSE;
+                r.pid = p.pid;
+                r.rank = rank_;
+                r.seq = p.app_seq;
+                r.err = ETIMEDOUT;
+                send_app(p.pid, r);
+            }
+            pending_.erase(it);
+        }
+    }
+}
+
+}  // namespace ocm

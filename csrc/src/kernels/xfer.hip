@@ -1,0 +1,306 @@
+// gfx950 one-sided transfer kernels (put/get over xGMI, HBM and pinned host).
+//
+// See ocm/xfer.h for the contract. Two variants:
+//   XFER_REG  register-staged: each lane keeps UNROLL 16-byte loads in flight,
+//             then issues UNROLL 16-byte stores (nontemporal on the destination).
+//   XFER_LDS  LDS-DMA staged: each wave streams its 8 KiB slice of a tile into a
+//             wave-private LDS double buffer with global_load_lds_dwordx4 while
+//             it drains the previous tile from LDS (ds_read_b128 + global store).
+//             Wave-private buffers need no workgroup barrier; ordering is the
+//             issuing wave's own counted vmcnt (guide: "Pipelining across barriers").
+// Work decomposition: the striped address space is cut into tiles aligned to
+// the tile size (a power of two <= stripe unit), so a tile never crosses a
+// stripe unit and maps to one contiguous range on both sides. Workgroups
+// grid-stride over tiles; per-tile extent/offset math runs once per workgroup.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+
+#include "ocm/xfer.h"
+
+namespace ocm {
+
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 8;                                    // 8 x 16 B in flight per lane
+constexpr uint32_t kTileShift = 15;                           // 32 KiB tiles = 256 lanes x 16 B x 8
+constexpr int kWaves = kThreads / 64;
+constexpr int kWaveSlice = (1 << kTileShift) / kWaves;        // 8 KiB per wave per tile
+constexpr int kChunksPerWave = kWaveSlice / 1024;             // 8 glds (1 KiB each) per wave per tile
+
+template <bool NT>
+__device__ __forceinline__ void store16(u32x4 *p, u32x4 v) {
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+__device__ __forceinline__ u32x4 load16(const u32x4 *p) { return __builtin_nontemporal_load(p); }
+
+// Block-cooperative copy of n bytes (n <= one tile is the common case, any n works).
+template <bool NT>
+__device__ __forceinline__ void span_copy(char *__restrict__ dst, const char *__restrict__ src, uint64_t n) {
+    const int tid = threadIdx.x;
+    uint64_t head = (16u - ((uintptr_t)dst & 15u)) & 15u;
+    if (head > n) head = n;
+    if ((uint64_t)tid < head) dst[tid] = src[tid];
+    dst += head;
+    src += head;
+    n -= head;
+    if (((uintptr_t)src & 15u) == 0) {
+        const uint64_t nv = n >> 4;
+        const u32x4 *s = reinterpret_cast<const u32x4 *>(src);
+        u32x4 *d = reinterpret_cast<u32x4 *>(dst);
+        uint64_t base = 0;
+        for (; base + (uint64_t)kThreads * kUnroll <= nv; base += (uint64_t)kThreads * kUnroll) {
+            u32x4 v[kUnroll];
+#pragma unroll
+            for (int k = 0; k < kUnroll; k++) v[k] = load16(s + base + (uint64_t)k * kThreads + tid);
+#pragma unroll
+            for (int k = 0; k < kUnroll; k++) store16<NT>(d + base + (uint64_t)k * kThreads + tid, v[k]);
+        }
+        for (uint64_t i = base + tid; i < nv; i += kThreads) store16<NT>(d + i, load16(s + i));
+        const uint64_t tail = n & 15u;
+        if ((uint64_t)tid < tail) dst[(nv << 4) + tid] = src[(nv << 4) + tid];
+    } else {
+        // Source and destination disagree mod 16: byte loop (rare; unaligned user offsets).
+        for (uint64_t i = tid; i < n; i += kThreads) dst[i] = src[i];
+    }
+}
+
+struct TileSpan {
+    char *dst;
+    const char *src;
+    uint64_t n;
+};
+
+__device__ __forceinline__ TileSpan tile_span(const XferArgs &a, uint64_t ti, uint64_t first_tile) {
+    const uint64_t tile = 1ull << a.tile_shift;
+    const uint64_t r0 = a.rem_off, r1 = a.rem_off + a.len;
+    const uint64_t lo = first_tile + (ti << a.tile_shift);
+    const uint64_t ts = lo > r0 ? lo : r0;
+    const uint64_t te = (lo + tile) < r1 ? (lo + tile) : r1;
+    char *rp;
+    if (a.n_ext == 1) {
+        rp = a.ext[0] + ts;
+    } else {
+        // Stripe unit u of the address space lives on extent u % n at (u / n) * unit.
+        const uint64_t unit_mask = (1ull << a.unit_shift) - 1;
+        const uint32_t u = (uint32_t)(ts >> a.unit_shift);
+        const uint32_t e = u % a.n_ext;
+        const uint64_t eoff = ((uint64_t)(u / a.n_ext) << a.unit_shift) | (ts & unit_mask);
+        rp = a.ext[e] + eoff;
+    }
+    char *lp = a.lin + (ts - r0);
+    TileSpan s;
+    s.dst = a.put ? rp : lp;
+    s.src = a.put ? lp : rp;
+    s.n = te - ts;
+    return s;
+}
+
+template <bool NT>
+__global__ __launch_bounds__(kThreads) void xfer_reg_kernel(XferArgs a) {
+    const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
+    const uint64_t first = a.rem_off & ~tile_mask;
+    const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;
+    for (uint64_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
+        TileSpan s = tile_span(a, ti, first);
+        span_copy<NT>(s.dst, s.src, s.n);
+    }
+}
+
+// ---- LDS-DMA variant ----
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void glob_void;
+
+__device__ __forceinline__ bool full_aligned(const TileSpan &s) {
+    return s.n == (1ull << kTileShift) && (((uintptr_t)s.dst | (uintptr_t)s.src) & 15u) == 0;
+}
+
+// Issue this wave's 8 x 1 KiB LDS-DMA loads of a full tile into `buf`.
+__device__ __forceinline__ void stage_tile(const char *src, char *buf, int wave, int lane) {
+    const char *g = src + (size_t)wave * kWaveSlice + (size_t)lane * 16;
+    char *l = buf + (size_t)wave * kWaveSlice;  // wave-uniform LDS base; lane offset is implicit
+#pragma unroll
+    for (int c = 0; c < kChunksPerWave; c++)
+        __builtin_amdgcn_global_load_lds((glob_void *)(g + c * 1024), (lds_void *)(l + c * 1024), 16, 0, 0);
+}
+
+template <bool NT>
+__device__ __forceinline__ void drain_tile(char *dst, const char *buf, int wave, int lane) {
+    const char *l = buf + (size_t)wave * kWaveSlice + (size_t)lane * 16;
+    char *g = dst + (size_t)wave * kWaveSlice + (size_t)lane * 16;
+    u32x4 v[kChunksPerWave];
+#pragma unroll
+    for (int c = 0; c < kChunksPerWave; c++) v[c] = *reinterpret_cast<const u32x4 *>(l + c * 1024);
+#pragma unroll
+    for (int c = 0; c < kChunksPerWave; c++) store16<NT>(reinterpret_cast<u32x4 *>(g + c * 1024), v[c]);
+}
+
+template <bool NT>
+__global__ __launch_bounds__(kThreads) void xfer_lds_kernel(XferArgs a) {
+    // One LDS array (guide: a second __shared__ object can de-pipeline glds).
+    __shared__ __attribute__((aligned(16))) char lds[2 * (1 << kTileShift)];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
+    const uint64_t first = a.rem_off & ~tile_mask;
+    const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;
+    uint64_t ti = blockIdx.x;
+    if (ti >= ntiles) return;
+    TileSpan cur = tile_span(a, ti, first);
+    bool cur_staged = full_aligned(cur);
+    if (cur_staged) stage_tile(cur.src, lds, wave, lane);
+    int slot = 0;
+    for (;;) {
+        const uint64_t nt = ti + gridDim.x;
+        TileSpan nxt;
+        bool nxt_staged = false;
+        if (nt < ntiles) {
+            nxt = tile_span(a, nt, first);
+            nxt_staged = full_aligned(nxt);
+            if (nxt_staged) stage_tile(nxt.src, lds + (slot ^ 1) * (1 << kTileShift), wave, lane);
+        }
+        if (cur_staged) {
+            // Retire this wave's loads of `cur`, leaving the next tile's 8 in flight.
+            if (nxt_staged)
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            drain_tile<NT>(cur.dst, lds + slot * (1 << kTileShift), wave, lane);
+        } else {
+            span_copy<NT>(cur.dst, cur.src, cur.n);
+        }
+        if (nt >= ntiles) break;
+        ti = nt;
+        cur = nxt;
+        cur_staged = nxt_staged;
+        slot ^= 1;
+    }
+}
+
+int env_int(const char *k, int dflt) {
+    const char *v = std::getenv(k);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
+int g_num_cus = 0;
+
+int num_cus() {
+    if (g_num_cus) return g_num_cus;
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+        g_num_cus = n;
+    else
+        g_num_cus = 256;
+    return g_num_cus;
+}
+
+}  // namespace
+
+XferTuning xfer_tuning_from_env() {
+    XferTuning t;
+    const char *v = std::getenv("OCM_XFER_VARIANT");
+    if (v && (!std::strcmp(v, "lds") || !std::strcmp(v, "2"))) t.variant = XFER_LDS;
+    if (v && (!std::strcmp(v, "reg") || !std::strcmp(v, "1"))) t.variant = XFER_REG;
+    t.max_blocks = env_int("OCM_XFER_BLOCKS", 0);
+    t.nontemporal = env_int("OCM_XFER_NT", 1) != 0;
+    return t;
+}
+
+hipError_t xfer_launch(const XferArgs &in, const XferTuning &t, hipStream_t stream) {
+    if (in.len == 0) return hipSuccess;
+    if (in.n_ext < 1 || in.n_ext > (uint32_t)kXferMaxExtents) return hipErrorInvalidValue;
+    XferArgs a = in;
+    a.tile_shift = kTileShift;
+    if (a.n_ext > 1) {
+        if (a.unit_shift < kTileShift) a.tile_shift = a.unit_shift;  // tile must not cross a stripe unit
+        if (a.unit_shift < 4) return hipErrorInvalidValue;
+    }
+    const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
+    const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - (a.rem_off & ~tile_mask)) >> a.tile_shift;
+    int variant = t.variant;
+    if (variant == XFER_AUTO) variant = XFER_REG;
+    if (a.tile_shift != kTileShift) variant = XFER_REG;  // LDS path is built for 32 KiB tiles
+    // Enough workgroups to cover every CU several times over, never more than tiles.
+    int cap = t.max_blocks > 0 ? t.max_blocks : num_cus() * (variant == XFER_LDS ? 2 : 4);
+    const unsigned grid = (unsigned)(ntiles < (uint64_t)cap ? ntiles : (uint64_t)cap);
+    if (variant == XFER_LDS) {
+        if (t.nontemporal)
+            hipLaunchKernelGGL(xfer_lds_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a);
+        else
+            hipLaunchKernelGGL(xfer_lds_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a);
+    } else {
+        if (t.nontemporal)
+            hipLaunchKernelGGL(xfer_reg_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a);
+        else
+            hipLaunchKernelGGL(xfer_reg_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t xfer_copy(void *dst, const void *src, uint64_t bytes, const XferTuning &t, hipStream_t stream) {
+    XferArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.lin = const_cast<char *>(static_cast<const char *>(src));
+    a.ext[0] = static_cast<char *>(dst);
+    a.rem_off = 0;
+    a.len = bytes;
+    a.n_ext = 1;
+    a.put = 1;
+    return xfer_launch(a, t, stream);
+}
+
+// ---- verification patterns (benchmarks and tests check data without a host round trip) ----
+
+__device__ __host__ __forceinline__ uint32_t pattern_word(uint64_t i, uint32_t seed) {
+    uint64_t x = (i + 1) * 0x9E3779B97F4A7C15ull ^ ((uint64_t)seed << 32 | seed);
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    return (uint32_t)x;
+}
+
+namespace {
+
+__global__ __launch_bounds__(kThreads) void fill_kernel(uint32_t *p, uint64_t words, uint64_t first, uint32_t seed) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < words; i += (uint64_t)gridDim.x * kThreads)
+        p[i] = pattern_word(first + i, seed);
+}
+
+__global__ __launch_bounds__(kThreads) void check_kernel(const uint32_t *p, uint64_t words, uint64_t first, uint32_t seed,
+                                                         unsigned long long *bad) {
+    unsigned long long local = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < words; i += (uint64_t)gridDim.x * kThreads)
+        local += p[i] != pattern_word(first + i, seed);
+    if (local) atomicAdd(bad, local);
+}
+
+}  // namespace
+
+hipError_t pattern_fill(void *p, uint64_t words, uint64_t first_word, uint32_t seed, hipStream_t stream) {
+    if (!words) return hipSuccess;
+    const uint64_t want = (words + kThreads - 1) / kThreads;
+    const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
+    hipLaunchKernelGGL(fill_kernel, dim3(grid), dim3(kThreads), 0, stream, static_cast<uint32_t *>(p), words, first_word, seed);
+    return hipGetLastError();
+}
+
+hipError_t pattern_check(const void *p, uint64_t words, uint64_t first_word, uint32_t seed, unsigned long long *bad_dev,
+                         hipStream_t stream) {
+    if (!words) return hipSuccess;
+    const uint64_t want = (words + kThreads - 1) / kThreads;
+    const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
+    hipLaunchKernelGGL(check_kernel, dim3(grid), dim3(kThreads), 0, stream, static_cast<const uint32_t *>(p), words,
+                       first_word, seed, bad_dev);
+    return hipGetLastError();
+}
+
+uint32_t pattern_word_host(uint64_t i, uint32_t seed) { return pattern_word(i, seed); }
+
+}  // namespace ocm

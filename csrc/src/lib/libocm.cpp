@@ -1,0 +1,931 @@
+// libocm: the application library behind oncillamem.h.
+//
+// Parity with reference src/lib.c (struct lib_alloc, ocm_init/tini/alloc/free,
+// accessors, ocm_copy, ocm_copy_onesided). MI355X design:
+//   * control: one mailbox RPC to the local ocmd (seq-matched, blocking
+//     mq_timedreceive — no spinning), multi-record replies for striped pairs;
+//   * registration: remote HBM extents are imported once per slab with
+//     hipIpcOpenMemHandle (lazy peer access) and cached; host-tier extents are
+//     mmap'ed from the owner's memfd and hipHostRegister'ed (device-mapped);
+//   * data: one-sided put/get run the gfx950 transfer kernel (ocm/xfer.h) on a
+//     per-process non-blocking stream; host-tier legs use the DMA engines
+//     (hipMemcpyAsync); completion = stream sync, or ocm_wait() for the async form.
+// Reference defects deliberately not reproduced: inverted ocm_is_remote
+// (src/lib.c:461), NULL deref before check in ocm_free (:357-359), stub
+// copy_in/out (:491-499), swapped GPU->RMA offsets (:654).
+#include <fcntl.h>
+#include <hip/hip_runtime_api.h>
+#include <sys/mman.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "oncillamem.h"
+#include "ocm/log.h"
+#include "ocm/msg.h"
+#include "ocm/pmsg.h"
+#include "ocm/xfer.h"
+
+using namespace ocm;
+
+namespace {
+
+enum Loc { LOC_HOST = 0, LOC_PINNED = 1, LOC_DEVICE = 2 };
+
+struct Extent {
+    Region r;
+    char *dptr = nullptr;  // device-usable address of the extent start (nullptr: none)
+    char *hptr = nullptr;  // host address (host tier only)
+};
+
+}  // namespace
+
+struct lib_alloc {
+    enum ocm_kind kind;
+    uint64_t alloc_id = 0;
+    void *local = nullptr;
+    size_t local_bytes = 0;
+    Loc loc = LOC_HOST;
+    bool remote = false;
+    size_t remote_bytes = 0;
+    uint64_t stripe_unit = 0;
+    std::vector<Extent> ext;
+    bool all_gpu = false;
+    bool any_gpu = false;
+    bool async_pending = false;
+};
+
+namespace {
+
+struct SlabKey {
+    int owner;
+    uint32_t tier;
+    uint32_t slab;
+    bool operator<(const SlabKey &o) const {
+        return owner != o.owner ? owner < o.owner : tier != o.tier ? tier < o.tier : slab < o.slab;
+    }
+};
+
+struct Mapping {
+    char *dbase = nullptr;
+    char *hbase = nullptr;
+    uint64_t bytes = 0;
+    uint8_t handle[kHandleBytes] = {};
+    int refs = 0;
+    bool dedicated = false;
+    bool registered = false;
+};
+
+struct State {
+    std::recursive_mutex mu;
+    bool inited = false;
+    pid_t pid = 0;
+    std::string ns, daemon_mbox;
+    Mailbox box;
+    NodeConfig daemon{};
+    int daemon_rank = 0;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint64_t seq = 0;
+    std::map<SlabKey, Mapping> imports;
+    std::set<lib_alloc *> allocs;
+    XferTuning tuning;
+    bool host_engine_kernel = false;
+    int rpc_timeout_ms = 60000;
+};
+
+State &S() {
+    static State *s = new State();  // never destroyed: safe at process exit
+    return *s;
+}
+
+int env_int(const char *k, int dflt) {
+    const char *v = std::getenv(k);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    bool active = false;
+    explicit DeviceGuard(int dev) {
+        if (dev < 0) return;
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
+            (void)hipSetDevice(dev);
+            active = true;
+        }
+    }
+    ~DeviceGuard() {
+        if (active) (void)hipSetDevice(prev);
+    }
+};
+
+long now_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1000L + ts.tv_nsec / 1000000L;
+}
+
+Msg new_msg(uint32_t type) {
+    Msg m;
+    std::memset(&m, 0, sizeof(m));
+    m.type = type;
+    m.status = MSG_REQUEST;
+    m.pid = S().pid;
+    m.rank = S().daemon_rank;
+    m.src_rank = -1;
+    return m;
+}
+
+// Send a request and wait for the reply carrying the same seq.
+int rpc(Msg &req, Msg *reply, int timeout_ms) {
+    State &s = S();
+    req.seq = ++s.seq;
+    if (s.box.send(s.daemon_mbox, &req, timeout_ms) != 1) OCM_FAIL(-1, "mailbox send to daemon failed");
+    const long deadline = now_ms() + timeout_ms;
+    for (;;) {
+        long left = deadline - now_ms();
+        if (left <= 0) OCM_FAIL(-1, "daemon did not answer %s within %d ms", msg_type_str(req.type), timeout_ms);
+        int rc = s.box.recv(reply, (int)std::min<long>(left, 1000));
+        if (rc < 0) return -1;
+        if (rc == 0) continue;
+        if (reply->seq == req.seq && reply->type != MSG_EXTENT) return 0;
+        OCM_LOG("dropping stale reply %s seq %llu", msg_type_str(reply->type), (unsigned long long)reply->seq);
+    }
+}
+
+int recv_seq(Msg *m, uint64_t seq, uint32_t type, int timeout_ms) {
+    const long deadline = now_ms() + timeout_ms;
+    for (;;) {
+        long left = deadline - now_ms();
+        if (left <= 0) OCM_FAIL(-1, "timed out waiting for %s", msg_type_str(type));
+        int rc = S().box.recv(m, (int)std::min<long>(left, 1000));
+        if (rc < 0) return -1;
+        if (rc == 1 && m->seq == seq && m->type == type) return 0;
+    }
+}
+
+bool is_pair(enum ocm_kind k) { return k == OCM_REMOTE_GPU || k == OCM_REMOTE_RDMA || k == OCM_REMOTE_RMA; }
+
+// ---------------------------------------------------------------- import cache
+
+int import_extent(Extent &e) {
+    State &s = S();
+    const Region &r = e.r;
+    SlabKey key{r.owner_rank, r.tier, r.slab_id};
+    auto it = s.imports.find(key);
+    if (it != s.imports.end() && std::memcmp(it->second.handle, r.handle, kHandleBytes) != 0) {
+        // Same id, different export: the owner restarted. Drop the stale mapping.
+        Mapping &m = it->second;
+        if (r.tier == TIER_GPU && m.dbase) (void)hipIpcCloseMemHandle(m.dbase);
+        if (m.registered) (void)hipHostUnregister(m.hbase);
+        if (m.hbase) munmap(m.hbase, m.bytes);
+        s.imports.erase(it);
+        it = s.imports.end();
+    }
+    if (it == s.imports.end()) {
+        Mapping m;
+        m.bytes = r.slab_bytes;
+        m.dedicated = (r.flags & REGION_DEDICATED) != 0;
+        std::memcpy(m.handle, r.handle, kHandleBytes);
+        if (r.tier == TIER_GPU) {
+            if (s.device < 0) OCM_FAIL(-1, "remote HBM extent but this process has no GPU");
+            DeviceGuard g(s.device);
+            hipIpcMemHandle_t h;
+            std::memcpy(&h, r.handle, sizeof(h));
+            void *p = nullptr;
+            hipError_t err = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+            if (err != hipSuccess) OCM_FAIL(-1, "hipIpcOpenMemHandle(owner %d slab %u): %s", r.owner_rank, r.slab_id, hipGetErrorString(err));
+            m.dbase = static_cast<char *>(p);
+        } else {
+            char path[kHandleBytes + 1];
+            std::memcpy(path, r.handle, kHandleBytes);
+            path[kHandleBytes] = 0;
+            int fd = open(path, O_RDWR | O_CLOEXEC);
+            if (fd < 0) OCM_FAIL(-1, "open host-tier slab %s: %s", path, strerror(errno));
+            void *p = mmap(nullptr, r.slab_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            close(fd);
+            if (p == MAP_FAILED) OCM_FAIL(-1, "mmap host-tier slab: %s", strerror(errno));
+            m.hbase = static_cast<char *>(p);
+            m.dbase = m.hbase;
+            if (s.device >= 0) {
+                DeviceGuard g(s.device);
+                hipError_t err = hipHostRegister(p, r.slab_bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+                if (err == hipSuccess) {
+                    void *dp = nullptr;
+                    if (hipHostGetDevicePointer(&dp, p, 0) == hipSuccess) m.dbase = static_cast<char *>(dp);
+                    m.registered = true;
+                } else {
+                    (void)hipGetLastError();
+                    OCM_WARN("hipHostRegister of host-tier slab failed: %s (DMA from pageable memory)", hipGetErrorString(err));
+                }
+            }
+        }
+        it = s.imports.emplace(key, m).first;
+    }
+    it->second.refs++;
+    e.dptr = it->second.dbase + r.offset;
+    e.hptr = it->second.hbase ? it->second.hbase + r.offset : nullptr;
+    return 0;
+}
+
+void release_extent(const Extent &e, bool force) {
+    State &s = S();
+    SlabKey key{e.r.owner_rank, e.r.tier, e.r.slab_id};
+    auto it = s.imports.find(key);
+    if (it == s.imports.end()) return;
+    Mapping &m = it->second;
+    if (--m.refs > 0 && !force) return;
+    if (!m.dedicated && !force) return;  // shared slabs stay mapped for reuse
+    DeviceGuard g(s.device);
+    if (e.r.tier == TIER_GPU && m.dbase) (void)hipIpcCloseMemHandle(m.dbase);
+    if (m.registered) (void)hipHostUnregister(m.hbase);
+    if (m.hbase) munmap(m.hbase, m.bytes);
+    s.imports.erase(it);
+}
+
+// ---------------------------------------------------------------- copy engine
+
+struct Seg {
+    int ext;
+    uint64_t ext_off;
+    uint64_t lin_off;
+    uint64_t len;
+};
+
+// Split [rem_off, rem_off+len) of a striped buffer into contiguous pieces.
+void segments(const lib_alloc *a, uint64_t rem_off, uint64_t len, std::vector<Seg> &out) {
+    out.clear();
+    const int n = (int)a->ext.size();
+    if (n == 1 || a->stripe_unit == 0) {
+        out.push_back({0, rem_off, 0, len});
+        return;
+    }
+    const uint64_t unit = a->stripe_unit;
+    uint64_t pos = rem_off, done = 0;
+    while (done < len) {
+        const uint64_t u = pos / unit, within = pos % unit;
+        const uint64_t take = std::min(unit - within, len - done);
+        out.push_back({(int)(u % n), (u / n) * unit + within, done, take});
+        pos += take;
+        done += take;
+    }
+}
+
+int log2_exact(uint64_t v) {
+    if (v == 0 || (v & (v - 1))) return -1;
+    return __builtin_ctzll(v);
+}
+
+int sync_stream() {
+    State &s = S();
+    if (!s.stream) return 0;
+    DeviceGuard g(s.device);
+    hipError_t e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess) OCM_FAIL(-1, "stream sync: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// One-sided transfer between the linear buffer `lin` (location `lloc`) and the
+// remote half of `a` at striped offset `rem_off`.
+int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async) {
+    State &s = S();
+    if (len == 0) return 0;
+    std::vector<Seg> segs;
+    if (s.device < 0) {
+        segments(a, rem_off, len, segs);
+        for (auto &g : segs) {
+            char *r = a->ext[g.ext].hptr + g.ext_off;
+            if (put)
+                std::memcpy(r, lin + g.lin_off, g.len);
+            else
+                std::memcpy(lin + g.lin_off, r, g.len);
+        }
+        return 0;
+    }
+    DeviceGuard guard(s.device);
+    const bool lin_dev = lloc == LOC_DEVICE;
+    const bool use_kernel = lin_dev && (a->any_gpu || s.host_engine_kernel);
+    hipError_t err = hipSuccess;
+    if (use_kernel) {
+        XferArgs x;
+        std::memset(&x, 0, sizeof(x));
+        x.lin = lin;
+        for (size_t i = 0; i < a->ext.size(); i++) x.ext[i] = a->ext[i].dptr;
+        x.n_ext = (uint32_t)a->ext.size();
+        x.rem_off = rem_off;
+        x.len = len;
+        x.put = put ? 1 : 0;
+        if (x.n_ext > 1) {
+            int sh = log2_exact(a->stripe_unit);
+            if (sh < 0) OCM_FAIL(-1, "stripe unit %llu is not a power of two", (unsigned long long)a->stripe_unit);
+            x.unit_shift = (uint32_t)sh;
+        }
+        err = xfer_launch(x, s.tuning, s.stream);
+    } else {
+        segments(a, rem_off, len, segs);
+        for (auto &g : segs) {
+            const Extent &e = a->ext[g.ext];
+            char *r = (lloc == LOC_DEVICE || e.r.tier == TIER_GPU) ? e.dptr : e.hptr;
+            r += g.ext_off;
+            if (lloc != LOC_DEVICE && e.r.tier != TIER_GPU) {
+                // host <-> host tier: the CPU is the fastest engine.
+                if (put)
+                    std::memcpy(r, lin + g.lin_off, g.len);
+                else
+                    std::memcpy(lin + g.lin_off, r, g.len);
+                continue;
+            }
+            err = put ? hipMemcpyAsync(r, lin + g.lin_off, g.len, hipMemcpyDefault, s.stream)
+                      : hipMemcpyAsync(lin + g.lin_off, r, g.len, hipMemcpyDefault, s.stream);
+            if (err != hipSuccess) break;
+        }
+    }
+    if (err != hipSuccess) OCM_FAIL(-1, "transfer launch failed: %s", hipGetErrorString(err));
+    if (async) {
+        a->async_pending = true;
+        return 0;
+    }
+    return sync_stream();
+}
+
+// Copy between two process-local buffers.
+int copy_local(void *dst, Loc dl, const void *src, Loc sl, size_t n) {
+    State &s = S();
+    if (n == 0) return 0;
+    if (dl != LOC_DEVICE && sl != LOC_DEVICE) {
+        std::memcpy(dst, src, n);
+        return 0;
+    }
+    DeviceGuard g(s.device);
+    hipError_t e;
+    if (dl == LOC_DEVICE && sl == LOC_DEVICE)
+        e = xfer_copy(dst, src, n, s.tuning, s.stream);
+    else
+        e = hipMemcpyAsync(dst, src, n, hipMemcpyDefault, s.stream);
+    if (e != hipSuccess) OCM_FAIL(-1, "local copy failed: %s", hipGetErrorString(e));
+    return sync_stream();
+}
+
+Loc pointer_loc(const void *p) {
+    State &s = S();
+    if (s.device < 0 || !p) return LOC_HOST;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return LOC_HOST;
+    }
+    if (at.type == hipMemoryTypeDevice) return LOC_DEVICE;
+    if (at.type == hipMemoryTypeHost) return LOC_PINNED;
+    return LOC_HOST;
+}
+
+int free_local_half(lib_alloc *a) {
+    State &s = S();
+    if (!a->local) return 0;
+    if (a->loc == LOC_DEVICE) {
+        DeviceGuard g(s.device);
+        (void)hipFree(a->local);
+    } else if (a->loc == LOC_PINNED) {
+        DeviceGuard g(s.device);
+        (void)hipHostFree(a->local);
+    } else {
+        std::free(a->local);
+    }
+    a->local = nullptr;
+    return 0;
+}
+
+int alloc_local_half(lib_alloc *a, size_t bytes, Loc want) {
+    State &s = S();
+    a->local_bytes = bytes;
+    if (bytes == 0) return 0;
+    if (want != LOC_HOST && s.device < 0) want = LOC_HOST;
+    if (want == LOC_DEVICE) {
+        DeviceGuard g(s.device);
+        hipError_t e = hipMalloc(&a->local, bytes);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            OCM_FAIL(-1, "hipMalloc(%zu) for local half: %s", bytes, hipGetErrorString(e));
+        }
+    } else if (want == LOC_PINNED) {
+        DeviceGuard g(s.device);
+        hipError_t e = hipHostMalloc(&a->local, bytes, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            OCM_FAIL(-1, "hipHostMalloc(%zu) for local half: %s", bytes, hipGetErrorString(e));
+        }
+    } else {
+        if (posix_memalign(&a->local, 4096, bytes) != 0) OCM_FAIL(-1, "host allocation of %zu bytes failed", bytes);
+    }
+    a->loc = want;
+    return 0;
+}
+
+}  // namespace
+
+// ================================================================ C API
+
+extern "C" {
+
+int ocm_init(void) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (s.inited) return 0;
+    s.pid = getpid();
+    s.ns = pmsg_namespace();
+    const char *dr = std::getenv("OCM_DAEMON_RANK");
+    const char *lr = std::getenv("LOCAL_RANK");
+    s.daemon_rank = dr && *dr ? std::atoi(dr) : (lr && *lr ? std::atoi(lr) : 0);
+    s.daemon_mbox = daemon_mailbox_name(s.daemon_rank, s.ns);
+    s.rpc_timeout_ms = env_int("OCM_RPC_TIMEOUT_MS", 60000);
+    const int connect_ms = env_int("OCM_CONNECT_TIMEOUT_MS", 10000);
+    if (s.box.open_self(app_mailbox_name(s.pid, s.ns), kMsgBytes, 8, true) != 0) return -1;
+    // Attach to the daemon mailbox, retrying while it starts (reference: 10 x 10 ms).
+    long deadline = now_ms() + connect_ms;
+    while (s.box.attach(s.daemon_mbox, false) != 0) {
+        if (now_ms() > deadline) {
+            s.box.close_self(true);
+            OCM_FAIL(-1, "no ocmd mailbox %s (is the daemon running?)", s.daemon_mbox.c_str());
+        }
+        usleep(10000);
+    }
+    Msg reply;
+    for (;;) {
+        Msg c = new_msg(MSG_CONNECT);
+        if (rpc(c, &reply, std::max(1000, connect_ms)) != 0) {
+            s.box.close_self(true);
+            return -1;
+        }
+        if (reply.err != EAGAIN) break;
+        if (now_ms() > deadline) {
+            s.box.close_self(true);
+            OCM_FAIL(-1, "daemon mesh not ready after %d ms", connect_ms);
+        }
+        usleep(20000);  // mesh still joining
+    }
+    s.daemon = reply.u.node;
+    // Pick the GPU this process copies on: OCM_GPU, else the daemon's GPU.
+    int ndev = 0;
+    if (!std::getenv("OCM_NO_GPU") && hipGetDeviceCount(&ndev) != hipSuccess) {
+        (void)hipGetLastError();
+        ndev = 0;
+    }
+    const char *g = std::getenv("OCM_GPU");
+    int dev = g && *g ? std::atoi(g) : s.daemon.gpu;
+    if (dev < 0 && ndev > 0 && s.daemon.gpu >= 0) dev = 0;
+    s.device = (ndev > 0 && dev >= 0 && dev < ndev) ? dev : -1;
+    if (s.device >= 0) {
+        DeviceGuard guard(s.device);
+        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) {
+            (void)hipGetLastError();
+            OCM_FAIL(-1, "cannot create HIP stream on device %d", s.device);
+        }
+    }
+    s.tuning = xfer_tuning_from_env();
+    const char *he = std::getenv("OCM_HOST_ENGINE");
+    s.host_engine_kernel = he && !std::strcmp(he, "kernel");
+    s.inited = true;
+    OCM_LOG("attached to ocmd rank %d (gpu %d, %u nodes), copying on device %d", s.daemon_rank, s.daemon.gpu,
+            s.daemon.num_nodes, s.device);
+    return 0;
+}
+
+int ocm_tini(void) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!s.inited) return -1;
+    std::vector<lib_alloc *> left(s.allocs.begin(), s.allocs.end());
+    for (auto *a : left) ocm_free(a);
+    Msg d = new_msg(MSG_DISCONNECT);
+    s.box.send(s.daemon_mbox, &d, 1000);
+    for (auto &kv : s.imports) {
+        Mapping &m = kv.second;
+        DeviceGuard g(s.device);
+        if (kv.first.tier == TIER_GPU && m.dbase) (void)hipIpcCloseMemHandle(m.dbase);
+        if (m.registered) (void)hipHostUnregister(m.hbase);
+        if (m.hbase) munmap(m.hbase, m.bytes);
+    }
+    s.imports.clear();
+    if (s.stream) {
+        DeviceGuard g(s.device);
+        (void)hipStreamDestroy(s.stream);
+        s.stream = nullptr;
+    }
+    s.box.close_self(true);
+    s.inited = false;
+    return 0;
+}
+
+ocm_alloc_t ocm_alloc(ocm_alloc_param_t p) { return ocm_alloc_ex(p, nullptr); }
+
+ocm_alloc_t ocm_alloc_ex(ocm_alloc_param_t p, const struct ocm_alloc_ex_params *ex) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!s.inited) OCM_FAIL(nullptr, "ocm_alloc before ocm_init");
+    if (!p) OCM_FAIL(nullptr, "ocm_alloc: NULL parameters");
+    enum ocm_kind kind = p->kind;
+    if (kind == OCM_LOCAL_RMA || kind == OCM_LOCAL_RDMA) kind = OCM_LOCAL_HOST;
+    if (kind < OCM_LOCAL_HOST || kind > OCM_REMOTE_GPU) OCM_FAIL(nullptr, "ocm_alloc: invalid kind %d", (int)p->kind);
+    const bool pair = is_pair(kind);
+    if (kind == OCM_LOCAL_GPU && s.device < 0) OCM_FAIL(nullptr, "OCM_LOCAL_GPU requested but no GPU is available");
+    const uint64_t req_bytes = pair ? p->rem_alloc_bytes : p->local_alloc_bytes;
+    if (req_bytes == 0) OCM_FAIL(nullptr, "ocm_alloc: zero-byte request");
+
+    Msg m = new_msg(MSG_REQ_ALLOC);
+    m.u.req.orig_rank = s.daemon_rank;
+    m.u.req.remote_rank = ex ? ex->remote_rank : -1;
+    m.u.req.bytes = req_bytes;
+    m.u.req.kind = (uint32_t)kind;
+    m.u.req.flags = ex ? ex->flags : 0;
+    if (s.device < 0) m.u.req.flags |= OCM_ALLOC_HOST_TIER;  // a CPU-only app cannot map HBM
+    m.u.req.stripe_width = ex ? ex->stripe_width : 0;
+    m.u.req.stripe_unit = ex ? ex->stripe_unit : 0;
+    m.u.req.tier = (m.u.req.flags & OCM_ALLOC_HOST_TIER) ? TIER_HOST : TIER_GPU;
+    m.u.req.app_pid = s.pid;
+    if (m.u.req.stripe_unit && log2_exact(m.u.req.stripe_unit) < 12)
+        OCM_FAIL(nullptr, "stripe unit must be a power of two >= 4 KiB");
+    Msg r;
+    if (rpc(m, &r, s.rpc_timeout_ms) != 0) return nullptr;
+    if (r.type != MSG_RELEASE_APP) OCM_FAIL(nullptr, "unexpected reply %s", msg_type_str(r.type));
+    if (r.err) OCM_FAIL(nullptr, "ocm_alloc of %llu bytes failed: %s", (unsigned long long)req_bytes, strerror(r.err));
+
+    auto *a = new lib_alloc();
+    a->kind = kind;
+    a->alloc_id = r.u.region.alloc_id;
+    if (pair) {
+        a->remote = true;
+        a->remote_bytes = r.u.region.bytes;
+        a->stripe_unit = r.u.region.stripe_unit;
+        const int n = r.u.region.n_extents;
+        a->ext.resize(n);
+        bool ok = n >= 1 && n <= kMaxExtents;
+        for (int i = 0; ok && i < n; i++) {
+            Msg e;
+            if (recv_seq(&e, r.seq, MSG_EXTENT, s.rpc_timeout_ms) != 0) {
+                ok = false;
+                break;
+            }
+            const int idx = e.u.region.extent_idx;
+            if (idx >= n) {
+                ok = false;
+                break;
+            }
+            a->ext[idx].r = e.u.region;
+        }
+        for (int i = 0; ok && i < n; i++) ok = import_extent(a->ext[i]) == 0;
+        if (ok) {
+            a->all_gpu = a->any_gpu = false;
+            bool all = true;
+            for (auto &e : a->ext) {
+                all &= e.r.tier == TIER_GPU;
+                a->any_gpu |= e.r.tier == TIER_GPU;
+            }
+            a->all_gpu = all;
+            Loc want = kind == OCM_REMOTE_GPU ? LOC_DEVICE : LOC_PINNED;
+            ok = alloc_local_half(a, p->local_alloc_bytes, want) == 0;
+        }
+        if (!ok) {
+            std::string why = last_error();
+            for (auto &e : a->ext)
+                if (e.dptr || e.hptr) release_extent(e, false);
+            Msg f = new_msg(MSG_REQ_FREE);
+            f.u.req.alloc_id = a->alloc_id;
+            Msg fr;
+            rpc(f, &fr, s.rpc_timeout_ms);
+            free_local_half(a);
+            delete a;
+            set_last_error("%s", why.c_str());
+            return nullptr;
+        }
+    } else {
+        Loc want = kind == OCM_LOCAL_GPU ? LOC_DEVICE : LOC_HOST;
+        if (alloc_local_half(a, p->local_alloc_bytes, want) != 0) {
+            std::string why = last_error();
+            Msg f = new_msg(MSG_REQ_FREE);
+            f.u.req.alloc_id = a->alloc_id;
+            Msg fr;
+            rpc(f, &fr, s.rpc_timeout_ms);
+            delete a;
+            set_last_error("%s", why.c_str());
+            return nullptr;
+        }
+    }
+    if ((m.u.req.flags & OCM_ALLOC_ZERO) && a->local) {
+        if (a->loc == LOC_DEVICE) {
+            DeviceGuard g(s.device);
+            (void)hipMemsetAsync(a->local, 0, a->local_bytes, s.stream);
+            sync_stream();
+        } else {
+            std::memset(a->local, 0, a->local_bytes);
+        }
+    }
+    s.allocs.insert(a);
+    return a;
+}
+
+int ocm_free(ocm_alloc_t a) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!a || !s.allocs.count(a)) OCM_FAIL(-1, "ocm_free: unknown allocation");
+    if (a->async_pending) ocm_wait(a);
+    // Unmap dedicated remote slabs before the owner frees them.
+    for (auto &e : a->ext) release_extent(e, false);
+    free_local_half(a);
+    Msg f = new_msg(MSG_REQ_FREE);
+    f.u.req.alloc_id = a->alloc_id;
+    f.u.req.n_extents = (int32_t)a->ext.size();
+    Msg r;
+    int rc = rpc(f, &r, s.rpc_timeout_ms);
+    s.allocs.erase(a);
+    delete a;
+    if (rc != 0) return -1;
+    if (r.err) OCM_FAIL(-1, "ocm_free: %s", strerror(r.err));
+    return 0;
+}
+
+int ocm_localbuf(ocm_alloc_t a, void **buf, size_t *len) {
+    if (!a || !buf || !len) return -1;
+    *buf = a->local;
+    *len = a->local_bytes;
+    return 0;
+}
+
+bool ocm_is_remote(ocm_alloc_t a) { return a && a->remote; }
+
+enum ocm_kind ocm_alloc_kind(ocm_alloc_t a) { return a ? a->kind : (enum ocm_kind)0; }
+
+int ocm_remote_sz(ocm_alloc_t a, size_t *len) {
+    if (!a || !len || !a->remote) return -1;  // no remote buffer for local kinds
+    *len = a->remote_bytes;
+    return 0;
+}
+
+int ocm_copy_onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!a || !p) OCM_FAIL(-1, "ocm_copy_onesided: NULL argument");
+    if (!a->remote) OCM_FAIL(-1, "one-sided copy needs a remote pair (kind %d)", (int)a->kind);
+    // Bounds (reference src/rdma.c:55-59, src/lib.c:679): the local side is
+    // src_offset, the remote side dest_offset, for both directions.
+    if (p->bytes > a->local_bytes || p->src_offset + p->bytes > a->local_bytes)
+        OCM_FAIL(-1, "one-sided copy: local range [%llu,+%llu) exceeds %zu bytes", (unsigned long long)p->src_offset,
+                 (unsigned long long)p->bytes, a->local_bytes);
+    if (p->dest_offset + p->bytes > a->remote_bytes)
+        OCM_FAIL(-1, "one-sided copy: remote range [%llu,+%llu) exceeds %zu bytes", (unsigned long long)p->dest_offset,
+                 (unsigned long long)p->bytes, a->remote_bytes);
+    return xfer(a, p->op_flag != 0, static_cast<char *>(a->local) + p->src_offset, a->loc, p->dest_offset, p->bytes,
+                async);
+}
+
+int ocm_copy_onesided(ocm_alloc_t a, ocm_param_t p) { return ocm_copy_onesided_impl(a, p, false); }
+int ocm_copy_onesided_async(ocm_alloc_t a, ocm_param_t p) { return ocm_copy_onesided_impl(a, p, true); }
+
+int ocm_wait(ocm_alloc_t a) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (a) a->async_pending = false;
+    return sync_stream();
+}
+
+static bool range_ok(uint64_t off, uint64_t n, uint64_t cap) { return off <= cap && n <= cap - off; }
+
+int ocm_copy(ocm_alloc_t dst, ocm_alloc_t src, ocm_param_t p) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!dst || !src || !p) OCM_FAIL(-1, "ocm_copy: NULL argument");
+    // A read (op_flag == 0) is the write with the roles swapped (reference src/lib.c:511-515).
+    struct ocm_params q = *p;
+    if (!q.op_flag) {
+        std::swap(dst, src);
+        q.op_flag = 1;
+    }
+    const uint64_t n = q.bytes;
+    if (!src->remote && !dst->remote) {
+        if (!range_ok(q.src_offset, n, src->local_bytes) || !range_ok(q.dest_offset, n, dst->local_bytes))
+            OCM_FAIL(-1, "ocm_copy: range out of bounds");
+        return copy_local(static_cast<char *>(dst->local) + q.dest_offset, dst->loc,
+                          static_cast<char *>(src->local) + q.src_offset, src->loc, n);
+    }
+    if (!src->remote && dst->remote) {
+        // Stage into dst's local half, then one-sided write local[src_offset_2] -> remote[dest_offset_2].
+        if (!range_ok(q.src_offset, n, src->local_bytes) || !range_ok(q.dest_offset, n, dst->local_bytes) ||
+            !range_ok(q.src_offset_2, n, dst->local_bytes) || !range_ok(q.dest_offset_2, n, dst->remote_bytes))
+            OCM_FAIL(-1, "ocm_copy: range out of bounds");
+        if (copy_local(static_cast<char *>(dst->local) + q.dest_offset, dst->loc,
+                       static_cast<char *>(src->local) + q.src_offset, src->loc, n) != 0)
+            return -1;
+        return xfer(dst, true, static_cast<char *>(dst->local) + q.src_offset_2, dst->loc, q.dest_offset_2, n, false);
+    }
+    if (src->remote && !dst->remote) {
+        // One-sided read remote[dest_offset_2] -> src local[src_offset_2], then unstage.
+        if (!range_ok(q.src_offset_2, n, src->local_bytes) || !range_ok(q.dest_offset_2, n, src->remote_bytes) ||
+            !range_ok(q.src_offset, n, src->local_bytes) || !range_ok(q.dest_offset, n, dst->local_bytes))
+            OCM_FAIL(-1, "ocm_copy: range out of bounds");
+        if (xfer(src, false, static_cast<char *>(src->local) + q.src_offset_2, src->loc, q.dest_offset_2, n, false) != 0)
+            return -1;
+        return copy_local(static_cast<char *>(dst->local) + q.dest_offset, dst->loc,
+                          static_cast<char *>(src->local) + q.src_offset, src->loc, n);
+    }
+    // remote -> remote (not supported by the reference): direct, no staging.
+    if (!range_ok(q.src_offset, n, src->remote_bytes) || !range_ok(q.dest_offset, n, dst->remote_bytes))
+        OCM_FAIL(-1, "ocm_copy: range out of bounds");
+    std::vector<Seg> ss;
+    segments(src, q.src_offset, n, ss);
+    for (auto &g : ss) {
+        const Extent &e = src->ext[g.ext];
+        char *sp = (s.device >= 0 ? e.dptr : e.hptr) + g.ext_off;
+        Loc sl = (s.device >= 0 && (e.r.tier == TIER_GPU || e.dptr != e.hptr)) ? LOC_DEVICE : LOC_HOST;
+        if (s.device >= 0 && sl == LOC_DEVICE) {
+            if (xfer(dst, true, sp, LOC_DEVICE, q.dest_offset + g.lin_off, g.len, false) != 0) return -1;
+        } else {
+            if (xfer(dst, true, sp, LOC_HOST, q.dest_offset + g.lin_off, g.len, false) != 0) return -1;
+        }
+    }
+    return 0;
+}
+
+int ocm_copy_in(ocm_alloc_t dst, void *src) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!dst || !src) OCM_FAIL(-1, "ocm_copy_in: NULL argument");
+    const Loc sl = pointer_loc(src);
+    if (dst->remote) return xfer(dst, true, static_cast<char *>(src), sl, 0, dst->remote_bytes, false);
+    return copy_local(dst->local, dst->loc, src, sl, dst->local_bytes);
+}
+
+int ocm_copy_out(void *dst, ocm_alloc_t src) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!dst || !src) OCM_FAIL(-1, "ocm_copy_out: NULL argument");
+    const Loc dl = pointer_loc(dst);
+    if (src->remote) return xfer(src, false, static_cast<char *>(dst), dl, 0, src->remote_bytes, false);
+    return copy_local(dst, dl, src->local, src->loc, src->local_bytes);
+}
+
+int ocm_remote_info(ocm_alloc_t a, struct ocm_remote_info *info) {
+    if (!a || !info) return -1;
+    std::memset(info, 0, sizeof(*info));
+    info->alloc_id = a->alloc_id;
+    info->remote_bytes = a->remote_bytes;
+    info->stripe_unit = a->stripe_unit;
+    info->n_extents = (uint32_t)a->ext.size();
+    for (size_t i = 0; i < a->ext.size() && i < OCM_MAX_EXTENTS; i++) {
+        info->tier[i] = a->ext[i].r.tier;
+        info->owner_rank[i] = a->ext[i].r.owner_rank;
+        info->owner_gpu[i] = a->ext[i].r.owner_gpu;
+        info->extent_bytes[i] = a->ext[i].r.bytes;
+    }
+    return a->remote ? 0 : -1;
+}
+
+void *ocm_remotebuf(ocm_alloc_t a) {
+    if (!a || a->ext.size() != 1) return nullptr;
+    return S().device >= 0 ? a->ext[0].dptr : a->ext[0].hptr;
+}
+
+int ocm_stats(int rank, struct ocm_daemon_stats *out) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!s.inited || !out) return -1;
+    Msg m = new_msg(MSG_STATS);
+    m.u.req.remote_rank = rank;
+    Msg r;
+    if (rpc(m, &r, s.rpc_timeout_ms) != 0) return -1;
+    if (r.err) OCM_FAIL(-1, "stats from rank %d: %s", rank, strerror(r.err));
+    const NodeConfig &c = r.u.node;
+    std::memset(out, 0, sizeof(*out));
+    out->rank = c.rank;
+    out->gpu = c.gpu;
+    out->num_nodes = (int32_t)c.num_nodes;
+    out->num_apps = (int32_t)c.num_apps;
+    out->gpu_capacity = c.gpu_capacity;
+    out->gpu_used = c.gpu_used;
+    out->host_capacity = c.host_capacity;
+    out->host_used = c.host_used;
+    out->n_alloc = c.n_alloc;
+    out->n_free = c.n_free;
+    out->n_reclaimed = c.n_reclaimed;
+    out->n_spilled = c.n_spilled;
+    out->n_slabs = c.n_slabs;
+    return 0;
+}
+
+int ocm_rank(void) { return S().inited ? S().daemon_rank : -1; }
+int ocm_num_nodes(void) { return S().inited ? (int)S().daemon.num_nodes : -1; }
+int ocm_device(void) { return S().inited ? S().device : -1; }
+const char *ocm_last_error(void) { return last_error(); }
+
+// ---------------- internal hooks for tests and benchmarks (not part of the ABI) ----------------
+
+void ocm_x_layout(uint64_t out[8]) {
+    out[0] = sizeof(Msg);
+    out[1] = sizeof(struct ocm_params);
+    out[2] = sizeof(struct ocm_alloc_params);
+    out[3] = offsetof(Msg, u);
+    out[4] = sizeof(Region);
+    out[5] = sizeof(NodeConfig);
+    out[6] = sizeof(AllocReq);
+    out[7] = kHandleBytes;
+}
+
+// Striped transfer between raw device pointers on `device` (kernel numerics tests).
+int ocm_x_xfer(int device, void *lin, void **ext, int n_ext, uint64_t unit, uint64_t rem_off, uint64_t len, int put,
+               int variant, int blocks) {
+    if (n_ext < 1 || n_ext > kXferMaxExtents) return -1;
+    DeviceGuard g(device);
+    XferArgs x;
+    std::memset(&x, 0, sizeof(x));
+    x.lin = static_cast<char *>(lin);
+    for (int i = 0; i < n_ext; i++) x.ext[i] = static_cast<char *>(ext[i]);
+    x.n_ext = (uint32_t)n_ext;
+    x.rem_off = rem_off;
+    x.len = len;
+    x.put = (uint32_t)put;
+    if (n_ext > 1) {
+        int sh = log2_exact(unit);
+        if (sh < 4) return -1;
+        x.unit_shift = (uint32_t)sh;
+    }
+    XferTuning t = xfer_tuning_from_env();
+    if (variant) t.variant = variant;
+    if (blocks) t.max_blocks = blocks;
+    if (xfer_launch(x, t, nullptr) != hipSuccess) return -1;
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+// Time `iters` back-to-back device copies (seconds per copy, event-timed).
+double ocm_x_time_device_copy(int device, void *dst, const void *src, uint64_t bytes, int variant, int blocks,
+                              int nt, int iters) {
+    DeviceGuard g(device);
+    XferTuning t;
+    t.variant = variant;
+    t.max_blocks = blocks;
+    t.nontemporal = nt != 0;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)xfer_copy(dst, src, bytes, t, nullptr);  // warm
+    (void)hipEventRecord(e0, nullptr);
+    for (int i = 0; i < iters; i++) (void)xfer_copy(dst, src, bytes, t, nullptr);
+    (void)hipEventRecord(e1, nullptr);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return (double)ms / 1e3 / (iters > 0 ? iters : 1);
+}
+
+// Wall-clock seconds per blocking one-sided op, measured inside the library
+// (no Python in the loop): the sweep primitive of bench.py.
+double ocm_x_time_onesided(ocm_alloc_t a, ocm_param_t p, int iters) {
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < iters; i++)
+        if (ocm_copy_onesided(a, p) != 0) return -1.0;
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    double dt = (double)(t1.tv_sec - t0.tv_sec) + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-9;
+    return dt / (iters > 0 ? iters : 1);
+}
+
+// Fill / check the deterministic word pattern on device or host memory.
+// `words` 32-bit words starting at pattern index `first`; returns mismatches (check) or 0 / -1.
+long long ocm_x_pattern(void *p, uint64_t words, uint64_t first, uint32_t seed, int check) {
+    State &s = S();
+    Loc l = pointer_loc(p);
+    if (s.device < 0 || l == LOC_HOST) {
+        uint32_t *w = static_cast<uint32_t *>(p);
+        long long bad = 0;
+        for (uint64_t i = 0; i < words; i++) {
+            if (check)
+                bad += w[i] != pattern_word_host(first + i, seed);
+            else
+                w[i] = pattern_word_host(first + i, seed);
+        }
+        return bad;
+    }
+    DeviceGuard g(s.device);
+    if (!check) {
+        if (pattern_fill(p, words, first, seed, s.stream) != hipSuccess) return -1;
+        return sync_stream() == 0 ? 0 : -1;
+    }
+    unsigned long long *bad_dev = nullptr, bad = 0;
+    if (hipMalloc(&bad_dev, sizeof(bad)) != hipSuccess) return -1;
+    (void)hipMemsetAsync(bad_dev, 0, sizeof(bad), s.stream);
+    hipError_t e = pattern_check(p, words, first, seed, bad_dev, s.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&bad, bad_dev, sizeof(bad), hipMemcpyDeviceToHost, s.stream);
+    int rc = sync_stream();
+    (void)hipFree(bad_dev);
+    return (e == hipSuccess && rc == 0) ? (long long)bad : -1;
+}
+
+}  // extern "C"

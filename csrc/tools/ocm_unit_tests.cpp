@@ -1,0 +1,247 @@
+// Native unit tests (no daemon, no GPU): wire layout, nodefile, range
+// allocator, governor placement policies, stripe geometry, host-tier arena.
+// Prints one line per test and exits non-zero on the first failure.
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <random>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "oncillamem.h"
+#include "ocm/arena.h"
+#include "ocm/governor.h"
+#include "ocm/msg.h"
+#include "ocm/nodefile.h"
+#include "ocm/range_alloc.h"
+
+using namespace ocm;
+
+static int g_fail = 0;
+#define CHECK(c)                                                        \
+    do {                                                                \
+        if (!(c)) {                                                     \
+            fprintf(stderr, "  CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+            g_fail++;                                                   \
+            return;                                                     \
+        }                                                               \
+    } while (0)
+
+static void t_layout() {
+    CHECK(sizeof(Msg) == 160);
+    CHECK(sizeof(struct ocm_params) == 48);
+    CHECK(sizeof(struct ocm_alloc_params) == 24);
+    CHECK(OCM_LOCAL_HOST == 1 && OCM_REMOTE_GPU == 7 && OCM_REMOTE_RDMA == 5);
+    CHECK(std::string(msg_type_str(MSG_DO_ALLOC)) == "MSG_DO_ALLOC");
+}
+
+static void t_nodefile() {
+    NodeFile nf;
+    std::string err;
+    const char *ref = "#rank dns ethernet_ip ocm_port rdmacm_port\n"
+                      "0 shiva.cc 143.215.131.65 12345 67890\n"
+                      "1 ifrit.cc 143.215.131.185 12345 67890\n";
+    CHECK(parse_nodefile_text(ref, &nf, &err) == 0);
+    CHECK(nf.size() == 2 && nf.nodes[1].dns == "ifrit.cc" && nf.nodes[1].ocm_port == 12345);
+    CHECK(nf.nodes[0].data_port == 67890 && nf.nodes[0].gpu == -1);
+    const char *rma = "#rank dns ethernet_ip ocm_port\n0 peac14 192.168.1.114 12345\n1 peac15 192.168.1.115 12345\n";
+    CHECK(parse_nodefile_text(rma, &nf, &err) == 0 && nf.size() == 2);
+    const char *gpu = "0 n 127.0.0.1 5000 0 gpu=3\n1 n 127.0.0.1 5001 0 4  # comment\n";
+    CHECK(parse_nodefile_text(gpu, &nf, &err) == 0 && nf.nodes[0].gpu == 3 && nf.nodes[1].gpu == 4);
+    CHECK(resolve_rank(nf, 1, &err) == 1);
+    CHECK(resolve_rank(nf, 5, &err) == -1);
+    CHECK(parse_nodefile_text("0 a b notaport\n", &nf, &err) == -1);
+    CHECK(parse_nodefile_text("0 a b 1\n0 a b 2\n", &nf, &err) == -1);  // duplicate rank
+    CHECK(parse_nodefile_text("1 a b 1\n", &nf, &err) == -1);            // not dense
+    CHECK(parse_nodefile_text("# only comments\n", &nf, &err) == -1);
+}
+
+static void t_range_alloc() {
+    RangeAllocator ra(1 << 20);
+    uint64_t a, b, c;
+    CHECK(ra.alloc(1000, 4096, &a) && a == 0);
+    CHECK(ra.alloc(5000, 4096, &b) && b == 4096);
+    CHECK(ra.alloc(4096, 4096, &c) && c % 4096 == 0);
+    CHECK(!ra.alloc(2 << 20, 4096, &a));
+    CHECK(ra.free(b) && !ra.free(b));
+    CHECK(ra.free(0) && ra.free(c));
+    CHECK(ra.used() == 0 && ra.num_free_ranges() == 1 && ra.largest_free() == (1u << 20));
+    // random churn keeps accounting exact and ranges disjoint
+    std::mt19937 g(7);
+    std::vector<std::pair<uint64_t, uint64_t>> live;
+    uint64_t used = 0;
+    for (int i = 0; i < 5000; i++) {
+        if (live.empty() || g() % 3) {
+            uint64_t n = 1 + g() % 20000, off;
+            if (ra.alloc(n, 256, &off)) {
+                for (auto &l : live) CHECK(off + n <= l.first || l.first + l.second <= off);
+                live.push_back({off, n});
+                used += n;
+            }
+        } else {
+            size_t k = g() % live.size();
+            CHECK(ra.free(live[k].first));
+            used -= live[k].second;
+            live.erase(live.begin() + (long)k);
+        }
+        CHECK(ra.used() == used);
+    }
+    for (auto &l : live) CHECK(ra.free(l.first));
+    CHECK(ra.used() == 0 && ra.num_free_ranges() == 1);
+}
+
+static NodeConfig cfg(int rank, uint64_t gpu, uint64_t host) {
+    NodeConfig c;
+    std::memset(&c, 0, sizeof(c));
+    c.rank = rank;
+    c.gpu = gpu ? rank : -1;
+    c.gpu_capacity = gpu;
+    c.host_capacity = host;
+    return c;
+}
+
+static void t_governor() {
+    const uint64_t G = 1ull << 30;
+    {  // ring: (orig + 1) % N, the reference policy
+        Governor gov(4, Policy::Ring, 1 << 20);
+        for (int r = 0; r < 4; r++) gov.add_node(cfg(r, 8 * G, G));
+        PlaceRequest pr;
+        pr.orig_rank = 3;
+        pr.bytes = G;
+        Placement p = gov.place(pr);
+        CHECK(p.err == 0 && p.extents.size() == 1 && p.extents[0].owner == 0 && p.extents[0].tier == TIER_GPU);
+        pr.remote_rank = 2;  // explicit owner honoured
+        p = gov.place(pr);
+        CHECK(p.extents[0].owner == 2);
+        CHECK(gov.node(2).gpu_reserved == G);
+        CHECK(gov.release(p.alloc_id) && gov.node(2).gpu_reserved == 0);
+        CHECK(!gov.release(p.alloc_id));
+    }
+    {  // spill to the host tier when HBM is exhausted, then ENOMEM
+        Governor gov(2, Policy::Ring, 1 << 20);
+        gov.add_node(cfg(0, 2 * G, 4 * G));
+        gov.add_node(cfg(1, 2 * G, 1 * G));
+        PlaceRequest pr;
+        pr.orig_rank = 0;
+        pr.bytes = 2 * G;
+        Placement a = gov.place(pr);
+        CHECK(a.err == 0 && a.extents[0].owner == 1 && a.extents[0].tier == TIER_GPU);
+        Placement b = gov.place(pr);  // rank1 full -> rank0 HBM? (fallback peers exclude origin) -> host tier
+        CHECK(b.err == 0 && b.extents[0].tier == TIER_HOST && b.extents[0].spilled);
+        CHECK(gov.spilled_count() == 1);
+        pr.flags = OCM_ALLOC_NO_SPILL;
+        Placement c = gov.place(pr);
+        CHECK(c.err == ENOMEM);
+        pr.flags = 0;
+        pr.bytes = 100 * G;
+        CHECK(gov.place(pr).err == ENOMEM);
+    }
+    {  // stripe over every peer, extents sum to the request
+        Governor gov(8, Policy::Stripe, 1 << 20);
+        for (int r = 0; r < 8; r++) gov.add_node(cfg(r, 8 * G, G));
+        PlaceRequest pr;
+        pr.orig_rank = 5;
+        pr.bytes = 3 * G + 12345;
+        Placement p = gov.place(pr);
+        CHECK(p.err == 0 && p.extents.size() == 7 && p.stripe_unit == (1u << 20));
+        uint64_t sum = 0;
+        std::set<int> owners;
+        for (auto &e : p.extents) {
+            sum += e.bytes;
+            owners.insert(e.owner);
+            CHECK(e.owner != 5);
+        }
+        CHECK(sum == pr.bytes && owners.size() == 7);
+        pr.bytes = 2 << 20;  // smaller than 7 units: only 2 extents
+        CHECK(gov.place(pr).extents.size() == 2);
+        pr.stripe_width = 3;
+        pr.bytes = G;
+        CHECK(gov.place(pr).extents.size() == 3);
+    }
+    {  // single node: remote requests land in the host tier
+        Governor gov(1, Policy::Ring, 1 << 20);
+        gov.add_node(cfg(0, 8 * G, G));
+        PlaceRequest pr;
+        pr.orig_rank = 0;
+        pr.bytes = 1 << 20;
+        Placement p = gov.place(pr);
+        CHECK(p.err == 0 && p.extents[0].owner == 0 && p.extents[0].tier == TIER_HOST);
+        pr.flags = OCM_ALLOC_LOOPBACK;
+        p = gov.place(pr);
+        CHECK(p.extents[0].owner == 0 && p.extents[0].tier == TIER_GPU);
+    }
+    {  // least loaded + dead nodes are skipped + re-placement
+        Governor gov(3, Policy::LeastLoaded, 1 << 20);
+        gov.add_node(cfg(0, 8 * G, G));
+        gov.add_node(cfg(1, 2 * G, G));
+        gov.add_node(cfg(2, 6 * G, G));
+        PlaceRequest pr;
+        pr.orig_rank = 0;
+        pr.bytes = G;
+        Placement p = gov.place(pr);
+        CHECK(p.extents[0].owner == 2);
+        gov.mark_dead(2);
+        p = gov.place(pr);
+        CHECK(p.extents[0].owner == 1);
+        PlacedExtent e;
+        CHECK(gov.replace_extent(p.alloc_id, 0, 1, &e) && e.owner != 1);
+        CHECK(gov.allocations_from(0).size() == 2);
+    }
+}
+
+static void t_stripe_geometry() {
+    for (uint64_t total : {1ull, 4095ull, 4096ull, 1000000ull, (3ull << 20) + 7}) {
+        for (int n = 1; n <= 8; n++) {
+            uint64_t sum = 0;
+            for (int i = 0; i < n; i++) sum += stripe_extent_bytes(total, 4096, n, i);
+            CHECK(sum == total);
+        }
+    }
+    CHECK(stripe_extent_bytes(10000, 4096, 2, 0) == 4096 + (10000 - 8192));
+    CHECK(stripe_extent_bytes(10000, 4096, 2, 1) == 4096);
+}
+
+static void t_arena_host() {
+    ArenaConfig ac;
+    ac.gpu = -1;
+    ac.host_capacity = 64ull << 20;
+    ac.slab_bytes = 16ull << 20;
+    Arena ar(ac);
+    Region r1, r2, r3;
+    std::memset(&r1, 0, sizeof(r1));
+    std::memset(&r2, 0, sizeof(r2));
+    std::memset(&r3, 0, sizeof(r3));
+    CHECK(ar.alloc(TIER_HOST, 1 << 20, &r1) == 0);
+    CHECK(ar.alloc(TIER_HOST, 1 << 20, &r2) == 0);
+    CHECK(r1.slab_id == r2.slab_id && r1.offset != r2.offset);
+    CHECK(ar.alloc(TIER_GPU, 1 << 20, &r3) != 0);  // no GPU tier on a CPU daemon
+    CHECK(ar.alloc(TIER_HOST, 12ull << 20, &r3) == 0 && (r3.flags & REGION_DEDICATED));
+    CHECK(ar.used(TIER_HOST) == (14ull << 20));
+    CHECK(ar.alloc(TIER_HOST, 60ull << 20, &r3) == ENOMEM);
+    // the exported handle is a path another process can open
+    char path[65] = {0};
+    std::memcpy(path, r1.handle, 64);
+    CHECK(std::string(path).find("/proc/") == 0 && access(path, R_OK | W_OK) == 0);
+    std::memset(ar.resolve(r1.slab_id, r1.offset), 0xab, 1 << 20);
+    CHECK(ar.free(r1.slab_id, r1.offset) == 0 && ar.free(r1.slab_id, r1.offset) == ENOENT);
+    CHECK(ar.free(r2.slab_id, r2.offset) == 0);
+}
+
+int main() {
+    struct T {
+        const char *name;
+        std::function<void()> fn;
+    } tests[] = {{"layout", t_layout},           {"nodefile", t_nodefile}, {"range_alloc", t_range_alloc},
+                 {"governor", t_governor},       {"stripe_geometry", t_stripe_geometry},
+                 {"arena_host", t_arena_host}};
+    for (auto &t : tests) {
+        int before = g_fail;
+        t.fn();
+        printf("%s %s\n", g_fail == before ? "PASS" : "FAIL", t.name);
+    }
+    return g_fail ? 1 : 0;
+}

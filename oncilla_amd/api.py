@@ -1,0 +1,360 @@
+"""Python binding of the libocm C ABI (``csrc/include/oncillamem.h``).
+
+Thin ctypes layer over the in-tree ``build/lib/libocm.so``: the native library
+does all the work (mailbox RPC to ocmd, IPC import, gfx950 transfer kernels).
+Mirrors the reference app API (reference inc/oncillamem.h:69-89) plus the
+MI355X extensions (``ocm_alloc_ex``, async one-sided copies, stats).
+
+    from oncilla_amd import api
+    with api.Client() as ocm:
+        a = ocm.alloc(api.OCM_REMOTE_GPU, local_bytes=1 << 20, remote_bytes=1 << 20)
+        a.fill(seed=1); a.put(0, 0, 1 << 20); a.get(0, 0, 1 << 20)
+        assert a.check(seed=1) == 0
+        a.free()
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+from .utils.paths import lib_path
+
+OCM_LOCAL_HOST = 1
+OCM_LOCAL_RMA = 2
+OCM_REMOTE_RMA = 3
+OCM_LOCAL_RDMA = 4
+OCM_REMOTE_RDMA = 5
+OCM_LOCAL_GPU = 6
+OCM_REMOTE_GPU = 7
+
+OCM_ALLOC_STRIPE = 1 << 0
+OCM_ALLOC_HOST_TIER = 1 << 1
+OCM_ALLOC_NO_SPILL = 1 << 2
+OCM_ALLOC_ZERO = 1 << 3
+OCM_ALLOC_LOOPBACK = 1 << 4
+
+OCM_TIER_HOST = 1
+OCM_TIER_GPU = 2
+OCM_MAX_EXTENTS = 8
+
+REMOTE_KINDS = (OCM_REMOTE_GPU, OCM_REMOTE_RDMA, OCM_REMOTE_RMA)
+
+
+class OcmParams(ctypes.Structure):
+    """struct ocm_params (48 bytes)."""
+
+    _fields_ = [
+        ("src_offset", ctypes.c_uint64),
+        ("dest_offset", ctypes.c_uint64),
+        ("src_offset_2", ctypes.c_uint64),
+        ("dest_offset_2", ctypes.c_uint64),
+        ("bytes", ctypes.c_uint64),
+        ("op_flag", ctypes.c_int),
+    ]
+
+
+class OcmAllocParams(ctypes.Structure):
+    """struct ocm_alloc_params (24 bytes)."""
+
+    _fields_ = [
+        ("local_alloc_bytes", ctypes.c_uint64),
+        ("rem_alloc_bytes", ctypes.c_uint64),
+        ("kind", ctypes.c_int),
+    ]
+
+
+class OcmAllocExParams(ctypes.Structure):
+    _fields_ = [
+        ("remote_rank", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("stripe_width", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("stripe_unit", ctypes.c_uint64),
+    ]
+
+
+class OcmRemoteInfo(ctypes.Structure):
+    _fields_ = [
+        ("n_extents", ctypes.c_uint32),
+        ("tier", ctypes.c_uint32 * OCM_MAX_EXTENTS),
+        ("owner_rank", ctypes.c_int32 * OCM_MAX_EXTENTS),
+        ("owner_gpu", ctypes.c_int32 * OCM_MAX_EXTENTS),
+        ("extent_bytes", ctypes.c_uint64 * OCM_MAX_EXTENTS),
+        ("stripe_unit", ctypes.c_uint64),
+        ("alloc_id", ctypes.c_uint64),
+        ("remote_bytes", ctypes.c_uint64),
+    ]
+
+
+class OcmDaemonStats(ctypes.Structure):
+    _fields_ = [
+        ("rank", ctypes.c_int32),
+        ("gpu", ctypes.c_int32),
+        ("num_nodes", ctypes.c_int32),
+        ("num_apps", ctypes.c_int32),
+        ("gpu_capacity", ctypes.c_uint64),
+        ("gpu_used", ctypes.c_uint64),
+        ("host_capacity", ctypes.c_uint64),
+        ("host_used", ctypes.c_uint64),
+        ("n_alloc", ctypes.c_uint64),
+        ("n_free", ctypes.c_uint64),
+        ("n_reclaimed", ctypes.c_uint64),
+        ("n_spilled", ctypes.c_uint64),
+        ("n_slabs", ctypes.c_uint64),
+        ("reserved", ctypes.c_uint64 * 4),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: (getattr(self, name) if name != "reserved" else None) for name, _ in self._fields_
+                if name != "reserved"}
+
+
+class OcmError(RuntimeError):
+    pass
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load libocm.so once (fails loudly if it has not been built)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        p = path or lib_path()
+        if not os.path.exists(p):
+            raise OcmError(f"{p} not found: build the native tree first (python -c 'import __graft_entry__ as g; g.build()')")
+        lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+        vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+        sigs = {
+            "ocm_init": (i32, []),
+            "ocm_tini": (i32, []),
+            "ocm_alloc": (vp, [ctypes.POINTER(OcmAllocParams)]),
+            "ocm_alloc_ex": (vp, [ctypes.POINTER(OcmAllocParams), ctypes.POINTER(OcmAllocExParams)]),
+            "ocm_free": (i32, [vp]),
+            "ocm_localbuf": (i32, [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]),
+            "ocm_is_remote": (ctypes.c_bool, [vp]),
+            "ocm_alloc_kind": (i32, [vp]),
+            "ocm_remote_sz": (i32, [vp, ctypes.POINTER(ctypes.c_size_t)]),
+            "ocm_copy_out": (i32, [vp, vp]),
+            "ocm_copy_in": (i32, [vp, vp]),
+            "ocm_copy": (i32, [vp, vp, ctypes.POINTER(OcmParams)]),
+            "ocm_copy_onesided": (i32, [vp, ctypes.POINTER(OcmParams)]),
+            "ocm_copy_onesided_async": (i32, [vp, ctypes.POINTER(OcmParams)]),
+            "ocm_wait": (i32, [vp]),
+            "ocm_remote_info": (i32, [vp, ctypes.POINTER(OcmRemoteInfo)]),
+            "ocm_remotebuf": (vp, [vp]),
+            "ocm_stats": (i32, [i32, ctypes.POINTER(OcmDaemonStats)]),
+            "ocm_rank": (i32, []),
+            "ocm_num_nodes": (i32, []),
+            "ocm_device": (i32, []),
+            "ocm_last_error": (ctypes.c_char_p, []),
+            "ocm_x_layout": (None, [ctypes.POINTER(u64)]),
+            "ocm_x_xfer": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, u64, u64, i32, i32, i32]),
+            "ocm_x_time_device_copy": (ctypes.c_double, [i32, vp, vp, u64, i32, i32, i32, i32]),
+            "ocm_x_time_onesided": (ctypes.c_double, [vp, ctypes.POINTER(OcmParams), i32]),
+            "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
+        }
+        for name, (res, args) in sigs.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def last_error() -> str:
+    e = load().ocm_last_error()
+    return e.decode(errors="replace") if e else ""
+
+
+def layout() -> dict:
+    out = (ctypes.c_uint64 * 8)()
+    load().ocm_x_layout(out)
+    keys = ["msg", "ocm_params", "ocm_alloc_params", "msg_union_offset", "region", "node_config", "alloc_req",
+            "ipc_handle"]
+    return dict(zip(keys, [int(v) for v in out]))
+
+
+class Allocation:
+    """An ocm_alloc_t handle."""
+
+    def __init__(self, client: "Client", handle: int, kind: int):
+        self._c = client
+        self.handle = ctypes.c_void_p(handle)
+        self.kind = kind
+
+    # --- reference accessors ---
+    def localbuf(self) -> tuple[int, int]:
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        if self._c.lib.ocm_localbuf(self.handle, ctypes.byref(p), ctypes.byref(n)) != 0:
+            raise OcmError("ocm_localbuf: " + last_error())
+        return (p.value or 0), n.value
+
+    @property
+    def local_ptr(self) -> int:
+        return self.localbuf()[0]
+
+    @property
+    def local_bytes(self) -> int:
+        return self.localbuf()[1]
+
+    def is_remote(self) -> bool:
+        return bool(self._c.lib.ocm_is_remote(self.handle))
+
+    def remote_size(self) -> int:
+        n = ctypes.c_size_t()
+        if self._c.lib.ocm_remote_sz(self.handle, ctypes.byref(n)) != 0:
+            raise OcmError("ocm_remote_sz: no remote buffer")
+        return n.value
+
+    def alloc_kind(self) -> int:
+        return int(self._c.lib.ocm_alloc_kind(self.handle))
+
+    def remote_info(self) -> dict:
+        info = OcmRemoteInfo()
+        if self._c.lib.ocm_remote_info(self.handle, ctypes.byref(info)) != 0:
+            raise OcmError("ocm_remote_info: not a remote allocation")
+        n = info.n_extents
+        return {
+            "alloc_id": info.alloc_id,
+            "remote_bytes": info.remote_bytes,
+            "stripe_unit": info.stripe_unit,
+            "extents": [
+                {"owner_rank": info.owner_rank[i], "owner_gpu": info.owner_gpu[i], "tier": info.tier[i],
+                 "bytes": info.extent_bytes[i]}
+                for i in range(n)
+            ],
+        }
+
+    # --- data movement ---
+    def onesided(self, op_flag: int, local_offset: int, remote_offset: int, nbytes: int, async_: bool = False) -> None:
+        p = OcmParams(local_offset, remote_offset, 0, 0, nbytes, op_flag)
+        fn = self._c.lib.ocm_copy_onesided_async if async_ else self._c.lib.ocm_copy_onesided
+        if fn(self.handle, ctypes.byref(p)) != 0:
+            raise OcmError("ocm_copy_onesided: " + last_error())
+
+    def put(self, local_offset: int, remote_offset: int, nbytes: int, async_: bool = False) -> None:
+        """One-sided write: local[local_offset:] -> remote[remote_offset:]."""
+        self.onesided(1, local_offset, remote_offset, nbytes, async_)
+
+    def get(self, local_offset: int, remote_offset: int, nbytes: int, async_: bool = False) -> None:
+        """One-sided read: remote[remote_offset:] -> local[local_offset:]."""
+        self.onesided(0, local_offset, remote_offset, nbytes, async_)
+
+    def wait(self) -> None:
+        if self._c.lib.ocm_wait(self.handle) != 0:
+            raise OcmError("ocm_wait: " + last_error())
+
+    def time_onesided(self, op_flag: int, nbytes: int, iters: int, local_offset: int = 0, remote_offset: int = 0) -> float:
+        """Seconds per blocking one-sided op, timed inside the native library."""
+        p = OcmParams(local_offset, remote_offset, 0, 0, nbytes, op_flag)
+        t = self._c.lib.ocm_x_time_onesided(self.handle, ctypes.byref(p), iters)
+        if t < 0:
+            raise OcmError("one-sided op failed: " + last_error())
+        return t
+
+    def copy_in(self, src_ptr: int) -> None:
+        if self._c.lib.ocm_copy_in(self.handle, ctypes.c_void_p(src_ptr)) != 0:
+            raise OcmError("ocm_copy_in: " + last_error())
+
+    def copy_out(self, dst_ptr: int) -> None:
+        if self._c.lib.ocm_copy_out(ctypes.c_void_p(dst_ptr), self.handle) != 0:
+            raise OcmError("ocm_copy_out: " + last_error())
+
+    def fill(self, seed: int, offset: int = 0, nbytes: Optional[int] = None) -> None:
+        """Write the deterministic word pattern into the local half."""
+        ptr, n = self.localbuf()
+        nbytes = n - offset if nbytes is None else nbytes
+        if self._c.lib.ocm_x_pattern(ctypes.c_void_p(ptr + offset), nbytes // 4, offset // 4, seed, 0) != 0:
+            raise OcmError("pattern fill failed")
+
+    def check(self, seed: int, offset: int = 0, nbytes: Optional[int] = None, first_word: Optional[int] = None) -> int:
+        """Mismatching 32-bit words of the local half against the pattern."""
+        ptr, n = self.localbuf()
+        nbytes = n - offset if nbytes is None else nbytes
+        fw = offset // 4 if first_word is None else first_word
+        bad = self._c.lib.ocm_x_pattern(ctypes.c_void_p(ptr + offset), nbytes // 4, fw, seed, 1)
+        if bad < 0:
+            raise OcmError("pattern check failed")
+        return int(bad)
+
+    def free(self) -> None:
+        if self.handle.value:
+            rc = self._c.lib.ocm_free(self.handle)
+            self.handle = ctypes.c_void_p(0)
+            if rc != 0:
+                raise OcmError("ocm_free: " + last_error())
+
+
+def copy(dst: Allocation, src: Allocation, nbytes: int, src_offset: int = 0, dest_offset: int = 0,
+         src_offset_2: int = 0, dest_offset_2: int = 0, op_flag: int = 1) -> None:
+    """ocm_copy (two-sided, staged through the pair's local half; see oncillamem.h)."""
+    p = OcmParams(src_offset, dest_offset, src_offset_2, dest_offset_2, nbytes, op_flag)
+    if dst._c.lib.ocm_copy(dst.handle, src.handle, ctypes.byref(p)) != 0:
+        raise OcmError("ocm_copy: " + last_error())
+
+
+class Client:
+    """Process attachment to the local ocmd (ocm_init / ocm_tini)."""
+
+    def __init__(self, daemon_rank: Optional[int] = None, gpu: Optional[int] = None, ns: Optional[str] = None):
+        if daemon_rank is not None:
+            os.environ["OCM_DAEMON_RANK"] = str(daemon_rank)
+        if gpu is not None:
+            os.environ["OCM_GPU"] = str(gpu)
+        if ns is not None:
+            os.environ["OCM_NS"] = ns
+        self.lib = load()
+        self.open = False
+
+    def __enter__(self) -> "Client":
+        self.init()
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    def init(self) -> None:
+        if self.lib.ocm_init() != 0:
+            raise OcmError("ocm_init: " + last_error())
+        self.open = True
+
+    def close(self) -> None:
+        if self.open:
+            self.lib.ocm_tini()
+            self.open = False
+
+    @property
+    def rank(self) -> int:
+        return int(self.lib.ocm_rank())
+
+    @property
+    def num_nodes(self) -> int:
+        return int(self.lib.ocm_num_nodes())
+
+    @property
+    def device(self) -> int:
+        return int(self.lib.ocm_device())
+
+    def alloc(self, kind: int, local_bytes: int = 0, remote_bytes: int = 0, remote_rank: int = -1, flags: int = 0,
+              stripe_width: int = 0, stripe_unit: int = 0) -> Allocation:
+        ap = OcmAllocParams(local_bytes, remote_bytes, kind)
+        if remote_rank < 0 and not flags and not stripe_width and not stripe_unit:
+            h = self.lib.ocm_alloc(ctypes.byref(ap))
+        else:
+            ex = OcmAllocExParams(remote_rank, flags, stripe_width, 0, stripe_unit)
+            h = self.lib.ocm_alloc_ex(ctypes.byref(ap), ctypes.byref(ex))
+        if not h:
+            raise OcmError("ocm_alloc: " + last_error())
+        return Allocation(self, h, kind)
+
+    def stats(self, rank: int = -1) -> dict:
+        s = OcmDaemonStats()
+        if self.lib.ocm_stats(rank, ctypes.byref(s)) != 0:
+            raise OcmError("ocm_stats: " + last_error())
+        return s.as_dict()

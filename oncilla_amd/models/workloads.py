@@ -1,0 +1,121 @@
+"""Benchmark workloads — the "model families" of a disaggregated-memory runtime.
+
+Each BASELINE.json config is one workload here:
+  #1 local malloc-backed ocm_alloc latency (CPU, loopback mailbox)   -> alloc_latency(kind=OCM_LOCAL_HOST)
+  #2 remote alloc into peer HBM + one-sided put/get                   -> alloc_latency + rw_sweep_step
+  #3 all-to-all remote alloc, 4 KiB-1 GiB put/get sweep               -> rw_sweep_step on a striped pair
+  #4 HBM exhaustion -> pinned host spill tier                         -> spill_probe
+  #5 concurrent clients, alloc/free churn + crash reclaim             -> churn
+The R/W sweep mirrors the reference `ocm_test 4` (test/ocm_test.c:323-425:
+a 2 GiB+1 pair, reads then writes, sizes doubling up to 1 GiB) with the
+timing the reference never had.
+"""
+from __future__ import annotations
+
+import time
+from typing import Iterable
+
+from .. import api
+
+
+def sweep_sizes(min_bytes: int = 4096, max_bytes: int = 1 << 30) -> list[int]:
+    out, s = [], min_bytes
+    while s <= max_bytes:
+        out.append(s)
+        s *= 2
+    return out
+
+
+def percentile(xs: list[float], q: float) -> float:
+    ys = sorted(xs)
+    if not ys:
+        return float("nan")
+    k = min(len(ys) - 1, max(0, int(round(q / 100.0 * (len(ys) - 1)))))
+    return ys[k]
+
+
+def alloc_latency(client: api.Client, kind: int, samples: int, local_bytes: int, remote_bytes: int = 0,
+                  flags: int = 0, warmup: int = 5) -> dict:
+    """Wall time of ocm_alloc (and ocm_free) through the daemon, in microseconds."""
+    a_us, f_us = [], []
+    for i in range(samples + warmup):
+        t0 = time.perf_counter()
+        a = client.alloc(kind, local_bytes=local_bytes, remote_bytes=remote_bytes, flags=flags)
+        t1 = time.perf_counter()
+        a.free()
+        t2 = time.perf_counter()
+        if i >= warmup:
+            a_us.append((t1 - t0) * 1e6)
+            f_us.append((t2 - t1) * 1e6)
+    return {
+        "alloc_p50_us": percentile(a_us, 50),
+        "alloc_p99_us": percentile(a_us, 99),
+        "free_p50_us": percentile(f_us, 50),
+        "samples": samples,
+    }
+
+
+def rw_sweep_step(alloc: api.Allocation, sizes: Iterable[int]) -> int:
+    """One step of the R/W sweep: a get then a put of every size. Returns bytes moved."""
+    moved = 0
+    for s in sizes:
+        alloc.get(0, 0, s)
+        alloc.put(0, 0, s)
+        moved += 2 * s
+    return moved
+
+
+def characterize(alloc: api.Allocation, sizes: Iterable[int], target_s: float = 0.02, max_iters: int = 200) -> dict:
+    """Per-size put/get seconds per op (timed in C, no Python in the loop)."""
+    out = {}
+    for s in sizes:
+        probe = alloc.time_onesided(1, s, 1)
+        iters = max(1, min(max_iters, int(target_s / max(probe, 1e-7))))
+        t_get = alloc.time_onesided(0, s, iters)
+        t_put = alloc.time_onesided(1, s, iters)
+        out[s] = {"get_s": t_get, "put_s": t_put, "iters": iters}
+    return out
+
+
+def spill_probe(client: api.Client, chunk_bytes: int, max_chunks: int) -> dict:
+    """Allocate remote chunks until HBM capacity runs out; count host-tier spills."""
+    allocs, tiers = [], {api.OCM_TIER_GPU: 0, api.OCM_TIER_HOST: 0}
+    try:
+        for _ in range(max_chunks):
+            try:
+                a = client.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=chunk_bytes)
+            except api.OcmError:
+                break
+            allocs.append(a)
+            for e in a.remote_info()["extents"]:
+                tiers[e["tier"]] = tiers.get(e["tier"], 0) + 1
+    finally:
+        for a in allocs:
+            a.free()
+    return {"chunks": len(allocs), "gpu_extents": tiers[api.OCM_TIER_GPU], "host_extents": tiers[api.OCM_TIER_HOST]}
+
+
+def churn(client: api.Client, rounds: int, kind: int, local_bytes: int, remote_bytes: int, seed: int = 0) -> dict:
+    """Alloc/free churn with data checks on every allocation."""
+    import random
+
+    rng = random.Random(seed)
+    live: list[api.Allocation] = []
+    n_alloc = 0
+    for i in range(rounds):
+        if live and rng.random() < 0.45:
+            live.pop(rng.randrange(len(live))).free()
+            continue
+        a = client.alloc(kind, local_bytes=local_bytes, remote_bytes=remote_bytes)
+        n_alloc += 1
+        if a.is_remote():
+            a.fill(seed=i + 1)
+            a.put(0, 0, local_bytes)
+            a.fill(seed=0)
+            a.get(0, 0, local_bytes)
+            if a.check(seed=i + 1) != 0:
+                raise RuntimeError(f"churn round {i}: data mismatch")
+        live.append(a)
+    for a in live:
+        a.free()
+    return {"allocs": n_alloc}

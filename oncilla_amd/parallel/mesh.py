@@ -1,0 +1,150 @@
+"""Launch and tear down an ocmd daemon mesh (the reference's hand-started
+`oncillamem <nodefile>` per host, src/main.c:187-224, made scriptable).
+
+One daemon per GPU on this node (or N CPU-only daemons). Each gets its own
+rank, TCP port and mailbox namespace; `Mesh.start()` returns when every daemon
+has written its ready file, i.e. the rank0 directory knows all N nodes.
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import socket
+import subprocess
+import tempfile
+import time
+import uuid
+from typing import Optional, Sequence
+
+from ..utils.paths import bin_path
+
+
+def free_ports(n: int) -> list[int]:
+    socks, ports = [], []
+    for _ in range(n):
+        s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        ports.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return ports
+
+
+def write_nodefile(path: str, ports: Sequence[int], gpus: Optional[Sequence[int]] = None, host: str = "127.0.0.1") -> str:
+    lines = ["#rank dns ethernet_ip ocm_port rdmacm_port gpu"]
+    for r, p in enumerate(ports):
+        g = "" if gpus is None or gpus[r] is None else f" gpu={gpus[r]}"
+        lines.append(f"{r} localhost {host} {p} 0{g}")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return path
+
+
+class Daemon:
+    def __init__(self, rank: int, proc: subprocess.Popen, ready_file: str, log_file: str):
+        self.rank = rank
+        self.proc = proc
+        self.ready_file = ready_file
+        self.log_file = log_file
+
+    def alive(self) -> bool:
+        return self.proc.poll() is None
+
+    def log(self) -> str:
+        try:
+            with open(self.log_file) as f:
+                return f.read()
+        except OSError:
+            return ""
+
+
+class Mesh:
+    """N daemons on this host.
+
+    gpus: per-rank GPU ordinal (None entries or gpus=None -> CPU-only daemons
+    unless `auto_gpu`), so tests can put several daemons on one MI355X.
+    """
+
+    def __init__(self, n: int, gpus: Optional[Sequence[Optional[int]]] = None, ns: Optional[str] = None,
+                 policy: str = "ring", extra_args: Sequence[str] = (), env: Optional[dict] = None,
+                 workdir: Optional[str] = None, ports: Optional[Sequence[int]] = None, ranks: Optional[Sequence[int]] = None):
+        self.n = n
+        self.gpus = list(gpus) if gpus is not None else [None] * n
+        self.ns = ns or f"m{uuid.uuid4().hex[:10]}"
+        self.policy = policy
+        self.extra_args = list(extra_args)
+        self.env = dict(env or {})
+        self.workdir = workdir or tempfile.mkdtemp(prefix=f"ocm_{self.ns}_")
+        self.ports = list(ports) if ports is not None else free_ports(n)
+        self.ranks = list(ranks) if ranks is not None else list(range(n))  # which ranks THIS process launches
+        self.nodefile = os.path.join(self.workdir, "nodefile")
+        self.daemons: list[Daemon] = []
+
+    def client_env(self, rank: int = 0) -> dict:
+        env = dict(os.environ)
+        env.update({"OCM_NS": self.ns, "OCM_DAEMON_RANK": str(rank)})
+        return env
+
+    def start(self, timeout: float = 60.0) -> "Mesh":
+        write_nodefile(self.nodefile, self.ports, self.gpus)
+        for r in self.ranks:
+            ready = os.path.join(self.workdir, f"ready.{r}.json")
+            log = os.path.join(self.workdir, f"ocmd.{r}.log")
+            args = [bin_path("ocmd"), self.nodefile, "--rank", str(r), "--ns", self.ns, "--policy", self.policy,
+                    "--ready-file", ready, "--bind", "127.0.0.1"]
+            if self.gpus[r] is None:
+                args += ["--gpu", "none"]
+            else:
+                args += ["--gpu", str(self.gpus[r])]
+            args += self.extra_args
+            env = dict(os.environ)
+            env.update(self.env)
+            env["OCM_NS"] = self.ns
+            with open(log, "w") as lf:
+                proc = subprocess.Popen(args, stdout=lf, stderr=subprocess.STDOUT, env=env, start_new_session=True)
+            self.daemons.append(Daemon(r, proc, ready, log))
+        deadline = time.time() + timeout
+        for d in self.daemons:
+            while not os.path.exists(d.ready_file):
+                if not d.alive():
+                    raise RuntimeError(f"ocmd rank {d.rank} exited ({d.proc.returncode}):\n{d.log()}")
+                if time.time() > deadline:
+                    self.stop()
+                    raise TimeoutError(f"ocmd rank {d.rank} not ready after {timeout}s:\n{d.log()}")
+                time.sleep(0.02)
+        return self
+
+    def ready_info(self) -> list[dict]:
+        out = []
+        for d in self.daemons:
+            with open(d.ready_file) as f:
+                out.append(json.load(f))
+        return out
+
+    def kill(self, rank: int, sig: int = signal.SIGKILL) -> None:
+        for d in self.daemons:
+            if d.rank == rank and d.alive():
+                d.proc.send_signal(sig)
+                d.proc.wait(timeout=10)
+
+    def stop(self, timeout: float = 10.0) -> None:
+        for d in self.daemons:
+            if d.alive():
+                d.proc.send_signal(signal.SIGTERM)
+        for d in self.daemons:
+            try:
+                d.proc.wait(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                d.proc.kill()
+                d.proc.wait(timeout=5)
+
+    def logs(self) -> str:
+        return "\n".join(f"--- ocmd rank {d.rank} ---\n{d.log()}" for d in self.daemons)
+
+    def __enter__(self) -> "Mesh":
+        return self.start()
+
+    def __exit__(self, *exc) -> None:
+        self.stop()

@@ -1,0 +1,35 @@
+"""bench.py contract on CPU (1 rank, and 2 ranks under torch.distributed.run/gloo)."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _last_json(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_single(native):
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--device", "cpu", "--steps", "2", "--warmup",
+                        "1", "--max-bytes", str(1 << 20), "--alloc-samples", "20"], capture_output=True, text=True,
+                       timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr
+    res = _last_json(r.stdout)
+    assert KEYS <= set(res) and res["n_gpus"] == 1 and res["value"] > 0
+    assert res["alloc_p50_us"] > 0 and res["config"]["remote_tier"] == "host"
+
+
+def test_bench_two_ranks(native):
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(REPO, "bench.py"),
+                        "--gpus", "2", "--device", "cpu", "--steps", "2", "--warmup", "1", "--max-bytes",
+                        str(1 << 20), "--alloc-samples", "20"], capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = _last_json(r.stdout)
+    assert res["n_gpus"] == 2 and res["value"] > 0 and res["config"]["parallelism"] == "stripe2"

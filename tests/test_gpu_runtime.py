@@ -1,0 +1,109 @@
+"""The runtime on a real MI355X: daemons owning HBM, IPC import into the app,
+put/get through the gfx950 kernel, multi-daemon meshes sharing one GPU, the
+graft smoke and the benchmark contract."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from oncilla_amd import api
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_native_library_is_the_path(native):
+    from oncilla_amd.utils.paths import lib_path
+
+    api.load()
+    maps = open(f"/proc/{os.getpid()}/maps").read()
+    assert os.path.realpath(lib_path()) in maps
+
+
+@pytest.mark.parametrize("args", [["1", "4", "8", "2"], ["1", "4", "8", "5"], ["1", "4", "8", "3"], ["2", "8", "8"],
+                                  ["3", "4", "8"], ["4", "2", "3", "16"], ["5", "8", "16"]])
+def test_ocm_test_single_gpu_daemon(mesh_factory, tool, native, args):
+    m = mesh_factory(1, gpus=[0])
+    rc, out = tool([f"{native}/ocm_test", *args], env=dict(m.client_env(0), OCM_GPU="0"))
+    assert rc == 0, out + m.logs()
+
+
+def test_remote_hbm_across_processes(mesh_factory):
+    # two daemons on the same MI355X: rank1's HBM is "remote" for an app on rank0
+    m = mesh_factory(2, gpus=[0, 0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 64 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n)
+        info = a.remote_info()
+        assert info["extents"][0]["owner_rank"] == 1 and info["extents"][0]["tier"] == api.OCM_TIER_GPU
+        a.fill(seed=5)
+        a.put(0, 0, n)
+        a.fill(seed=0)
+        a.get(0, 0, n)
+        assert a.check(seed=5) == 0
+        st = c.stats(1)
+        assert st["gpu_used"] == n and st["gpu"] == 0
+        a.free()
+        assert c.stats(1)["gpu_used"] == 0
+
+
+def test_striped_hbm_over_three_owners(mesh_factory):
+    m = mesh_factory(4, gpus=[0, 0, 0, 0], policy="stripe")
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = (96 << 20) + 4096
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n)
+        info = a.remote_info()
+        assert len(info["extents"]) == 3 and all(e["tier"] == api.OCM_TIER_GPU for e in info["extents"])
+        a.fill(seed=9)
+        a.put(0, 0, n)
+        a.fill(seed=0)
+        a.get(0, 0, n)
+        assert a.check(seed=9) == 0
+        # async put/get + wait
+        a.fill(seed=10)
+        a.put(0, 0, n, async_=True)
+        a.wait()
+        a.fill(seed=0)
+        a.get(0, 0, n, async_=True)
+        a.wait()
+        assert a.check(seed=10) == 0
+        a.free()
+
+
+def test_host_tier_pair_and_copy_in_out(mesh_factory):
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 16 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n)
+        assert a.remote_info()["extents"][0]["tier"] == api.OCM_TIER_HOST
+        src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda:0")
+        dst = torch.zeros_like(src)
+        a.copy_in(src.data_ptr())
+        a.copy_out(dst.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(src, dst)
+        hsrc = src.cpu()
+        hdst = torch.zeros_like(hsrc)
+        a.copy_in(hsrc.data_ptr())
+        a.copy_out(hdst.data_ptr())
+        assert torch.equal(hsrc, hdst)
+        a.free()
+
+
+def test_graft_smoke():
+    r = subprocess.run([sys.executable, os.path.join(REPO, "__graft_entry__.py"), "smoke"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "smoke OK" in r.stdout
+
+
+def test_bench_gpu_small():
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--max-bytes",
+                        str(64 << 20), "--alloc-samples", "50"], capture_output=True, text=True, timeout=600,
+                       cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["config"]["device"] == "gpu" and res["value"] > 0

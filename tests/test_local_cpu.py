@@ -1,0 +1,85 @@
+"""Config #1: one CPU-only daemon, loopback mailbox, malloc-backed local kinds.
+Runs the reference-equivalent ocm_test 1-4 (reference test/ocm_test.c) and the
+Python API against it."""
+import pytest
+
+from oncilla_amd import api
+from oncilla_amd.models import workloads as wl
+
+
+@pytest.fixture
+def one(mesh_factory):
+    return mesh_factory(1)
+
+
+@pytest.mark.parametrize("sub", [1, 3, 4, 5])
+def test_ocm_test_alloc(one, tool, native, sub):
+    rc, out = tool([f"{native}/ocm_test", "1", "1", "2", str(sub)], env=one.client_env(0))
+    assert rc == 0, out + one.logs()
+    assert "pass: test 1" in out
+
+
+def test_ocm_test_alloc_gpu_kind_fails_without_gpu(one, tool, native):
+    rc, out = tool([f"{native}/ocm_test", "1", "1", "2", "2"], env=dict(one.client_env(0), OCM_NO_GPU="1"))
+    assert rc != 0 and "no GPU" in out
+
+
+def test_ocm_test_onesided(one, tool, native):
+    rc, out = tool([f"{native}/ocm_test", "2", "4", "4"], env=one.client_env(0))
+    assert rc == 0, out + one.logs()
+
+
+def test_ocm_test_twosided(one, tool, native):
+    rc, out = tool([f"{native}/ocm_test", "3", "2", "4"], env=one.client_env(0))
+    assert rc == 0, out + one.logs()
+
+
+def test_ocm_test_bw_sweep(one, tool, native):
+    rc, out = tool([f"{native}/ocm_test", "4", "0", "2", "8"], env=one.client_env(0))
+    assert rc == 0, out + one.logs()
+    assert out.count("GiB/s") == 2 * 18  # 64 B .. 8 MiB, read and write
+
+
+def test_python_api_local(one, monkeypatch):
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    with api.Client(daemon_rank=0, ns=one.ns) as c:
+        assert c.num_nodes == 1 and c.rank == 0 and c.device == -1
+        h = c.alloc(api.OCM_LOCAL_HOST, local_bytes=1 << 20)
+        assert not h.is_remote() and h.local_bytes == 1 << 20
+        with pytest.raises(api.OcmError):
+            h.remote_size()
+        h.free()
+        # remote pair on a single node lands in the host tier of the only daemon
+        r = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=3 << 20)
+        info = r.remote_info()
+        assert info["extents"][0]["tier"] == api.OCM_TIER_HOST and info["remote_bytes"] == 3 << 20
+        r.fill(seed=3)
+        r.put(0, 1 << 20, 1 << 20)
+        r.fill(seed=0)
+        r.get(0, 1 << 20, 1 << 20)
+        assert r.check(seed=3) == 0
+        with pytest.raises(api.OcmError):
+            r.put(0, 3 << 20, 16)  # past the remote end
+        st = c.stats()
+        assert st["host_used"] >= 3 << 20 and st["num_apps"] == 1
+        r.free()
+        assert c.stats()["host_used"] == 0
+
+
+def test_alloc_latency_local(one, monkeypatch):
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    with api.Client(daemon_rank=0, ns=one.ns) as c:
+        lat = wl.alloc_latency(c, api.OCM_LOCAL_HOST, 100, local_bytes=4096)
+        # the reference's derived floor is ~0.5 ms (two 500 us mailbox polls)
+        assert lat["alloc_p50_us"] < 500
+
+
+def test_daemon_rejects_unknown_app_and_bad_requests(one, monkeypatch):
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    with api.Client(daemon_rank=0, ns=one.ns) as c:
+        with pytest.raises(api.OcmError):
+            c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=0)
+        with pytest.raises(api.OcmError):
+            c.alloc(99, local_bytes=4096)
+        with pytest.raises(api.OcmError):
+            c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 50)  # exceeds every tier

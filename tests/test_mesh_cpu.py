@@ -1,0 +1,156 @@
+"""Multi-daemon meshes on one host (CPU-only daemons, host-tier memory):
+placement policies, striping, explicit owners, spill/ENOMEM, crash reclaim and
+daemon death. The same protocol runs unchanged when daemons own HBM."""
+import os
+import signal
+import subprocess
+import sys
+import textwrap
+import time
+
+import pytest
+
+from oncilla_amd import api
+from oncilla_amd.models import workloads as wl
+
+
+@pytest.fixture
+def four(mesh_factory):
+    return mesh_factory(4)
+
+
+@pytest.fixture(autouse=True)
+def _cpu_app(monkeypatch):
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+
+
+def test_ring_placement_matches_reference(four):
+    # reference src/alloc.c:107,120: remote allocations go to (orig_rank + 1) % N
+    for orig in range(4):
+        with api.Client(daemon_rank=orig, ns=four.ns) as c:
+            a = c.alloc(api.OCM_REMOTE_RMA, local_bytes=4096, remote_bytes=1 << 20)
+            assert a.remote_info()["extents"][0]["owner_rank"] == (orig + 1) % 4
+            a.free()
+        api.load().ocm_tini()
+
+
+@pytest.mark.parametrize("orig", [0, 2])
+def test_ocm_test_suite_through_mesh(four, tool, native, orig):
+    env = four.client_env(orig)
+    for args in (["1", "1", "2", "3"], ["2", "8", "8"], ["3", "2", "4"], ["5", "8", "1"], ["4", "1", "2", "4"]):
+        rc, out = tool([f"{native}/ocm_test", *args], env=env)
+        assert rc == 0, f"ocm_test {args}: {out}\n{four.logs()}"
+
+
+def test_stripe_and_explicit_owner(four):
+    with api.Client(daemon_rank=1, ns=four.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=8 << 20, remote_bytes=8 << 20, flags=api.OCM_ALLOC_STRIPE,
+                    stripe_unit=64 << 10)
+        info = a.remote_info()
+        owners = [e["owner_rank"] for e in info["extents"]]
+        assert sorted(owners) == [0, 2, 3] and info["stripe_unit"] == 64 << 10
+        assert sum(e["bytes"] for e in info["extents"]) == 8 << 20
+        a.fill(seed=11)
+        a.put(0, 0, 8 << 20)
+        a.fill(seed=0)
+        a.get(0, 0, 8 << 20)
+        assert a.check(seed=11) == 0
+        # unaligned window straddling stripe units
+        a.fill(seed=12)
+        a.put(4, 65536 - 12, 300000)
+        a.fill(seed=0)
+        a.get(4, 65536 - 12, 300000)
+        assert a.check(seed=12, offset=4, nbytes=(300000 // 4) * 4 - 4, first_word=1) == 0
+        a.free()
+        b = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20, remote_rank=3)
+        assert b.remote_info()["extents"][0]["owner_rank"] == 3
+        b.free()
+        with pytest.raises(api.OcmError):
+            c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20, remote_rank=9)
+
+
+def test_two_sided_remote_to_remote(four):
+    with api.Client(daemon_rank=0, ns=four.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20, remote_rank=1)
+        b = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20, remote_rank=2)
+        a.fill(seed=21)
+        a.put(0, 0, 1 << 20)
+        api.copy(b, a, 1 << 20)  # remote -> remote, direct
+        b.get(0, 0, 1 << 20)
+        assert b.check(seed=21) == 0
+        a.free()
+        b.free()
+
+
+def test_capacity_enomem_and_accounting(mesh_factory):
+    m = mesh_factory(2, extra_args=["--host-capacity", str(8 << 20)])
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=6 << 20)
+        assert a.remote_info()["extents"][0]["owner_rank"] == 1
+        b = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=6 << 20)  # peer full -> origin host tier
+        assert b.remote_info()["extents"][0]["owner_rank"] == 0
+        with pytest.raises(api.OcmError):
+            c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=6 << 20)
+        assert c.stats(1)["host_used"] == 6 << 20
+        a.free()
+        b.free()
+        assert c.stats(1)["host_used"] == 0 and c.stats(0)["host_used"] == 0
+
+
+CRASHER = textwrap.dedent("""
+    import os, signal, sys
+    sys.path.insert(0, {repo!r})
+    from oncilla_amd import api
+    c = api.Client(daemon_rank={rank}, ns={ns!r}); c.init()
+    keep = [c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=2 << 20) for _ in range(4)]
+    print("ready", flush=True)
+    os.kill(os.getpid(), signal.SIGKILL)
+""")
+
+
+def test_crash_reclaim(four):
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = CRASHER.format(repo=repo, rank=2, ns=four.ns)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, OCM_NO_GPU="1"))
+    assert "ready" in r.stdout and r.returncode == -signal.SIGKILL
+    with api.Client(daemon_rank=0, ns=four.ns) as c:
+        deadline = time.time() + 10
+        while time.time() < deadline:
+            if c.stats(2)["n_reclaimed"] == 4 and c.stats(3)["host_used"] == 0:
+                break
+            time.sleep(0.05)
+        assert c.stats(2)["n_reclaimed"] == 4
+        assert c.stats(3)["host_used"] == 0  # owner (2 + 1) % 4 got its memory back
+
+
+def test_concurrent_clients_churn(four):
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent(f"""
+        import sys; sys.path.insert(0, {repo!r})
+        from oncilla_amd import api
+        from oncilla_amd.models import workloads as wl
+        r = int(sys.argv[1])
+        with api.Client(daemon_rank=r % 4, ns={four.ns!r}) as c:
+            print(wl.churn(c, 60, api.OCM_REMOTE_RDMA, 64 << 10, 64 << 10, seed=r))
+    """)
+    procs = [subprocess.Popen([sys.executable, "-c", code, str(i)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True, env=dict(os.environ, OCM_NO_GPU="1")) for i in range(8)]
+    for p in procs:
+        out, err = p.communicate(timeout=120)
+        assert p.returncode == 0, err + four.logs()
+    with api.Client(daemon_rank=0, ns=four.ns) as c:
+        for r in range(4):
+            assert c.stats(r)["host_used"] == 0
+
+
+def test_daemon_death_fails_fast(four):
+    with api.Client(daemon_rank=0, ns=four.ns) as c:
+        four.kill(1)
+        time.sleep(0.2)
+        # rank0's ring successor is dead: placement skips it
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20)
+        assert a.remote_info()["extents"][0]["owner_rank"] == 2
+        a.free()
+        with pytest.raises(api.OcmError):
+            c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20, remote_rank=1)
