@@ -60,11 +60,15 @@ public:
 private:
     struct App {
         pid_t pid = 0;
-        std::string mbox;
+        int fd = -1;               // mailbox connection the app CONNECTed on
         int pidfd = -1;
-        int mqfd = -1;
         std::deque<Msg> backlog;
         bool watching_out = false;
+    };
+    struct AppConn {
+        int fd = -1;
+        pid_t peer_pid = -1;       // SO_PEERCRED
+        pid_t app_pid = 0;         // set by MSG_CONNECT
     };
     struct Pending {
         uint64_t seq = 0;
@@ -105,11 +109,12 @@ private:
 
     // sources
     void on_mailbox();
+    void on_app_conn(int fd, uint32_t events);
+    void close_app_conn(int fd);
     void on_accept();
     void on_conn_readable(int fd);
     void on_conn_writable(int fd);
     void on_pidfd(pid_t pid);
-    void on_app_writable(pid_t pid);
     void on_signal();
     void drop_conn(int fd);
 
@@ -120,7 +125,7 @@ private:
     void send_app(pid_t pid, const Msg &m);
 
     // protocol steps
-    void app_connect(const Msg &m);
+    void app_connect(const Msg &m, int fd);
     void app_disconnect(pid_t pid, bool crashed);
     void app_req_alloc(Msg &m);
     void app_req_free(Msg &m);
@@ -147,7 +152,8 @@ private:
     int rank_ = -1, n_ = 0, gpu_ = -1, num_gpu_ = 0;
     uint64_t gpu_total_ = 0;
     std::string ns_;
-    Mailbox box_;
+    int mbox_fd_ = -1;                             // listening app mailbox
+    std::map<int, AppConn> app_conns_;             // fd -> connection
     int ep_ = -1, listen_fd_ = -1, sig_fd_ = -1;
     bool stop_ = false, ready_ = false;
     std::unique_ptr<Arena> arena_;

@@ -1,63 +1,62 @@
-// Process mailboxes over POSIX message queues (app <-> local daemon).
+// Process mailboxes (app <-> local daemon control plane).
 //
-// Parity with reference inc/pmsg.h:31-51 / src/pmsg.c: every process owns one
-// receive-only mailbox, "attaches" to others to send, messages have one fixed
-// size, and stale mailboxes can be cleaned up. Differences by design:
-//   * names are namespaced so 8 per-GPU daemons (and concurrent test meshes)
-//     share one host: /ocm_<ns>_d<rank> (daemon), /ocm_<ns>_p<pid> (app);
-//   * receives block in the kernel (mq_timedreceive) instead of spinning on
-//     EAGAIN (reference src/pmsg.c:135-151), and the daemon side exposes the
-//     queue descriptor so it can sit in an epoll set;
-//   * sends from the daemon are non-blocking so a stalled app can never wedge
-//     the event loop (the caller keeps a backlog and waits for EPOLLOUT).
+// Parity with reference inc/pmsg.h:31-51 / src/pmsg.c: fixed-size records,
+// one mailbox per process, attach-then-send, cleanup of stale mailboxes.
+// Transport: AF_UNIX SOCK_SEQPACKET in the abstract namespace instead of POSIX
+// message queues. Measured reason: on the MI355X pool the app user runs with
+// RLIMIT_MSGQUEUE = 0 (`ulimit -q` 0), so every mq_open fails with EMFILE; the
+// same holds in most containers. Seqpacket sockets keep record boundaries,
+// block in the kernel (no EAGAIN spin as in reference src/pmsg.c:135-151),
+// sit in an epoll set, report the peer's pid via SO_PEERCRED (an app cannot
+// impersonate another pid) and deliver EOF when the peer process dies (crash
+// reclaim without polling). Abstract names need no filesystem and vanish with
+// their owner, so there are no stale mailboxes to clean up.
+//   daemon endpoint: "@ocm_<ns>_d<rank>"   app endpoint (pmsg C API only): "@ocm_<ns>_p<pid>"
 #pragma once
-#include <mqueue.h>
 #include <sys/types.h>
 
+#include <cstddef>
+#include <map>
 #include <string>
-#include <unordered_map>
+#include <vector>
 
 namespace ocm {
 
-std::string pmsg_namespace();                       // OCM_NS or "default"
+std::string pmsg_namespace();                                   // OCM_NS or "default"
 std::string daemon_mailbox_name(int rank, const std::string &ns);
 std::string app_mailbox_name(pid_t pid, const std::string &ns);
 
-class Mailbox {
+// Listening endpoint (non-blocking). Returns fd or -1.
+int mbox_listen(const std::string &name, int backlog = 256);
+// Accept one pending connection (non-blocking), fills the peer pid. -1 when none.
+int mbox_accept(int listen_fd, pid_t *peer_pid);
+// Connect to a listening endpoint, retrying for `timeout_ms`. Returns fd or -1.
+int mbox_connect(const std::string &name, int timeout_ms);
+// Peer pid of a connected mailbox socket (SO_PEERCRED), -1 on error.
+pid_t mbox_peer_pid(int fd);
+// One record. timeout_ms < 0 blocks, 0 polls. Returns 1 ok, 0 timeout / would
+// block, -1 error or peer closed.
+int mbox_send(int fd, const void *msg, size_t size, int timeout_ms);
+int mbox_recv(int fd, void *msg, size_t size, int timeout_ms);
+
+// Client-side channel to one daemon (what libocm uses).
+class Channel {
 public:
-    Mailbox() = default;
-    ~Mailbox();
-    Mailbox(const Mailbox &) = delete;
-    Mailbox &operator=(const Mailbox &) = delete;
-
-    // Create (O_EXCL) and open our own receive queue. `replace` unlinks a stale
-    // queue of the same name first (daemon restart after a crash).
-    int open_self(const std::string &name, size_t msg_size, long depth, bool replace);
-    void close_self(bool unlink_queue = true);
-    int fd() const { return static_cast<int>(rx_); }
-    const std::string &name() const { return name_; }
-
-    // Receive one message. timeout_ms < 0 blocks, 0 polls.
-    // Returns 1 = got one, 0 = timeout / empty, -1 = error.
-    int recv(void *msg, int timeout_ms);
-    long pending() const;
-
-    // Sending side.
-    int attach(const std::string &peer, bool nonblocking);
-    void detach(const std::string &peer);
-    // Returns 1 sent, 0 would block (non-blocking peer queue full), -1 error.
-    int send(const std::string &peer, const void *msg, int timeout_ms = -1);
-    int peer_fd(const std::string &peer) const;
+    ~Channel() { close(); }
+    int connect(const std::string &name, int timeout_ms);
+    void close();
+    int fd() const { return fd_; }
+    bool connected() const { return fd_ >= 0; }
+    int send(const void *msg, size_t size, int timeout_ms) { return mbox_send(fd_, msg, size, timeout_ms); }
+    int recv(void *msg, size_t size, int timeout_ms) { return mbox_recv(fd_, msg, size, timeout_ms); }
 
 private:
-    mqd_t rx_ = (mqd_t)-1;
-    std::string name_;
-    size_t msg_size_ = 0;
-    std::unordered_map<std::string, mqd_t> tx_;
+    int fd_ = -1;
 };
 
-// Unlink every mailbox of namespace `ns` whose owner process is gone
-// (reference pmsg_cleanup unlinked /ocm_mq_2../ocm_mq_<pid_max> blindly).
+// Stale-mailbox cleanup. Abstract sockets disappear with their owner, so this
+// only reports whether `name` is still served by a live process.
+bool mbox_alive(const std::string &name);
 int pmsg_cleanup(const std::string &ns);
 
 }  // namespace ocm
@@ -65,7 +64,7 @@ int pmsg_cleanup(const std::string &ns);
 // ---- reference-shaped C interface (inc/pmsg.h:31-51), used by tools/tests ----
 extern "C" {
 int pmsg_init(size_t pmsg_size);
-int pmsg_open(pid_t self_pid);   // PMSG_DAEMON_PID (-1 - rank) opens a daemon mailbox
+int pmsg_open(pid_t self_pid);   // PMSG_DAEMON_PID(rank) opens a daemon mailbox
 int pmsg_close(void);
 int pmsg_attach(pid_t to_pid);
 int pmsg_detach(pid_t to_pid);

@@ -22,7 +22,7 @@ namespace ocm {
 
 namespace {
 
-enum Tag : uint64_t { T_MBOX = 1, T_LISTEN, T_CONN, T_PIDFD, T_APPMQ, T_SIGNAL };
+enum Tag : uint64_t { T_MBOX = 1, T_LISTEN, T_CONN, T_PIDFD, T_APPCONN, T_SIGNAL };
 inline uint64_t tag(Tag k, uint64_t id) { return (static_cast<uint64_t>(k) << 56) | (id & 0x00ffffffffffffffull); }
 inline Tag tag_kind(uint64_t t) { return static_cast<Tag>(t >> 56); }
 inline uint64_t tag_id(uint64_t t) { return t & 0x00ffffffffffffffull; }
@@ -253,12 +253,16 @@ int Daemon::init() {
     sig_fd_ = signalfd(-1, &mask, SFD_CLOEXEC | SFD_NONBLOCK);
     ep_add(sig_fd_, EPOLLIN, tag(T_SIGNAL, 0));
 
-    pmsg_cleanup(ns_);
-    if (box_.open_self(daemon_mailbox_name(rank_, ns_), kMsgBytes, 8, true) != 0) {
+    if (mbox_alive(daemon_mailbox_name(rank_, ns_))) {
+        OCM_ERR("another ocmd already serves rank %d in namespace %s", rank_, ns_.c_str());
+        return -1;
+    }
+    mbox_fd_ = mbox_listen(daemon_mailbox_name(rank_, ns_));
+    if (mbox_fd_ < 0) {
         OCM_ERR("cannot open daemon mailbox: %s", last_error());
         return -1;
     }
-    ep_add(box_.fd(), EPOLLIN, tag(T_MBOX, 0));
+    ep_add(mbox_fd_, EPOLLIN, tag(T_MBOX, 0));
 
     listen_fd_ = tcp_listen(cfg_.bind_ip.empty() ? "0.0.0.0" : cfg_.bind_ip, me.ocm_port, 64);
     if (listen_fd_ < 0) {
@@ -330,11 +334,14 @@ void Daemon::shutdown() {
         if (kv.second.pidfd >= 0) close(kv.second.pidfd);
     }
     apps_.clear();
+    for (auto &kv : app_conns_) close(kv.first);
+    app_conns_.clear();
+    if (mbox_fd_ >= 0) close(mbox_fd_);
+    mbox_fd_ = -1;
     for (auto &kv : conns_) close(kv.first);
     conns_.clear();
     if (listen_fd_ >= 0) close(listen_fd_);
     listen_fd_ = -1;
-    box_.close_self(true);
     arena_.reset();
     if (sig_fd_ >= 0) close(sig_fd_);
     sig_fd_ = -1;
@@ -382,7 +389,7 @@ int Daemon::loop() {
                 if ((e & EPOLLOUT) && conns_.count((int)tag_id(t))) on_conn_writable((int)tag_id(t));
                 break;
             case T_PIDFD: on_pidfd((pid_t)tag_id(t)); break;
-            case T_APPMQ: on_app_writable((pid_t)tag_id(t)); break;
+            case T_APPCONN: on_app_conn((int)tag_id(t), e); break;
             case T_SIGNAL: on_signal(); break;
             default: break;
             }
@@ -402,12 +409,72 @@ void Daemon::on_signal() {
 }
 
 void Daemon::on_mailbox() {
+    for (;;) {
+        pid_t peer = -1;
+        int fd = mbox_accept(mbox_fd_, &peer);
+        if (fd < 0) break;
+        AppConn c;
+        c.fd = fd;
+        c.peer_pid = peer;
+        app_conns_[fd] = c;
+        ep_add(fd, EPOLLIN, tag(T_APPCONN, (uint64_t)fd));
+    }
+}
+
+void Daemon::close_app_conn(int fd) {
+    auto it = app_conns_.find(fd);
+    if (it == app_conns_.end()) return;
+    const pid_t pid = it->second.app_pid;
+    ep_del(fd);
+    close(fd);
+    app_conns_.erase(it);
+    auto ap = apps_.find(pid);
+    if (pid && ap != apps_.end() && ap->second.fd == fd) {
+        // The connection died with the app (or the app closed it without
+        // MSG_DISCONNECT): reclaim exactly as for a crash.
+        ap->second.fd = -1;
+        OCM_INFO("rank %d: app %d went away without ocm_tini; reclaiming its memory", rank_, (int)pid);
+        app_disconnect(pid, true);
+    }
+}
+
+void Daemon::on_app_conn(int fd, uint32_t events) {
+    auto it = app_conns_.find(fd);
+    if (it == app_conns_.end()) return;
+    if (events & EPOLLOUT) {
+        auto ap = apps_.find(it->second.app_pid);
+        if (ap != apps_.end()) {
+            App &a = ap->second;
+            while (!a.backlog.empty()) {
+                int rc = mbox_send(fd, &a.backlog.front(), kMsgBytes, 0);
+                if (rc != 1) break;
+                a.backlog.pop_front();
+            }
+            if (a.backlog.empty() && a.watching_out) {
+                ep_mod(fd, EPOLLIN, tag(T_APPCONN, (uint64_t)fd));
+                a.watching_out = false;
+            }
+        }
+    }
+    if (!(events & (EPOLLIN | EPOLLHUP | EPOLLERR))) return;
     Msg m;
-    // Drain everything queued (the queue is small; senders block when it is full).
     for (int i = 0; i < 64; i++) {
-        int rc = box_.recv(&m, 0);
-        if (rc != 1) break;
+        int rc = mbox_recv(fd, &m, kMsgBytes, 0);
+        if (rc == 0) return;
+        if (rc < 0) {
+            close_app_conn(fd);
+            return;
+        }
+        // Trust the kernel's view of who is talking, not the record.
+        if (it->second.peer_pid > 0) m.pid = it->second.peer_pid;
+        if (m.type == MSG_CONNECT) {
+            it->second.app_pid = m.pid;
+            app_connect(m, fd);
+            continue;
+        }
         handle_app_msg(m);
+        it = app_conns_.find(fd);
+        if (it == app_conns_.end()) return;
     }
 }
 
@@ -464,21 +531,6 @@ void Daemon::on_pidfd(pid_t pid) {
     app_disconnect(pid, true);
 }
 
-void Daemon::on_app_writable(pid_t pid) {
-    auto it = apps_.find(pid);
-    if (it == apps_.end()) return;
-    App &a = it->second;
-    while (!a.backlog.empty()) {
-        int rc = box_.send(a.mbox, &a.backlog.front(), 0);
-        if (rc != 1) break;
-        a.backlog.pop_front();
-    }
-    if (a.backlog.empty() && a.watching_out) {
-        ep_del(a.mqfd);
-        a.watching_out = false;
-    }
-}
-
 // ---------------------------------------------------------------- routing
 
 void Daemon::send_rank(int r, Msg &m) {
@@ -516,10 +568,10 @@ void Daemon::send_rank(int r, Msg &m) {
 
 void Daemon::send_app(pid_t pid, const Msg &m) {
     auto it = apps_.find(pid);
-    if (it == apps_.end()) return;
+    if (it == apps_.end() || it->second.fd < 0) return;
     App &a = it->second;
     if (a.backlog.empty()) {
-        int rc = box_.send(a.mbox, &m, 0);
+        int rc = mbox_send(a.fd, &m, kMsgBytes, 0);
         if (rc == 1) return;
         if (rc < 0) {
             OCM_WARN("send to app %d failed: %s", (int)pid, last_error());
@@ -527,8 +579,8 @@ void Daemon::send_app(pid_t pid, const Msg &m) {
         }
     }
     a.backlog.push_back(m);
-    if (!a.watching_out && a.mqfd >= 0) {
-        ep_add(a.mqfd, EPOLLOUT, tag(T_APPMQ, (uint64_t)pid));
+    if (!a.watching_out) {
+        ep_mod(a.fd, EPOLLIN | EPOLLOUT, tag(T_APPCONN, (uint64_t)a.fd));
         a.watching_out = true;
     }
 }
@@ -542,7 +594,6 @@ void Daemon::handle_app_msg(Msg &m) {
         return;
     }
     switch (m.type) {
-    case MSG_CONNECT: app_connect(m); break;
     case MSG_DISCONNECT: app_disconnect(m.pid, false); break;
     case MSG_REQ_ALLOC: app_req_alloc(m); break;
     case MSG_REQ_FREE: app_req_free(m); break;
@@ -559,17 +610,15 @@ void Daemon::handle_app_msg(Msg &m) {
     }
 }
 
-void Daemon::app_connect(const Msg &m) {
+void Daemon::app_connect(const Msg &m, int fd) {
     pid_t pid = m.pid;
-    if (apps_.count(pid)) app_disconnect(pid, false);
+    if (apps_.count(pid)) {
+        auto &old = apps_[pid];
+        if (old.fd != fd) app_disconnect(pid, false);
+    }
     App a;
     a.pid = pid;
-    a.mbox = app_mailbox_name(pid, ns_);
-    if (box_.attach(a.mbox, true) != 0) {
-        OCM_WARN("rank %d: cannot attach mailbox of app %d: %s", rank_, (int)pid, last_error());
-        return;
-    }
-    a.mqfd = box_.peer_fd(a.mbox);
+    a.fd = fd;
     a.pidfd = pidfd_open_compat(pid);
     if (a.pidfd >= 0) ep_add(a.pidfd, EPOLLIN, tag(T_PIDFD, (uint64_t)pid));
     apps_[pid] = std::move(a);
@@ -599,14 +648,15 @@ void Daemon::app_disconnect(pid_t pid, bool crashed) {
     for (auto &kv : pending_)
         if (kv.second.pid == pid) kv.second.pid = 0;  // finish silently, then reclaim
     App &a = it->second;
-    if (a.watching_out && a.mqfd >= 0) ep_del(a.mqfd);
+    if (a.watching_out && a.fd >= 0) ep_mod(a.fd, EPOLLIN, tag(T_APPCONN, (uint64_t)a.fd));
     if (a.pidfd >= 0) {
         ep_del(a.pidfd);
         close(a.pidfd);
     }
-    box_.detach(a.mbox);
-    if (crashed) mq_unlink(a.mbox.c_str());
+    auto ac = app_conns_.find(a.fd);
+    if (ac != app_conns_.end()) ac->second.app_pid = 0;  // connection may be reused by a new CONNECT
     apps_.erase(it);
+    (void)crashed;
     OCM_LOG("rank %d: app %d detached (%zu allocations reclaimed)", rank_, (int)pid, mine.size());
 }
 

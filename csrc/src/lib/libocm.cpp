@@ -90,7 +90,7 @@ struct State {
     bool inited = false;
     pid_t pid = 0;
     std::string ns, daemon_mbox;
-    Mailbox box;
+    Channel chan;
     NodeConfig daemon{};
     int daemon_rank = 0;
     int device = -1;
@@ -149,12 +149,12 @@ Msg new_msg(uint32_t type) {
 int rpc(Msg &req, Msg *reply, int timeout_ms) {
     State &s = S();
     req.seq = ++s.seq;
-    if (s.box.send(s.daemon_mbox, &req, timeout_ms) != 1) OCM_FAIL(-1, "mailbox send to daemon failed");
+    if (s.chan.send(&req, kMsgBytes, timeout_ms) != 1) OCM_FAIL(-1, "mailbox send to daemon failed");
     const long deadline = now_ms() + timeout_ms;
     for (;;) {
         long left = deadline - now_ms();
         if (left <= 0) OCM_FAIL(-1, "daemon did not answer %s within %d ms", msg_type_str(req.type), timeout_ms);
-        int rc = s.box.recv(reply, (int)std::min<long>(left, 1000));
+        int rc = s.chan.recv(reply, kMsgBytes, (int)std::min<long>(left, 1000));
         if (rc < 0) return -1;
         if (rc == 0) continue;
         if (reply->seq == req.seq && reply->type != MSG_EXTENT) return 0;
@@ -167,7 +167,7 @@ int recv_seq(Msg *m, uint64_t seq, uint32_t type, int timeout_ms) {
     for (;;) {
         long left = deadline - now_ms();
         if (left <= 0) OCM_FAIL(-1, "timed out waiting for %s", msg_type_str(type));
-        int rc = S().box.recv(m, (int)std::min<long>(left, 1000));
+        int rc = S().chan.recv(m, kMsgBytes, (int)std::min<long>(left, 1000));
         if (rc < 0) return -1;
         if (rc == 1 && m->seq == seq && m->type == type) return 0;
     }
@@ -448,26 +448,20 @@ int ocm_init(void) {
     s.daemon_mbox = daemon_mailbox_name(s.daemon_rank, s.ns);
     s.rpc_timeout_ms = env_int("OCM_RPC_TIMEOUT_MS", 60000);
     const int connect_ms = env_int("OCM_CONNECT_TIMEOUT_MS", 10000);
-    if (s.box.open_self(app_mailbox_name(s.pid, s.ns), kMsgBytes, 8, true) != 0) return -1;
-    // Attach to the daemon mailbox, retrying while it starts (reference: 10 x 10 ms).
+    // Connect to the daemon mailbox, retrying while it starts (reference: 10 x 10 ms).
     long deadline = now_ms() + connect_ms;
-    while (s.box.attach(s.daemon_mbox, false) != 0) {
-        if (now_ms() > deadline) {
-            s.box.close_self(true);
-            OCM_FAIL(-1, "no ocmd mailbox %s (is the daemon running?)", s.daemon_mbox.c_str());
-        }
-        usleep(10000);
-    }
+    if (s.chan.connect(s.daemon_mbox, connect_ms) != 0)
+        OCM_FAIL(-1, "no ocmd mailbox @%s (is the daemon running?)", s.daemon_mbox.c_str());
     Msg reply;
     for (;;) {
         Msg c = new_msg(MSG_CONNECT);
         if (rpc(c, &reply, std::max(1000, connect_ms)) != 0) {
-            s.box.close_self(true);
+            s.chan.close();
             return -1;
         }
         if (reply.err != EAGAIN) break;
         if (now_ms() > deadline) {
-            s.box.close_self(true);
+            s.chan.close();
             OCM_FAIL(-1, "daemon mesh not ready after %d ms", connect_ms);
         }
         usleep(20000);  // mesh still joining
@@ -506,7 +500,7 @@ int ocm_tini(void) {
     std::vector<lib_alloc *> left(s.allocs.begin(), s.allocs.end());
     for (auto *a : left) ocm_free(a);
     Msg d = new_msg(MSG_DISCONNECT);
-    s.box.send(s.daemon_mbox, &d, 1000);
+    s.chan.send(&d, kMsgBytes, 1000);
     for (auto &kv : s.imports) {
         Mapping &m = kv.second;
         DeviceGuard g(s.device);
@@ -520,7 +514,7 @@ int ocm_tini(void) {
         (void)hipStreamDestroy(s.stream);
         s.stream = nullptr;
     }
-    s.box.close_self(true);
+    s.chan.close();
     s.inited = false;
     return 0;
 }

@@ -35,7 +35,8 @@ def test_device_copy_matches_torch(variant, n, soff, doff):
 def test_striped_matches_reference(variant, n_ext, unit, put):
     total = n_ext * unit * 5 + 12345
     rem_off, nbytes = unit // 2 + 3, total - unit - 100
-    exts = [_rand(unit * 6, 100 + i) for i in range(n_ext)]
+    ext_len = ((rem_off + nbytes) // unit // n_ext + 2) * unit
+    exts = [_rand(ext_len, 100 + i) for i in range(n_ext)]
     lin = _rand(nbytes + 64, 7)
     exts_ref = [e.clone() for e in exts]
     lin_ref = lin.clone()
