@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--min-bytes", type=int, default=4096)
     ap.add_argument("--max-bytes", type=int, default=None, help="largest transfer (default 1 GiB; 16 MiB on CPU)")
     ap.add_argument("--pattern", choices=["stripe", "ring"], default="stripe")
+    ap.add_argument("--remote", choices=["auto", "loopback", "host"], default="auto",
+                    help="auto: governor placement; loopback: the rank's own daemon HBM (IPC); host: pinned host tier")
     ap.add_argument("--alloc-samples", type=int, default=200)
     ap.add_argument("--no-characterize", action="store_true")
     ap.add_argument("--json-out", default=None)
@@ -85,6 +87,10 @@ def main() -> int:
 
     ndev = torch.cuda.device_count()
     use_gpu = args.device == "gpu" or (args.device == "auto" and ndev > 0)
+    if use_gpu and os.environ.get("OCM_BENCH_SHARE_GPU"):
+        # Rehearsal mode for a 1-GPU box: every rank (and daemon) on GPU 0, so the
+        # N-rank mesh, placement and IPC paths run without N devices.
+        local_rank = 0
     if use_gpu and local_rank >= ndev:
         print(f"rank {rank}: LOCAL_RANK {local_rank} but only {ndev} GPUs", file=sys.stderr)
         return 2
@@ -138,7 +144,8 @@ def main() -> int:
 
         # ---- the sweep pair: 2 x max + 1 bytes each side (reference: 2 GiB + 1) ----
         pair_bytes = 2 * max_bytes + 1
-        pair = client.alloc(remote_kind, local_bytes=pair_bytes, remote_bytes=pair_bytes)
+        rflags = {"auto": 0, "loopback": api.OCM_ALLOC_LOOPBACK, "host": api.OCM_ALLOC_HOST_TIER}[args.remote]
+        pair = client.alloc(remote_kind, local_bytes=pair_bytes, remote_bytes=pair_bytes, flags=rflags)
         info = pair.remote_info()
 
         # verify: pattern -> put -> clobber -> get -> check
@@ -212,6 +219,7 @@ def main() -> int:
                 "seq_len": max_bytes,
                 "parallelism": f"{args.pattern}{world}",
                 "pattern": args.pattern,
+                "remote": args.remote,
                 "remote_tier": "+".join({1: "host", 2: "hbm"}[t] for t in tiers),
                 "extents_per_pair": len(stats[0]["extents"]),
                 "sizes": f"{args.min_bytes}..{max_bytes} x2",

@@ -100,6 +100,9 @@ struct State {
     std::set<lib_alloc *> allocs;
     XferTuning tuning;
     bool host_engine_kernel = false;
+    uint64_t host_kernel_max = 0;  // measured: SDMA beats the kernel on registered host slabs
+    int sync_mode = 0;             // 0 stream sync, 1 spin on an event, 2 blocking event sync
+    hipEvent_t done = nullptr;
     int rpc_timeout_ms = 60000;
 };
 
@@ -289,7 +292,19 @@ int sync_stream() {
     State &s = S();
     if (!s.stream) return 0;
     DeviceGuard g(s.device);
-    hipError_t e = hipStreamSynchronize(s.stream);
+    hipError_t e = hipSuccess;
+    if (s.sync_mode == 0 || !s.done) {
+        e = hipStreamSynchronize(s.stream);
+    } else {
+        e = hipEventRecord(s.done, s.stream);
+        if (e == hipSuccess && s.sync_mode == 1) {
+            // Spin: lowest completion latency for small one-sided ops.
+            while ((e = hipEventQuery(s.done)) == hipErrorNotReady) {
+            }
+        } else if (e == hipSuccess) {
+            e = hipEventSynchronize(s.done);
+        }
+    }
     if (e != hipSuccess) OCM_FAIL(-1, "stream sync: %s", hipGetErrorString(e));
     return 0;
 }
@@ -313,7 +328,9 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     }
     DeviceGuard guard(s.device);
     const bool lin_dev = lloc == LOC_DEVICE;
-    const bool use_kernel = lin_dev && (a->any_gpu || s.host_engine_kernel);
+    // HBM extents: always the kernel. Host-tier extents: the kernel below
+    // host_kernel_max (lower latency), the DMA engines above (higher peak).
+    const bool use_kernel = lin_dev && (a->any_gpu || s.host_engine_kernel || len <= s.host_kernel_max);
     hipError_t err = hipSuccess;
     if (use_kernel) {
         XferArgs x;
@@ -483,10 +500,27 @@ int ocm_init(void) {
             (void)hipGetLastError();
             OCM_FAIL(-1, "cannot create HIP stream on device %d", s.device);
         }
+        if (hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            s.done = nullptr;
+        }
+        // Map every peer MI355X now: remote extents are read/written by kernels
+        // on this device over xGMI (imports also request lazy peer access).
+        for (int p = 0; p < ndev; p++) {
+            int can = 0;
+            if (p == s.device || hipDeviceCanAccessPeer(&can, s.device, p) != hipSuccess || !can) continue;
+            hipError_t pe = hipDeviceEnablePeerAccess(p, 0);
+            if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
+                OCM_WARN("peer access %d -> %d: %s", s.device, p, hipGetErrorString(pe));
+            (void)hipGetLastError();
+        }
     }
+    s.sync_mode = env_int("OCM_SYNC_MODE", 1);
     s.tuning = xfer_tuning_from_env();
     const char *he = std::getenv("OCM_HOST_ENGINE");
     s.host_engine_kernel = he && !std::strcmp(he, "kernel");
+    if (he && !std::strcmp(he, "sdma")) s.host_kernel_max = 0;
+    if (const char *hk = std::getenv("OCM_HOST_KERNEL_MAX")) s.host_kernel_max = std::strtoull(hk, nullptr, 0);
     s.inited = true;
     OCM_LOG("attached to ocmd rank %d (gpu %d, %u nodes), copying on device %d", s.daemon_rank, s.daemon.gpu,
             s.daemon.num_nodes, s.device);
@@ -833,7 +867,7 @@ void ocm_x_layout(uint64_t out[8]) {
 
 // Striped transfer between raw device pointers on `device` (kernel numerics tests).
 int ocm_x_xfer(int device, void *lin, void **ext, int n_ext, uint64_t unit, uint64_t rem_off, uint64_t len, int put,
-               int variant, int blocks) {
+               int variant, int blocks, int sync) {
     if (n_ext < 1 || n_ext > kXferMaxExtents) return -1;
     DeviceGuard g(device);
     XferArgs x;
@@ -853,6 +887,7 @@ int ocm_x_xfer(int device, void *lin, void **ext, int n_ext, uint64_t unit, uint
     if (variant) t.variant = variant;
     if (blocks) t.max_blocks = blocks;
     if (xfer_launch(x, t, nullptr) != hipSuccess) return -1;
+    if (!sync) return 0;  // caller orders it on the null stream
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 

@@ -154,7 +154,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_device": (i32, []),
             "ocm_last_error": (ctypes.c_char_p, []),
             "ocm_x_layout": (None, [ctypes.POINTER(u64)]),
-            "ocm_x_xfer": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, u64, u64, i32, i32, i32]),
+            "ocm_x_xfer": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, u64, u64, i32, i32, i32, i32]),
             "ocm_x_time_device_copy": (ctypes.c_double, [i32, vp, vp, u64, i32, i32, i32, i32]),
             "ocm_x_time_onesided": (ctypes.c_double, [vp, ctypes.POINTER(OcmParams), i32]),
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),

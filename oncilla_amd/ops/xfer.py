@@ -18,18 +18,19 @@ def _ptr(t) -> int:
 
 
 def xfer(lin, exts: list, unit: int, rem_off: int, nbytes: int, put: bool, variant: int = XFER_AUTO,
-         blocks: int = 0) -> None:
+         blocks: int = 0, sync: bool = True) -> None:
     """Striped one-sided transfer between uint8 tensors on one device.
 
     put=True : lin[0:nbytes] -> striped[rem_off : rem_off+nbytes]
     put=False: striped[rem_off : rem_off+nbytes] -> lin[0:nbytes]
     Unit u of the striped space is exts[u % n][(u // n) * unit + within].
+    sync=False enqueues on the null stream (ordered with torch's default stream).
     """
     lib = api.load()
     n = len(exts)
     arr = (ctypes.c_void_p * n)(*[_ptr(e) for e in exts])
     rc = lib.ocm_x_xfer(lin.device.index or 0, ctypes.c_void_p(_ptr(lin)), arr, n, unit, rem_off, nbytes,
-                        1 if put else 0, variant, blocks)
+                        1 if put else 0, variant, blocks, 1 if sync else 0)
     if rc != 0:
         raise api.OcmError("ocm_x_xfer failed")
 
