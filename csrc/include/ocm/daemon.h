@@ -169,6 +169,9 @@ private:
     std::map<std::pair<uint64_t, int>, OwnedExtent> owned_;
     uint64_t seq_ = 0, local_ids_ = 0;
     int request_timeout_ms_ = 30000;
+    // Fault injection (OCM_FAULT="do_alloc_fail=N,drop_do_alloc=N,crash_after_allocs=N"):
+    int fault_alloc_fail_ = 0, fault_drop_alloc_ = 0, fault_crash_after_ = -1;
+    void parse_faults();
     uint64_t n_alloc_ = 0, n_free_ = 0, n_reclaimed_ = 0, n_spilled_ = 0;
 };
 

@@ -14,6 +14,7 @@
 #pragma once
 #include <cstdint>
 #include <map>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -88,6 +89,8 @@ public:
         int orig_rank;
         int pid;
         Placement placement;
+        std::vector<std::pair<int, uint32_t>> failed;  // (owner, tier) that refused DO_ALLOC
+        int replacements = 0;
     };
     const Entry *find(uint64_t id) const;
 

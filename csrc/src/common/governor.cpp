@@ -145,7 +145,7 @@ Placement Governor::place(const PlaceRequest &r) {
         e.bytes = r.bytes;
         p.extents.push_back(e);
         p.alloc_id = next_id_++;
-        table_[p.alloc_id] = Entry{r.orig_rank, r.app_pid, p};
+        table_[p.alloc_id] = Entry{r.orig_rank, r.app_pid, p, {}, 0};
         table_[p.alloc_id].placement.extents[0].tier = TIER_NONE;  // nothing reserved
         return p;
     }
@@ -216,35 +216,48 @@ Placement Governor::place(const PlaceRequest &r) {
     }
     p.stripe_unit = unit;
     p.alloc_id = next_id_++;
-    table_[p.alloc_id] = Entry{r.orig_rank, r.app_pid, p};
+    table_[p.alloc_id] = Entry{r.orig_rank, r.app_pid, p, {}, 0};
     return p;
 }
 
 bool Governor::replace_extent(uint64_t alloc_id, int idx, int failed_owner, PlacedExtent *out) {
     auto it = table_.find(alloc_id);
     if (it == table_.end() || idx < 0 || idx >= (int)it->second.placement.extents.size()) return false;
-    PlacedExtent &old = it->second.placement.extents[idx];
+    Entry &ent = it->second;
+    PlacedExtent &old = ent.placement.extents[idx];
     reserve(old.owner, old.tier, old.bytes, -1);
-    std::vector<int> order;
+    // Never retry an (owner, tier) that already refused this allocation, and
+    // bound the retries: the directory's view can be wrong (HBM used by other
+    // processes, fragmentation), the owner's arena is authoritative.
+    ent.failed.emplace_back(failed_owner, old.tier);
     const int n = (int)nodes_.size();
-    for (int d = 1; d <= n; d++) {
-        int k = (failed_owner + d) % n;
-        if (k != failed_owner) order.push_back(k);
+    if (++ent.replacements > 2 * n) {
+        old.owner = -1;
+        return false;
     }
+    auto refused = [&](int k, uint32_t t) {
+        for (auto &f : ent.failed)
+            if (f.first == k && f.second == t) return true;
+        return false;
+    };
+    std::vector<int> order;
+    for (int d = 1; d <= n; d++) order.push_back((failed_owner + d) % n);  // failed owner last
     PlacedExtent e;
-    // Try HBM elsewhere first, then any host tier (including the failed owner's).
     bool ok = false;
-    for (int k : order)
-        if (!ok && fits(nodes_[k], TIER_GPU, old.bytes) && old.tier == TIER_GPU) {
-            reserve(k, TIER_GPU, old.bytes, +1);
-            e = PlacedExtent{k, TIER_GPU, old.bytes, false};
-            ok = true;
-        }
-    if (!ok) {
-        order.insert(order.begin(), failed_owner);
+    if (old.tier == TIER_GPU) {
         for (int k : order)
-            if (!ok && fits(nodes_[k], TIER_HOST, old.bytes)) {
-                reserve(k, TIER_HOST, old.bytes, +1);
+            if (!ok && !refused(k, TIER_GPU) && fits(nodes_[k], TIER_GPU, old.bytes)) {
+                e = PlacedExtent{k, TIER_GPU, old.bytes, false};
+                ok = true;
+            }
+    }
+    if (!ok) {
+        // Host tier: the failed owner's own host tier first (same node), then the others.
+        std::vector<int> horder{failed_owner};
+        for (int k : order)
+            if (k != failed_owner) horder.push_back(k);
+        for (int k : horder)
+            if (!ok && !refused(k, TIER_HOST) && fits(nodes_[k], TIER_HOST, old.bytes)) {
                 e = PlacedExtent{k, TIER_HOST, old.bytes, old.tier == TIER_GPU};
                 ok = true;
             }
@@ -253,6 +266,7 @@ bool Governor::replace_extent(uint64_t alloc_id, int idx, int failed_owner, Plac
         old.owner = -1;
         return false;
     }
+    reserve(e.owner, e.tier, e.bytes, +1);
     if (e.spilled) n_spilled_++;
     old = e;
     *out = e;

@@ -17,6 +17,7 @@
 
 #include "../../include/oncillamem.h"
 #include "ocm/log.h"
+#include "ocm/trace.h"
 
 namespace ocm {
 
@@ -194,6 +195,7 @@ int Daemon::init() {
     }
     n_ = nf_.size();
     ns_ = cfg_.ns;
+    parse_faults();
     const NodeEntry &me = nf_.nodes[rank_];
 
     // ---- GPU discovery ----
@@ -588,6 +590,7 @@ void Daemon::send_app(pid_t pid, const Msg &m) {
 // ---------------------------------------------------------------- app messages
 
 void Daemon::handle_app_msg(Msg &m) {
+    TraceRange tr(msg_type_str(m.type));
     OCM_LOG("rank %d <- app %d: %s", rank_, m.pid, msg_type_str(m.type));
     if (m.type != MSG_CONNECT && m.type != MSG_SHUTDOWN && !apps_.count(m.pid)) {
         OCM_WARN("rank %d: %s from unknown app %d ignored", rank_, msg_type_str(m.type), m.pid);
@@ -773,6 +776,7 @@ void Daemon::app_stats(Msg &m) {
 // ---------------------------------------------------------------- mesh messages
 
 void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
+    TraceRange tr(msg_type_str(m.type));
     OCM_LOG("rank %d <- rank %d: %s/%s seq %llu", rank_, m.src_rank, msg_type_str(m.type), msg_status_str(m.status),
             (unsigned long long)m.seq);
     switch (m.type) {
@@ -949,9 +953,42 @@ void Daemon::r0_place_fail(Msg &m) {
     send_rank(m.rank, r);
 }
 
+void Daemon::parse_faults() {
+    const char *f = std::getenv("OCM_FAULT");
+    if (const char *t = std::getenv("OCM_REQUEST_TIMEOUT_MS")) request_timeout_ms_ = std::atoi(t);
+    if (!f || !*f) return;
+    std::string spec = f;
+    size_t pos = 0;
+    while (pos < spec.size()) {
+        size_t end = spec.find(',', pos);
+        std::string item = spec.substr(pos, end == std::string::npos ? std::string::npos : end - pos);
+        size_t eq = item.find('=');
+        std::string k = item.substr(0, eq);
+        int v = eq == std::string::npos ? 1 : std::atoi(item.c_str() + eq + 1);
+        if (k == "do_alloc_fail") fault_alloc_fail_ = v;
+        else if (k == "drop_do_alloc") fault_drop_alloc_ = v;
+        else if (k == "crash_after_allocs") fault_crash_after_ = v;
+        else OCM_WARN("unknown OCM_FAULT item '%s'", item.c_str());
+        if (end == std::string::npos) break;
+        pos = end + 1;
+    }
+    OCM_INFO("rank %d: fault injection: do_alloc_fail=%d drop_do_alloc=%d crash_after_allocs=%d", rank_,
+             fault_alloc_fail_, fault_drop_alloc_, fault_crash_after_);
+}
+
 void Daemon::owner_do_alloc(Msg &m) {
     Region rg = m.u.region;
-    int err = arena_->alloc(rg.tier, rg.bytes, &rg);
+    if (fault_drop_alloc_ > 0) {
+        fault_drop_alloc_--;
+        OCM_WARN("rank %d: fault injection: dropping DO_ALLOC for alloc %llu", rank_, (unsigned long long)rg.alloc_id);
+        return;
+    }
+    if (fault_crash_after_ == 0) {
+        OCM_WARN("rank %d: fault injection: crashing", rank_);
+        _exit(3);
+    }
+    if (fault_crash_after_ > 0) fault_crash_after_--;
+    int err = fault_alloc_fail_ > 0 ? (fault_alloc_fail_--, ENOMEM) : arena_->alloc(rg.tier, rg.bytes, &rg);
     if (err) {
         OCM_LOG("rank %d: DO_ALLOC %llu bytes tier %u failed (%d)", rank_, (unsigned long long)rg.bytes, rg.tier, err);
         Msg f = m;
@@ -1169,8 +1206,14 @@ void Daemon::origin_do_free_resp(Msg &m) {
 
 void Daemon::fail_pending_on(int rank) {
     std::vector<uint64_t> dead;
-    for (auto &kv : pending_)
-        if (kv.second.awaiting.count(rank)) dead.push_back(kv.first);
+    for (auto &kv : pending_) {
+        const Pending &p = kv.second;
+        // Owners of not-yet-answered extents are unknown to the origin (rank0
+        // picked them), so an unfinished allocation may wait on the dead rank:
+        // fail it now; late successes are freed by origin_do_alloc_resp.
+        const bool open_alloc = p.type == MSG_REQ_ALLOC && (p.expect == 0 || p.got < p.expect);
+        if (p.awaiting.count(rank) || open_alloc) dead.push_back(kv.first);
+    }
     for (uint64_t s : dead) {
         auto it = pending_.find(s);
         if (it == pending_.end()) continue;

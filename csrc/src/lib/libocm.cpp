@@ -33,6 +33,7 @@
 #include "ocm/log.h"
 #include "ocm/msg.h"
 #include "ocm/pmsg.h"
+#include "ocm/trace.h"
 #include "ocm/xfer.h"
 
 using namespace ocm;
@@ -102,6 +103,7 @@ struct State {
     bool host_engine_kernel = false;
     uint64_t host_kernel_max = 0;  // measured: SDMA beats the kernel on registered host slabs
     int sync_mode = 0;             // 0 stream sync, 1 spin on an event, 2 blocking event sync
+    OpCounters ctr;
     hipEvent_t done = nullptr;
     int rpc_timeout_ms = 60000;
 };
@@ -550,12 +552,29 @@ int ocm_tini(void) {
     }
     s.chan.close();
     s.inited = false;
+    trace_flush("app");
     return 0;
 }
 
 ocm_alloc_t ocm_alloc(ocm_alloc_param_t p) { return ocm_alloc_ex(p, nullptr); }
 
+static ocm_alloc_t alloc_impl(ocm_alloc_param_t p, const struct ocm_alloc_ex_params *ex);
+
 ocm_alloc_t ocm_alloc_ex(ocm_alloc_param_t p, const struct ocm_alloc_ex_params *ex) {
+    TraceRange tr("ocm_alloc");
+    const uint64_t t0 = now_ns();
+    ocm_alloc_t a = alloc_impl(p, ex);
+    const uint64_t t1 = now_ns();
+    State &s = S();
+    if (a) {
+        s.ctr.n_alloc++;
+        s.ctr.ns_alloc += t1 - t0;
+    }
+    trace_op("alloc", p ? (p->rem_alloc_bytes ? p->rem_alloc_bytes : p->local_alloc_bytes) : 0, t0, t1, a ? 0 : -1);
+    return a;
+}
+
+static ocm_alloc_t alloc_impl(ocm_alloc_param_t p, const struct ocm_alloc_ex_params *ex) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (!s.inited) OCM_FAIL(nullptr, "ocm_alloc before ocm_init");
@@ -660,7 +679,20 @@ ocm_alloc_t ocm_alloc_ex(ocm_alloc_param_t p, const struct ocm_alloc_ex_params *
     return a;
 }
 
+static int free_impl(ocm_alloc_t a);
+
 int ocm_free(ocm_alloc_t a) {
+    TraceRange tr("ocm_free");
+    const uint64_t t0 = now_ns();
+    int rc = free_impl(a);
+    const uint64_t t1 = now_ns();
+    S().ctr.n_free += rc == 0;
+    S().ctr.ns_free += t1 - t0;
+    trace_op("free", 0, t0, t1, rc);
+    return rc;
+}
+
+static int free_impl(ocm_alloc_t a) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (!a || !s.allocs.count(a)) OCM_FAIL(-1, "ocm_free: unknown allocation");
@@ -697,7 +729,25 @@ int ocm_remote_sz(ocm_alloc_t a, size_t *len) {
     return 0;
 }
 
-int ocm_copy_onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
+static int onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async);
+
+static int ocm_copy_onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
+    const bool put = p && p->op_flag != 0;
+    TraceRange tr(put ? "ocm_put" : "ocm_get");
+    const uint64_t t0 = now_ns();
+    int rc = onesided_impl(a, p, async);
+    const uint64_t t1 = now_ns();
+    if (rc == 0 && p) {
+        OpCounters &c = S().ctr;
+        (put ? c.n_put : c.n_get)++;
+        (put ? c.bytes_put : c.bytes_get) += p->bytes;
+        (put ? c.ns_put : c.ns_get) += t1 - t0;
+    }
+    trace_op(put ? "put" : "get", p ? p->bytes : 0, t0, t1, rc);
+    return rc;
+}
+
+static int onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (!a || !p) OCM_FAIL(-1, "ocm_copy_onesided: NULL argument");
@@ -726,7 +776,22 @@ int ocm_wait(ocm_alloc_t a) {
 
 static bool range_ok(uint64_t off, uint64_t n, uint64_t cap) { return off <= cap && n <= cap - off; }
 
+static int copy_impl(ocm_alloc_t dst, ocm_alloc_t src, ocm_param_t p);
+
 int ocm_copy(ocm_alloc_t dst, ocm_alloc_t src, ocm_param_t p) {
+    TraceRange tr("ocm_copy");
+    const uint64_t t0 = now_ns();
+    int rc = copy_impl(dst, src, p);
+    const uint64_t t1 = now_ns();
+    if (rc == 0 && p) {
+        S().ctr.n_copy++;
+        S().ctr.bytes_copy += p->bytes;
+    }
+    trace_op("copy", p ? p->bytes : 0, t0, t1, rc);
+    return rc;
+}
+
+static int copy_impl(ocm_alloc_t dst, ocm_alloc_t src, ocm_param_t p) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (!dst || !src || !p) OCM_FAIL(-1, "ocm_copy: NULL argument");
@@ -853,6 +918,14 @@ int ocm_device(void) { return S().inited ? S().device : -1; }
 const char *ocm_last_error(void) { return last_error(); }
 
 // ---------------- internal hooks for tests and benchmarks (not part of the ABI) ----------------
+
+// Per-process operation counters (see ocm/trace.h): 12 x uint64.
+void ocm_x_counters(uint64_t out[12]) {
+    const OpCounters &c = S().ctr;
+    const uint64_t v[12] = {c.n_put, c.n_get, c.bytes_put, c.bytes_get, c.n_alloc, c.n_free,
+                            c.n_copy, c.bytes_copy, c.ns_put, c.ns_get, c.ns_alloc, c.ns_free};
+    std::memcpy(out, v, sizeof(v));
+}
 
 void ocm_x_layout(uint64_t out[8]) {
     out[0] = sizeof(Msg);

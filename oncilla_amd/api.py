@@ -158,6 +158,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_time_device_copy": (ctypes.c_double, [i32, vp, vp, u64, i32, i32, i32, i32]),
             "ocm_x_time_onesided": (ctypes.c_double, [vp, ctypes.POINTER(OcmParams), i32]),
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
+            "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(lib, name)
@@ -170,6 +171,17 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
 def last_error() -> str:
     e = load().ocm_last_error()
     return e.decode(errors="replace") if e else ""
+
+
+COUNTER_KEYS = ["n_put", "n_get", "bytes_put", "bytes_get", "n_alloc", "n_free", "n_copy", "bytes_copy", "ns_put",
+                "ns_get", "ns_alloc", "ns_free"]
+
+
+def counters() -> dict:
+    """This process's libocm operation counters."""
+    out = (ctypes.c_uint64 * 12)()
+    load().ocm_x_counters(out)
+    return dict(zip(COUNTER_KEYS, [int(v) for v in out]))
 
 
 def layout() -> dict:

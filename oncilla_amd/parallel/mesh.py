@@ -69,13 +69,15 @@ class Mesh:
 
     def __init__(self, n: int, gpus: Optional[Sequence[Optional[int]]] = None, ns: Optional[str] = None,
                  policy: str = "ring", extra_args: Sequence[str] = (), env: Optional[dict] = None,
-                 workdir: Optional[str] = None, ports: Optional[Sequence[int]] = None, ranks: Optional[Sequence[int]] = None):
+                 workdir: Optional[str] = None, ports: Optional[Sequence[int]] = None, ranks: Optional[Sequence[int]] = None,
+                 rank_env: Optional[dict] = None):
         self.n = n
         self.gpus = list(gpus) if gpus is not None else [None] * n
         self.ns = ns or f"m{uuid.uuid4().hex[:10]}"
         self.policy = policy
         self.extra_args = list(extra_args)
         self.env = dict(env or {})
+        self.rank_env = dict(rank_env or {})  # rank -> extra env (fault injection)
         self.workdir = workdir or tempfile.mkdtemp(prefix=f"ocm_{self.ns}_")
         self.ports = list(ports) if ports is not None else free_ports(n)
         self.ranks = list(ranks) if ranks is not None else list(range(n))  # which ranks THIS process launches
@@ -101,6 +103,7 @@ class Mesh:
             args += self.extra_args
             env = dict(os.environ)
             env.update(self.env)
+            env.update(self.rank_env.get(r, {}))
             env["OCM_NS"] = self.ns
             with open(log, "w") as lf:
                 proc = subprocess.Popen(args, stdout=lf, stderr=subprocess.STDOUT, env=env, start_new_session=True)
