@@ -42,6 +42,9 @@ struct XferTuning {
     bool nontemporal = true; // nt stores on the destination
 };
 
+// Validate and fill tile_shift (xfer_launch does this itself; the service needs it up front).
+hipError_t xfer_normalize(XferArgs &a);
+
 // Launch one transfer on `stream`. Returns hipSuccess or the launch error.
 hipError_t xfer_launch(const XferArgs &a, const XferTuning &t, hipStream_t stream);
 
@@ -50,6 +53,27 @@ hipError_t xfer_copy(void *dst, const void *src, uint64_t bytes, const XferTunin
 
 // Default tuning from the environment (OCM_XFER_VARIANT, OCM_XFER_BLOCKS, OCM_XFER_NT).
 XferTuning xfer_tuning_from_env();
+
+// ---- persistent copy service (low-latency small one-sided ops) ----
+// One resident workgroup polls a doorbell in host-pinned coherent memory. The
+// host writes the transfer arguments, then bumps `seq` (release); the kernel
+// copies, makes the bytes visible system-wide (acq_rel fence), and publishes
+// `done = seq`. Bounded: the kernel exits on kServiceStop or after `idle_ticks`
+// of s_memrealtime (100 MHz) without work; `exited` records that it left.
+constexpr unsigned long long kServiceStop = ~0ull;
+
+struct alignas(64) ServiceSlot {
+    unsigned long long seq;           // host -> device, written last
+    unsigned long long pad0[7];
+    XferArgs args;                    // host -> device
+    unsigned long long pad1[3];
+    unsigned long long done;          // device -> host (own cache line)
+    unsigned long long exited;        // device -> host: first seq NOT served when it left
+    unsigned long long pad2[6];
+};
+
+hipError_t service_launch(ServiceSlot *slot, unsigned long long first_seq, unsigned long long idle_ticks,
+                          hipStream_t stream);
 
 // Deterministic 32-bit word pattern (word i of a buffer) for data verification.
 hipError_t pattern_fill(void *p, uint64_t words, uint64_t first_word, uint32_t seed, hipStream_t stream);

@@ -213,15 +213,20 @@ XferTuning xfer_tuning_from_env() {
     return t;
 }
 
-hipError_t xfer_launch(const XferArgs &in, const XferTuning &t, hipStream_t stream) {
-    if (in.len == 0) return hipSuccess;
-    if (in.n_ext < 1 || in.n_ext > (uint32_t)kXferMaxExtents) return hipErrorInvalidValue;
-    XferArgs a = in;
+hipError_t xfer_normalize(XferArgs &a) {
+    if (a.n_ext < 1 || a.n_ext > (uint32_t)kXferMaxExtents) return hipErrorInvalidValue;
     a.tile_shift = kTileShift;
     if (a.n_ext > 1) {
-        if (a.unit_shift < kTileShift) a.tile_shift = a.unit_shift;  // tile must not cross a stripe unit
         if (a.unit_shift < 4) return hipErrorInvalidValue;
+        if (a.unit_shift < kTileShift) a.tile_shift = a.unit_shift;  // tile must not cross a stripe unit
     }
+    return hipSuccess;
+}
+
+hipError_t xfer_launch(const XferArgs &in, const XferTuning &t, hipStream_t stream) {
+    if (in.len == 0) return hipSuccess;
+    XferArgs a = in;
+    if (xfer_normalize(a) != hipSuccess) return hipErrorInvalidValue;
     const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
     const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - (a.rem_off & ~tile_mask)) >> a.tile_shift;
     int variant = t.variant;
@@ -254,6 +259,70 @@ hipError_t xfer_copy(void *dst, const void *src, uint64_t bytes, const XferTunin
     a.n_ext = 1;
     a.put = 1;
     return xfer_launch(a, t, stream);
+}
+
+// ---- persistent copy service ----
+
+namespace {
+
+constexpr int kArgWords = (sizeof(XferArgs) + 7) / 8;
+static_assert(kArgWords <= 64, "args must fit one wave's loads");
+
+__global__ __launch_bounds__(kThreads) void service_kernel(ServiceSlot *slot, unsigned long long first_seq,
+                                                           unsigned long long idle_ticks) {
+    __shared__ __attribute__((aligned(16))) unsigned long long sh[kArgWords + 2];
+    unsigned long long expect = first_seq;
+    unsigned long long idle_start = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (threadIdx.x == 0) {
+            unsigned long long s;
+            for (;;) {
+                s = __hip_atomic_load(&slot->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (s == expect || s == kServiceStop) break;
+                if (__builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks) {
+                    s = kServiceStop;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);  // ~0.2 us between PCIe polls
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // order the argument loads after the doorbell
+            sh[kArgWords] = s;
+        }
+        __syncthreads();
+        const unsigned long long s = sh[kArgWords];
+        if (s == kServiceStop) break;
+        // The arguments live in host memory: fetch them with one wave, in parallel.
+        if (threadIdx.x < kArgWords)
+            sh[threadIdx.x] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(&slot->args) + threadIdx.x,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();
+        XferArgs a = *reinterpret_cast<const XferArgs *>(sh);
+        const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
+        const uint64_t first = a.rem_off & ~tile_mask;
+        const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;
+        for (uint64_t ti = 0; ti < ntiles; ti++) {
+            TileSpan sp = tile_span(a, ti, first);
+            span_copy<false>(sp.dst, sp.src, sp.n);
+        }
+        // Make the bytes visible to the host, other kernels and DMA, and drop
+        // any cached copies before the next request (acq_rel, system scope).
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(&slot->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            idle_start = __builtin_amdgcn_s_memrealtime();
+        }
+        expect++;
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(&slot->exited, expect, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace
+
+hipError_t service_launch(ServiceSlot *slot, unsigned long long first_seq, unsigned long long idle_ticks,
+                          hipStream_t stream) {
+    hipLaunchKernelGGL(service_kernel, dim3(1), dim3(kThreads), 0, stream, slot, first_seq, idle_ticks);
+    return hipGetLastError();
 }
 
 // ---- verification patterns (benchmarks and tests check data without a host round trip) ----

@@ -107,3 +107,43 @@ def test_bench_gpu_small():
     assert r.returncode == 0, r.stderr[-4000:]
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert res["config"]["device"] == "gpu" and res["value"] > 0
+
+
+@pytest.mark.parametrize("policy", ["ring", "stripe"])
+def test_copy_service_small_ops(mesh_factory, policy):
+    """Small blocking put/get run on the resident copy service; interleave them
+    with launch-path transfers and fills so stale caches would show."""
+    import time
+
+    m = mesh_factory(4, gpus=[0, 0, 0, 0], policy=policy)
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 8 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, stripe_unit=64 << 10)
+        before = api.counters()
+        for i, (size, loff, roff) in enumerate([(4, 0, 0), (4096, 0, 4096), (4096 + 12, 64, 65536 - 100),
+                                                (65536, 4096, 3 << 16), (200000, 8, 1 << 20), (256 << 10, 0, 0)]):
+            seed = 100 + i
+            a.fill(seed=seed)                     # launch path writes the local half
+            a.put(loff, roff, size)               # service reads it
+            a.fill(seed=0)
+            a.get(loff, roff, size)               # service writes the local half
+            nb = (size // 4) * 4
+            assert a.check(seed=seed, offset=loff - loff % 4 + (4 if loff % 4 else 0),
+                           nbytes=max(0, nb - 8), first_word=(loff + 3) // 4) == 0, (size, loff, roff)
+            # big put (launch path) then small get (service) of what it just wrote
+            a.fill(seed=seed + 50)
+            a.put(0, 0, n)
+            a.fill(seed=0)
+            a.get(0, 0, 4096)
+            assert a.check(seed=seed + 50, nbytes=4096) == 0
+        for k in range(5):
+            time.sleep(0.02)                      # service idles out (2 ms); the next op relaunches it
+            a.fill(seed=7 + k)
+            t0 = time.perf_counter()
+            a.put(0, 0, 4096)
+            assert time.perf_counter() - t0 < 1.0, "relaunch after idle exit stalled"
+            a.fill(seed=0)
+            a.get(0, 0, 4096)
+            assert a.check(seed=7 + k, nbytes=4096) == 0
+        assert api.counters()["n_put"] > before["n_put"]
+        a.free()
