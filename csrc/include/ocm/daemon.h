@@ -27,6 +27,7 @@
 #include "ocm/nodefile.h"
 #include "ocm/pmsg.h"
 #include "ocm/sock.h"
+#include "ocm/tick.h"
 
 namespace ocm {
 
@@ -46,6 +47,7 @@ struct DaemonConfig {
     bool zero_on_alloc = false;
     std::string ready_file;
     std::string bind_ip;             // default: 0.0.0.0
+    std::string ctrl = "tcp";        // daemon<->daemon records: tcp | rccl | socket (tick transports)
 };
 
 int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err);
@@ -142,6 +144,9 @@ private:
     void fail_pending_on(int rank);
     void peer_lost(int rank);
     void sweep_timeouts();
+    void start_tick(const uint8_t *id);
+    void on_tick();
+    void send_tcp(int r, Msg &m);
 
     NodeConfig my_config() const;
     void check_ready();
@@ -169,6 +174,7 @@ private:
     std::map<std::pair<uint64_t, int>, OwnedExtent> owned_;
     uint64_t seq_ = 0, local_ids_ = 0;
     int request_timeout_ms_ = 30000;
+    std::unique_ptr<TickTransport> tick_;
     // Fault injection (OCM_FAULT="do_alloc_fail=N,drop_do_alloc=N,crash_after_allocs=N"):
     int fault_alloc_fail_ = 0, fault_drop_alloc_ = 0, fault_crash_after_ = -1;
     void parse_faults();

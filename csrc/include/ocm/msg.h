@@ -38,6 +38,8 @@ enum MsgType : uint32_t {
     MSG_APP_DEAD,         // origin daemon -> rank0: app crashed, drop its directory entries
     MSG_SHUTDOWN,         // any -> daemon: orderly exit
     MSG_PING,             // liveness / latency probe
+    MSG_TICK_START,       // rank0 -> all (TCP): start the tick transport; u.raw = ncclUniqueId
+    MSG_TICK_WAKE,        // any -> all (TCP): join tick number u.req.bytes
     MSG_MAX
 };
 
@@ -99,7 +101,7 @@ struct NodeConfig {
     uint32_t num_nodes;
     uint32_t num_apps;
     uint32_t n_alloc, n_free, n_reclaimed, n_spilled, n_slabs;
-    uint32_t pad;
+    uint32_t ticks;        // allgather ticks of the control transport (0 on TCP)
 };
 
 struct Msg {

@@ -1,0 +1,112 @@
+// Tick transport: daemon<->daemon control records carried by a collective.
+//
+// the reference's control plane was one TCP connection per
+// RPC (src/mem.c:62-111) plus "start the master first"; the MI355X design
+// carries the 160-byte records over RCCL on xGMI. RCCL operations must be
+// matched on every rank, so records move in *ticks*: every daemon contributes
+// one fixed slot (up to kTickMsgs addressed records) to an allgather, then
+// keeps the records addressed to it. An idle mesh does not tick; a daemon that
+// posts into an idle mesh nudges its peers awake (a 1-byte doorbell on the
+// existing mesh sockets) and everybody ticks back-to-back while traffic lasts.
+//
+// The collective is pluggable: RcclCollective (ncclAllGather on the daemon's
+// MI355X) in production, SocketCollective (ring allgather over abstract unix
+// sockets) so the tick protocol itself is exercised multi-rank on CPU. Any
+// collective error disables the transport; the daemon falls back to TCP links.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ocm/msg.h"
+
+namespace ocm {
+
+constexpr int kTickMsgs = 8;
+
+struct TickRecord {
+    int32_t dest;      // destination rank
+    int32_t pad;
+    Msg msg;
+};
+
+struct TickSlot {
+    uint32_t count;    // records used in this slot
+    uint32_t busy;     // sender still has queued records (keep ticking)
+    TickRecord rec[kTickMsgs];
+};
+static_assert(sizeof(TickRecord) == 168, "tick record layout");
+
+class Collective {
+public:
+    virtual ~Collective() = default;
+    // recv = concat over ranks of every rank's `bytes`-byte send buffer. 0 ok.
+    virtual int allgather(const void *send, void *recv, size_t bytes) = 0;
+    virtual void abort() {}
+    virtual const char *name() const = 0;
+};
+
+// Collective constructors block until every rank joined; `cancel` aborts them.
+// RCCL over xGMI. `id` is the ncclUniqueId (128 bytes) chosen by rank0.
+std::unique_ptr<Collective> make_rccl_collective(int gpu, int rank, int nranks, const uint8_t *id, std::string *err,
+                                                 const std::atomic<bool> *cancel);
+// Fill a fresh ncclUniqueId (rank0). Returns 0 on success.
+int rccl_unique_id(uint8_t out[128], std::string *err);
+// Ring allgather over abstract unix sockets (same host), for CPU meshes/tests.
+std::unique_ptr<Collective> make_socket_collective(const std::string &ns, int rank, int nranks, std::string *err,
+                                                   const std::atomic<bool> *cancel);
+
+using CollectiveFactory = std::function<std::unique_ptr<Collective>(std::string *err, const std::atomic<bool> *cancel)>;
+
+class TickTransport {
+public:
+    // The collective is created on the tick thread (its construction blocks
+    // until every rank joined).
+    TickTransport(int rank, int nranks, CollectiveFactory factory);
+    ~TickTransport();
+    void start();
+    void stop();
+    void abort();          // a peer died: stop ticking, fall back to TCP
+    bool up() const { return up_.load() && !failed_.load(); }
+    // Queue a record for `dest`. Returns false once the transport has failed.
+    bool post(int dest, const Msg &m);
+    // Records delivered to this rank (drained by the event loop).
+    std::vector<Msg> drain();
+    // Readable when drain() has records, a wake-up must be announced, or the
+    // transport failed.
+    int event_fd() const { return efd_; }
+    bool failed() const { return failed_.load(); }
+    // A peer asked everybody to perform tick number `tick` (1-based).
+    void wake_at(uint64_t tick);
+    // True once when this rank starts a burst from idle; `tick` = the tick
+    // number the peers must join (broadcast it to them).
+    bool take_announce(uint64_t *tick);
+    // Records still queued when the transport failed (re-send them over TCP).
+    std::vector<TickRecord> take_unsent();
+    uint64_t ticks() const { return ticks_.load(); }
+    const char *collective_name() const { return coll_ ? coll_->name() : "none"; }
+
+private:
+    void run();
+    int rank_, n_;
+    CollectiveFactory factory_;
+    std::unique_ptr<Collective> coll_;
+    std::thread th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<TickRecord> out_;
+    std::vector<Msg> in_;
+    std::atomic<bool> stop_{false}, failed_{false}, announce_{false}, up_{false};
+    std::atomic<uint64_t> ticks_{0}, wake_upto_{0};
+    int efd_ = -1;
+    std::vector<TickSlot> recv_;
+};
+
+}  // namespace ocm

@@ -124,7 +124,8 @@ struct ocm_daemon_stats {
     uint64_t host_capacity, host_used;
     uint64_t n_alloc, n_free, n_reclaimed, n_spilled;
     uint64_t n_slabs;
-    uint64_t reserved[4];
+    uint64_t ctrl_ticks;   /* allgather ticks of the RCCL/socket control transport (0 on TCP) */
+    uint64_t reserved[3];
 };
 
 ocm_alloc_t ocm_alloc_ex(ocm_alloc_param_t alloc_param, const struct ocm_alloc_ex_params *ex);

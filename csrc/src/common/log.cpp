@@ -69,6 +69,8 @@ const char *msg_type_str(uint32_t t) {
     case MSG_APP_DEAD: return "MSG_APP_DEAD";
     case MSG_SHUTDOWN: return "MSG_SHUTDOWN";
     case MSG_PING: return "MSG_PING";
+    case MSG_TICK_START: return "MSG_TICK_START";
+    case MSG_TICK_WAKE: return "MSG_TICK_WAKE";
     default: return "INVALID MSG TYPE";
     }
 }

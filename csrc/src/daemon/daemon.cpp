@@ -23,7 +23,7 @@ namespace ocm {
 
 namespace {
 
-enum Tag : uint64_t { T_MBOX = 1, T_LISTEN, T_CONN, T_PIDFD, T_APPCONN, T_SIGNAL };
+enum Tag : uint64_t { T_MBOX = 1, T_LISTEN, T_CONN, T_PIDFD, T_APPCONN, T_SIGNAL, T_TICK };
 inline uint64_t tag(Tag k, uint64_t id) { return (static_cast<uint64_t>(k) << 56) | (id & 0x00ffffffffffffffull); }
 inline Tag tag_kind(uint64_t t) { return static_cast<Tag>(t >> 56); }
 inline uint64_t tag_id(uint64_t t) { return t & 0x00ffffffffffffffull; }
@@ -79,6 +79,7 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
     if (const char *v = env("OCM_HOST_FRACTION")) cfg->host_fraction = std::atof(v);
     if (env("OCM_ZERO_ON_ALLOC")) cfg->zero_on_alloc = true;
     if (env("OCM_NO_GPU")) cfg->gpu = -1;
+    if (const char *v = env("OCM_CTRL")) cfg->ctrl = v;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto val = [&](std::string *out) {
@@ -120,6 +121,12 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
             if (!val(&cfg->ready_file)) return -1;
         } else if (a == "--bind") {
             if (!val(&cfg->bind_ip)) return -1;
+        } else if (a == "--ctrl") {
+            if (!val(&cfg->ctrl)) return -1;
+            if (cfg->ctrl != "tcp" && cfg->ctrl != "rccl" && cfg->ctrl != "socket") {
+                *err = "--ctrl must be tcp, rccl or socket";
+                return -1;
+            }
         } else if (a == "--zero") {
             cfg->zero_on_alloc = true;
         } else if (!a.empty() && a[0] == '-') {
@@ -179,6 +186,7 @@ NodeConfig Daemon::my_config() const {
     c.n_reclaimed = (uint32_t)n_reclaimed_;
     c.n_spilled = (uint32_t)(gov_ ? gov_->spilled_count() : n_spilled_);
     c.n_slabs = (uint32_t)(arena_ ? arena_->num_slabs() : 0);
+    c.ticks = (uint32_t)(tick_ ? tick_->ticks() : 0);
     return c;
 }
 
@@ -320,6 +328,21 @@ void Daemon::check_ready() {
         if (!joined_[r]) return;
     ready_ = true;
     OCM_LOG("rank %d: mesh complete (%d nodes)", rank_, n_);
+    if (rank_ == 0 && cfg_.ctrl != "tcp") {
+        // Bootstrap the tick transport: rank0 picks the RCCL id and tells everybody over TCP.
+        Msg t;
+        std::memset(&t, 0, sizeof(t));
+        t.type = MSG_TICK_START;
+        t.status = MSG_REQUEST;
+        t.rank = 0;
+        std::string err;
+        if (cfg_.ctrl == "rccl" && rccl_unique_id(t.u.raw, &err) != 0) {
+            OCM_WARN("rccl control plane unavailable (%s); staying on TCP", err.c_str());
+        } else {
+            for (int r = 1; r < n_; r++) send_tcp(r, t);
+            start_tick(t.u.raw);
+        }
+    }
     if (!cfg_.ready_file.empty()) {
         std::string tmp = cfg_.ready_file + ".tmp";
         std::ofstream f(tmp);
@@ -332,6 +355,10 @@ void Daemon::check_ready() {
 
 void Daemon::shutdown() {
     if (ep_ < 0) return;
+    if (tick_) {
+        tick_->stop();
+        tick_.reset();
+    }
     for (auto &kv : apps_) {
         if (kv.second.pidfd >= 0) close(kv.second.pidfd);
     }
@@ -393,6 +420,7 @@ int Daemon::loop() {
             case T_PIDFD: on_pidfd((pid_t)tag_id(t)); break;
             case T_APPCONN: on_app_conn((int)tag_id(t), e); break;
             case T_SIGNAL: on_signal(); break;
+            case T_TICK: on_tick(); break;
             default: break;
             }
         }
@@ -537,10 +565,23 @@ void Daemon::on_pidfd(pid_t pid) {
 
 void Daemon::send_rank(int r, Msg &m) {
     m.src_rank = rank_;
+    // OCM_TICK_SELF=1 (tests): self-addressed records also ride the tick
+    // transport, so a 1-GPU box exercises the real ncclAllGather path.
+    static const bool tick_self = std::getenv("OCM_TICK_SELF") != nullptr;
+    if (r == rank_ && !(tick_self && tick_ && tick_->up())) {
+        self_q_.push_back(m);
+        return;
+    }
+    if (tick_ && tick_->up() && r >= 0 && r < n_ && tick_->post(r, m)) return;
     if (r == rank_) {
         self_q_.push_back(m);
         return;
     }
+    send_tcp(r, m);
+}
+
+void Daemon::send_tcp(int r, Msg &m) {
+    m.src_rank = rank_;
     if (r < 0 || r >= n_ || peer_fd_[r] < 0) {
         OCM_WARN("rank %d: no link to rank %d for %s", rank_, r, msg_type_str(m.type));
         // Bounce the request back as a local failure so the origin can answer the app.
@@ -839,6 +880,12 @@ void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
             if (it->second.pid) send_app(it->second.pid, r);
             pending_.erase(it);
         }
+        break;
+    case MSG_TICK_START:
+        if (!tick_ && cfg_.ctrl != "tcp") start_tick(m.u.raw);
+        break;
+    case MSG_TICK_WAKE:
+        if (tick_) tick_->wake_at(m.u.req.bytes);
         break;
     case MSG_SHUTDOWN: stop_ = true; break;
     case MSG_PING:
@@ -1245,6 +1292,7 @@ void Daemon::fail_pending_on(int rank) {
 
 void Daemon::peer_lost(int rank) {
     OCM_WARN("rank %d: lost link to rank %d", rank_, rank);
+    if (tick_) tick_->abort();  // the dead rank will never join another tick
     if (gov_) gov_->mark_dead(rank);
     fail_pending_on(rank);
     // Extents we own for allocations that originated at the dead daemon stay
@@ -1293,6 +1341,52 @@ void Daemon::sweep_timeouts() {
             }
             pending_.erase(it);
         }
+    }
+}
+
+void Daemon::start_tick(const uint8_t *id) {
+    if (tick_) return;
+    CollectiveFactory f;
+    if (cfg_.ctrl == "rccl") {
+        if (gpu_ < 0) {
+            OCM_WARN("rank %d: --ctrl rccl needs a GPU; staying on TCP", rank_);
+            return;
+        }
+        std::vector<uint8_t> uid(id, id + 128);
+        const int gpu = gpu_, rank = rank_, n = n_;
+        f = [uid, gpu, rank, n](std::string *err, const std::atomic<bool> *cancel) {
+            return make_rccl_collective(gpu, rank, n, uid.data(), err, cancel);
+        };
+    } else {
+        const std::string ns = ns_;
+        const int rank = rank_, n = n_;
+        f = [ns, rank, n](std::string *err, const std::atomic<bool> *cancel) {
+            return make_socket_collective(ns, rank, n, err, cancel);
+        };
+    }
+    tick_ = std::make_unique<TickTransport>(rank_, n_, f);
+    ep_add(tick_->event_fd(), EPOLLIN, tag(T_TICK, 0));
+    tick_->start();
+    OCM_INFO("rank %d: control records will ride the %s tick transport", rank_, cfg_.ctrl.c_str());
+}
+
+void Daemon::on_tick() {
+    if (!tick_) return;
+    for (Msg &m : tick_->drain()) handle_mesh_msg(m, -1);
+    uint64_t t = 0;
+    if (tick_->take_announce(&t)) {
+        // Wake the peers for the tick this rank is starting from idle.
+        Msg w;
+        std::memset(&w, 0, sizeof(w));
+        w.type = MSG_TICK_WAKE;
+        w.status = MSG_REQUEST;
+        w.rank = rank_;
+        w.u.req.bytes = t;
+        for (int r = 0; r < n_; r++)
+            if (r != rank_) send_tcp(r, w);
+    }
+    if (tick_->failed()) {
+        for (TickRecord &rec : tick_->take_unsent()) send_tcp(rec.dest, rec.msg);
     }
 }
 

@@ -1026,6 +1026,7 @@ int ocm_stats(int rank, struct ocm_daemon_stats *out) {
     out->n_reclaimed = c.n_reclaimed;
     out->n_spilled = c.n_spilled;
     out->n_slabs = c.n_slabs;
+    out->ctrl_ticks = c.ticks;
     return 0;
 }
 

@@ -103,7 +103,8 @@ class OcmDaemonStats(ctypes.Structure):
         ("n_reclaimed", ctypes.c_uint64),
         ("n_spilled", ctypes.c_uint64),
         ("n_slabs", ctypes.c_uint64),
-        ("reserved", ctypes.c_uint64 * 4),
+        ("ctrl_ticks", ctypes.c_uint64),
+        ("reserved", ctypes.c_uint64 * 3),
     ]
 
     def as_dict(self) -> dict:

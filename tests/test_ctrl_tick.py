@@ -1,0 +1,116 @@
+"""Tick control transport (daemon records over a collective).
+On CPU the collective is the socket ring; on a GPU box `--ctrl rccl` uses
+ncclAllGather over xGMI (N=1 on a single-GPU box)."""
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+from oncilla_amd import api
+
+
+@pytest.fixture(autouse=True)
+def _cpu_app(monkeypatch):
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+
+
+def _wait_tick_up(c, n):
+    import time
+
+    # The transport starts right after the mesh is complete; wait until every rank ticked.
+    deadline = time.time() + 20
+    while time.time() < deadline:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=4096)
+        a.free()
+        if all(c.stats(r)["ctrl_ticks"] > 0 for r in range(n)):
+            return
+        time.sleep(0.05)
+    raise AssertionError("tick transport never came up")
+
+
+def test_socket_tick_mesh_suite(mesh_factory, native, tool):
+    m = mesh_factory(4, extra_args=["--ctrl", "socket"])
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        _wait_tick_up(c, 4)
+        t0 = [c.stats(r)["ctrl_ticks"] for r in range(4)]
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=8 << 20, remote_bytes=8 << 20, flags=api.OCM_ALLOC_STRIPE)
+        assert len(a.remote_info()["extents"]) == 3
+        a.fill(seed=5)
+        a.put(0, 0, 8 << 20)
+        a.fill(seed=0)
+        a.get(0, 0, 8 << 20)
+        assert a.check(seed=5) == 0
+        a.free()
+        t1 = [c.stats(r)["ctrl_ticks"] for r in range(4)]
+        assert all(b > a_ for a_, b in zip(t0, t1)), (t0, t1)
+    for orig in (1, 3):
+        for args in (["1", "1", "2", "3"], ["3", "2", "4"], ["5", "8", "1"]):
+            rc, out = tool([f"{native}/ocm_test", *args], env=dict(m.client_env(orig), OCM_NO_GPU="1"))
+            assert rc == 0, out + m.logs()
+
+
+def test_socket_tick_concurrent_churn(mesh_factory):
+    m = mesh_factory(4, extra_args=["--ctrl", "socket"])
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent(f"""
+        import sys; sys.path.insert(0, {repo!r})
+        from oncilla_amd import api
+        from oncilla_amd.models import workloads as wl
+        r = int(sys.argv[1])
+        with api.Client(daemon_rank=r % 4, ns={m.ns!r}) as c:
+            wl.churn(c, 40, api.OCM_REMOTE_RDMA, 64 << 10, 64 << 10, seed=r)
+    """)
+    procs = [subprocess.Popen([sys.executable, "-c", code, str(i)], stderr=subprocess.PIPE, text=True,
+                              env=dict(os.environ, OCM_NO_GPU="1")) for i in range(8)]
+    for p in procs:
+        _, err = p.communicate(timeout=180)
+        assert p.returncode == 0, err + m.logs()
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        assert all(c.stats(r)["host_used"] == 0 for r in range(4))
+        assert all(c.stats(r)["ctrl_ticks"] > 0 for r in range(4))
+
+
+def test_tick_peer_death_falls_back_to_tcp(mesh_factory):
+    m = mesh_factory(3, extra_args=["--ctrl", "socket"])
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        _wait_tick_up(c, 3)
+        m.kill(2)
+        import time
+
+        time.sleep(0.3)
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20)  # rank1 over TCP now
+        assert a.remote_info()["extents"][0]["owner_rank"] == 1
+        a.free()
+
+
+def test_socket_tick_self_loop(mesh_factory):
+    # OCM_TICK_SELF routes a daemon's self-addressed records through the collective too.
+    m = mesh_factory(1, extra_args=["--ctrl", "socket"], env={"OCM_TICK_SELF": "1"})
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        _wait_tick_up(c, 1)
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)
+        a.free()
+        assert c.stats(0)["ctrl_ticks"] > 0
+
+
+@pytest.mark.gpu
+def test_rccl_tick_single_gpu(mesh_factory, monkeypatch):
+    """ncclCommInitRank + ncclAllGather on the MI355X carry the daemon's own
+    REQ_ALLOC/DO_ALLOC/FREED records (1-rank communicator, OCM_TICK_SELF)."""
+    monkeypatch.delenv("OCM_NO_GPU", raising=False)
+    m = mesh_factory(1, gpus=[0], extra_args=["--ctrl", "rccl"], env={"OCM_TICK_SELF": "1"})
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        _wait_tick_up(c, 1)
+        before = c.stats(0)["ctrl_ticks"]
+        for flags in (api.OCM_ALLOC_LOOPBACK, 0):
+            a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=1 << 20, remote_bytes=1 << 20, flags=flags)
+            a.fill(seed=1)
+            a.put(0, 0, 1 << 20)
+            a.fill(seed=0)
+            a.get(0, 0, 1 << 20)
+            assert a.check(seed=1) == 0
+            a.free()
+        assert c.stats(0)["ctrl_ticks"] > before
+    assert "rccl tick transport" in m.logs()
