@@ -48,6 +48,7 @@ struct DaemonConfig {
     std::string ready_file;
     std::string bind_ip;             // default: 0.0.0.0
     std::string ctrl = "tcp";        // daemon<->daemon records: tcp | rccl | socket (tick transports)
+    int watch_pid = 0;               // exit when this process (the launcher) exits
 };
 
 int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err);

@@ -23,7 +23,7 @@ namespace ocm {
 
 namespace {
 
-enum Tag : uint64_t { T_MBOX = 1, T_LISTEN, T_CONN, T_PIDFD, T_APPCONN, T_SIGNAL, T_TICK };
+enum Tag : uint64_t { T_MBOX = 1, T_LISTEN, T_CONN, T_PIDFD, T_APPCONN, T_SIGNAL, T_TICK, T_WATCH };
 inline uint64_t tag(Tag k, uint64_t id) { return (static_cast<uint64_t>(k) << 56) | (id & 0x00ffffffffffffffull); }
 inline Tag tag_kind(uint64_t t) { return static_cast<Tag>(t >> 56); }
 inline uint64_t tag_id(uint64_t t) { return t & 0x00ffffffffffffffull; }
@@ -127,6 +127,9 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
                 *err = "--ctrl must be tcp, rccl or socket";
                 return -1;
             }
+        } else if (a == "--watch-pid") {
+            if (!val(&v)) return -1;
+            cfg->watch_pid = std::atoi(v.c_str());
         } else if (a == "--zero") {
             cfg->zero_on_alloc = true;
         } else if (!a.empty() && a[0] == '-') {
@@ -262,6 +265,14 @@ int Daemon::init() {
     signal(SIGPIPE, SIG_IGN);
     sig_fd_ = signalfd(-1, &mask, SFD_CLOEXEC | SFD_NONBLOCK);
     ep_add(sig_fd_, EPOLLIN, tag(T_SIGNAL, 0));
+    if (cfg_.watch_pid > 0) {
+        int wfd = pidfd_open_compat(cfg_.watch_pid);
+        if (wfd < 0) {
+            OCM_ERR("--watch-pid %d: process not found", cfg_.watch_pid);
+            return -1;
+        }
+        ep_add(wfd, EPOLLIN, tag(T_WATCH, 0));
+    }
 
     if (mbox_alive(daemon_mailbox_name(rank_, ns_))) {
         OCM_ERR("another ocmd already serves rank %d in namespace %s", rank_, ns_.c_str());
@@ -421,6 +432,10 @@ int Daemon::loop() {
             case T_APPCONN: on_app_conn((int)tag_id(t), e); break;
             case T_SIGNAL: on_signal(); break;
             case T_TICK: on_tick(); break;
+            case T_WATCH:
+                OCM_INFO("rank %d: launcher %d exited; shutting down", rank_, cfg_.watch_pid);
+                stop_ = true;
+                break;
             default: break;
             }
         }

@@ -70,7 +70,7 @@ class Mesh:
     def __init__(self, n: int, gpus: Optional[Sequence[Optional[int]]] = None, ns: Optional[str] = None,
                  policy: str = "ring", extra_args: Sequence[str] = (), env: Optional[dict] = None,
                  workdir: Optional[str] = None, ports: Optional[Sequence[int]] = None, ranks: Optional[Sequence[int]] = None,
-                 rank_env: Optional[dict] = None):
+                 rank_env: Optional[dict] = None, bin_dir: Optional[str] = None, watch: bool = True):
         self.n = n
         self.gpus = list(gpus) if gpus is not None else [None] * n
         self.ns = ns or f"m{uuid.uuid4().hex[:10]}"
@@ -78,6 +78,8 @@ class Mesh:
         self.extra_args = list(extra_args)
         self.env = dict(env or {})
         self.rank_env = dict(rank_env or {})  # rank -> extra env (fault injection)
+        self.ocmd = os.path.join(bin_dir, "ocmd") if bin_dir else bin_path("ocmd")
+        self.watch = watch  # daemons exit when this process does (no orphans after a crash)
         self.workdir = workdir or tempfile.mkdtemp(prefix=f"ocm_{self.ns}_")
         self.ports = list(ports) if ports is not None else free_ports(n)
         self.ranks = list(ranks) if ranks is not None else list(range(n))  # which ranks THIS process launches
@@ -94,12 +96,14 @@ class Mesh:
         for r in self.ranks:
             ready = os.path.join(self.workdir, f"ready.{r}.json")
             log = os.path.join(self.workdir, f"ocmd.{r}.log")
-            args = [bin_path("ocmd"), self.nodefile, "--rank", str(r), "--ns", self.ns, "--policy", self.policy,
+            args = [self.ocmd, self.nodefile, "--rank", str(r), "--ns", self.ns, "--policy", self.policy,
                     "--ready-file", ready, "--bind", "127.0.0.1"]
             if self.gpus[r] is None:
                 args += ["--gpu", "none"]
             else:
                 args += ["--gpu", str(self.gpus[r])]
+            if self.watch:
+                args += ["--watch-pid", str(os.getpid())]
             args += self.extra_args
             env = dict(os.environ)
             env.update(self.env)

@@ -154,3 +154,24 @@ def test_daemon_death_fails_fast(four):
         a.free()
         with pytest.raises(api.OcmError):
             c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20, remote_rank=1)
+
+
+def test_daemons_exit_with_their_launcher(native, tmp_path):
+    code = textwrap.dedent(f"""
+        import sys, time; sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})
+        from oncilla_amd.parallel.mesh import Mesh
+        m = Mesh(2, workdir={str(tmp_path)!r}).start()
+        print(" ".join(str(d.proc.pid) for d in m.daemons), flush=True)
+        time.sleep(60)
+    """)
+    p = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
+    pids = [int(x) for x in p.stdout.readline().split()]
+    p.kill()  # launcher dies without stopping its mesh
+    p.wait()
+    deadline = time.time() + 10
+    alive = pids
+    while alive and time.time() < deadline:
+        alive = [pid for pid in pids if os.path.exists(f"/proc/{pid}") and
+                 open(f"/proc/{pid}/stat").read().split()[2] != "Z"]
+        time.sleep(0.05)
+    assert not alive, f"orphan daemons {alive}"

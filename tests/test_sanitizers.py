@@ -1,0 +1,40 @@
+"""Host-code sanitizers (the reference had only -Wall -Werror).
+Builds the tree with -fsanitize=address,undefined (build-asan/) and runs the
+daemon mesh + reference-equivalent tests on the instrumented binaries; any
+ASan/UBSan report fails the test."""
+import os
+import subprocess
+
+import pytest
+
+from oncilla_amd.parallel.mesh import Mesh
+from oncilla_amd.utils.build import build
+
+SAN_ENV = {"ASAN_OPTIONS": "detect_leaks=0:abort_on_error=0:halt_on_error=1", "UBSAN_OPTIONS": "print_stacktrace=1",
+           "OCM_NO_GPU": "1"}
+BAD = ("ERROR: AddressSanitizer", "runtime error:", "ERROR: LeakSanitizer")
+
+
+@pytest.fixture(scope="module")
+def asan_bin():
+    return os.path.join(build(sanitize=True), "bin")
+
+
+def test_unit_tests_under_asan(asan_bin):
+    r = subprocess.run([f"{asan_bin}/ocm_unit_tests"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, **SAN_ENV))
+    assert r.returncode == 0 and not any(b in r.stderr for b in BAD), r.stdout + r.stderr
+
+
+def test_mesh_under_asan(asan_bin):
+    m = Mesh(3, bin_dir=asan_bin, env=SAN_ENV).start(timeout=120)
+    try:
+        env = dict(m.client_env(1), **SAN_ENV)
+        for args in (["1", "1", "2", "1"], ["1", "1", "2", "3"], ["2", "4", "4"], ["3", "2", "4"], ["5", "4", "1"],
+                     ["4", "1", "2", "2"]):
+            r = subprocess.run([f"{asan_bin}/ocm_test", *args], capture_output=True, text=True, timeout=300, env=env)
+            assert r.returncode == 0 and not any(b in r.stderr for b in BAD), f"{args}\n{r.stdout}\n{r.stderr}"
+    finally:
+        m.stop()
+    logs = m.logs()
+    assert not any(b in logs for b in BAD), logs
