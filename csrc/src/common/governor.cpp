@@ -99,11 +99,14 @@ void Governor::reserve(int rank, uint32_t tier, uint64_t bytes, int sign) {
 }
 
 std::vector<int> Governor::candidates(const PlaceRequest &r) const {
+    // Peers on the origin's host only: the data plane maps owner memory into
+    // the app (IPC for HBM, /proc/<pid>/fd for host slabs), which needs one node.
     std::vector<int> out;
     const int n = (int)nodes_.size();
+    const std::string &home = nodes_[r.orig_rank].host;
     for (int d = 1; d < n; d++) {
         int k = (r.orig_rank + d) % n;
-        if (nodes_[k].alive && nodes_[k].joined) out.push_back(k);
+        if (nodes_[k].alive && nodes_[k].joined && nodes_[k].host == home) out.push_back(k);
     }
     return out;
 }
@@ -157,6 +160,10 @@ Placement Governor::place(const PlaceRequest &r) {
     if (r.remote_rank >= 0) {
         if (r.remote_rank >= n || !nodes_[r.remote_rank].alive) {
             p.err = r.remote_rank >= n ? EINVAL : EHOSTDOWN;
+            return p;
+        }
+        if (nodes_[r.remote_rank].host != nodes_[r.orig_rank].host) {
+            p.err = EXDEV;  // another node: not reachable by the xGMI/PCIe data plane
             return p;
         }
         owners.push_back(r.remote_rank);

@@ -193,6 +193,26 @@ static void t_governor() {
     }
 }
 
+static void t_governor_hosts() {
+    const uint64_t G = 1ull << 30;
+    Governor gov(4, Policy::Stripe, 1 << 20);
+    for (int r = 0; r < 4; r++) {
+        NodeConfig c = cfg(r, 8 * G, G);
+        std::snprintf(c.host, sizeof(c.host), "%s", r < 2 ? "nodeA" : "nodeB");
+        gov.add_node(c);
+    }
+    PlaceRequest pr;
+    pr.orig_rank = 0;
+    pr.bytes = 64 << 20;
+    Placement p = gov.place(pr);
+    CHECK(p.err == 0 && p.extents.size() == 1 && p.extents[0].owner == 1);  // only the same-host peer
+    pr.orig_rank = 3;
+    p = gov.place(pr);
+    CHECK(p.err == 0 && p.extents.size() == 1 && p.extents[0].owner == 2);
+    pr.remote_rank = 0;
+    CHECK(gov.place(pr).err == EXDEV);
+}
+
 static void t_stripe_geometry() {
     for (uint64_t total : {1ull, 4095ull, 4096ull, 1000000ull, (3ull << 20) + 7}) {
         for (int n = 1; n <= 8; n++) {
@@ -236,7 +256,8 @@ int main() {
         const char *name;
         std::function<void()> fn;
     } tests[] = {{"layout", t_layout},           {"nodefile", t_nodefile}, {"range_alloc", t_range_alloc},
-                 {"governor", t_governor},       {"stripe_geometry", t_stripe_geometry},
+                 {"governor", t_governor},       {"governor_hosts", t_governor_hosts},
+                 {"stripe_geometry", t_stripe_geometry},
                  {"arena_host", t_arena_host}};
     for (auto &t : tests) {
         int before = g_fail;

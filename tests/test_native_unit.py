@@ -8,7 +8,7 @@ from oncilla_amd import api
 def test_native_unit_binary(native, tool):
     rc, out = tool([f"{native}/ocm_unit_tests"])
     assert rc == 0, out
-    for name in ("layout", "nodefile", "range_alloc", "governor", "stripe_geometry", "arena_host"):
+    for name in ("layout", "nodefile", "range_alloc", "governor", "governor_hosts", "stripe_geometry", "arena_host"):
         assert f"PASS {name}" in out
 
 
