@@ -49,6 +49,9 @@ struct DaemonConfig {
     std::string bind_ip;             // default: 0.0.0.0
     std::string ctrl = "tcp";        // daemon<->daemon records: tcp | rccl | socket (tick transports)
     int watch_pid = 0;               // exit when this process (the launcher) exits
+    uint64_t lease_bytes = 1ull << 30;  // HBM leased per owner for local sub-allocation (0 = off)
+    int lease_after = 2;             // normal placements on an owner before leasing there
+    bool lease_host = false;         // also lease host-tier capacity (tests; OCM_LEASE_HOST=1)
 };
 
 int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err);
@@ -88,10 +91,22 @@ private:
         std::vector<Region> extents;
         std::vector<bool> have;
         std::set<int> awaiting;   // ranks we wait on (peer death fails the request)
+        int lease_owner = -1;     // >= 0: this is a lease request for that owner
+        uint32_t lease_tier = 0;
+    };
+    // A chunk of an owner's HBM leased to this (origin) daemon: small remote
+    // allocations on that owner are carved from it and freed locally, with no
+    // mesh round trip (rank0 reserved the whole chunk when granting it).
+    struct Lease {
+        int owner = -1;
+        uint32_t tier = TIER_GPU;
+        Region base;               // the chunk as the owner exported it
+        RangeAllocator ra;
     };
     struct OriginAlloc {
         pid_t pid = 0;
         bool remote = false;
+        int lease = -1;            // index into leases_ when carved from a lease
         uint64_t bytes = 0;
         std::vector<Region> extents;
     };
@@ -145,6 +160,9 @@ private:
     void fail_pending_on(int rank);
     void peer_lost(int rank);
     void sweep_timeouts();
+    bool try_lease_alloc(Msg &m);
+    void request_lease(int owner, uint32_t tier);
+    int preferred_owner() const;
     void start_tick(const uint8_t *id);
     void on_tick();
     void send_tcp(int r, Msg &m);
@@ -176,6 +194,10 @@ private:
     uint64_t seq_ = 0, local_ids_ = 0;
     int request_timeout_ms_ = 30000;
     std::unique_ptr<TickTransport> tick_;
+    std::vector<std::unique_ptr<Lease>> leases_;
+    std::map<int, int> lease_demand_;   // owner -> normal placements seen
+    std::set<int> lease_inflight_;      // owners with an outstanding lease request
+    uint64_t lease_ids_ = 0, n_lease_allocs_ = 0;
     // Fault injection (OCM_FAULT="do_alloc_fail=N,drop_do_alloc=N,crash_after_allocs=N"):
     int fault_alloc_fail_ = 0, fault_drop_alloc_ = 0, fault_crash_after_ = -1;
     void parse_faults();

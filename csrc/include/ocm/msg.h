@@ -88,7 +88,7 @@ struct Region {
 
 // Node description (ADD_NODE / NODE_TABLE / CONNECT_CONFIRM / STATS reply).
 struct NodeConfig {
-    char host[40];
+    char host[32];
     int32_t rank;
     int32_t gpu;           // device ordinal, -1 = CPU-only daemon
     int32_t num_gpu;       // GPUs visible on the node
@@ -102,6 +102,8 @@ struct NodeConfig {
     uint32_t num_apps;
     uint32_t n_alloc, n_free, n_reclaimed, n_spilled, n_slabs;
     uint32_t ticks;        // allgather ticks of the control transport (0 on TCP)
+    uint32_t n_leases;     // capacity leases this daemon holds on peers
+    uint32_t lease_allocs; // allocations served from them (no mesh round trip)
 };
 
 struct Msg {

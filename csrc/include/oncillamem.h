@@ -125,7 +125,9 @@ struct ocm_daemon_stats {
     uint64_t n_alloc, n_free, n_reclaimed, n_spilled;
     uint64_t n_slabs;
     uint64_t ctrl_ticks;   /* allgather ticks of the RCCL/socket control transport (0 on TCP) */
-    uint64_t reserved[3];
+    uint64_t n_leases;     /* capacity leases held on peers */
+    uint64_t lease_allocs; /* allocations carved from them without a mesh round trip */
+    uint64_t reserved[1];
 };
 
 ocm_alloc_t ocm_alloc_ex(ocm_alloc_param_t alloc_param, const struct ocm_alloc_ex_params *ex);

@@ -80,6 +80,9 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
     if (env("OCM_ZERO_ON_ALLOC")) cfg->zero_on_alloc = true;
     if (env("OCM_NO_GPU")) cfg->gpu = -1;
     if (const char *v = env("OCM_CTRL")) cfg->ctrl = v;
+    if (const char *v = env("OCM_LEASE_BYTES")) cfg->lease_bytes = parse_bytes(v);
+    if (const char *v = env("OCM_LEASE_AFTER")) cfg->lease_after = std::atoi(v);
+    if (env("OCM_LEASE_HOST")) cfg->lease_host = true;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto val = [&](std::string *out) {
@@ -127,6 +130,9 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
                 *err = "--ctrl must be tcp, rccl or socket";
                 return -1;
             }
+        } else if (a == "--lease-bytes") {
+            if (!val(&v)) return -1;
+            cfg->lease_bytes = parse_bytes(v);
         } else if (a == "--watch-pid") {
             if (!val(&v)) return -1;
             cfg->watch_pid = std::atoi(v.c_str());
@@ -190,6 +196,8 @@ NodeConfig Daemon::my_config() const {
     c.n_spilled = (uint32_t)(gov_ ? gov_->spilled_count() : n_spilled_);
     c.n_slabs = (uint32_t)(arena_ ? arena_->num_slabs() : 0);
     c.ticks = (uint32_t)(tick_ ? tick_->ticks() : 0);
+    for (auto &l : leases_) c.n_leases += l != nullptr;
+    c.lease_allocs = (uint32_t)n_lease_allocs_;
     return c;
 }
 
@@ -756,6 +764,7 @@ void Daemon::app_req_alloc(Msg &m) {
         send_app(m.pid, r);
         return;
     }
+    if (try_lease_alloc(m)) return;
     Pending p;
     p.seq = next_seq();
     p.pid = m.pid;
@@ -1133,6 +1142,41 @@ void Daemon::finish_alloc(Pending &p) {
     const uint64_t seq = p.seq;
     const uint64_t app_seq = p.app_seq;
     const pid_t pid = p.pid;
+    if (p.lease_owner >= 0) {
+        const int owner = p.lease_owner;
+        lease_inflight_.erase(owner);
+        if (!p.err && p.expect == 1 && p.have[0] && p.extents[0].tier == p.lease_tier) {
+            auto l = std::make_unique<Lease>();
+            l->owner = owner;
+            l->tier = p.lease_tier;
+            l->base = p.extents[0];
+            l->ra.reset(l->base.bytes);
+            OCM_LOG("rank %d: leased %llu bytes of rank %d HBM", rank_, (unsigned long long)l->base.bytes, owner);
+            leases_.push_back(std::move(l));
+        } else if (p.err) {
+            // Refused (no capacity): need much more demand before asking again.
+            lease_demand_[owner] = -16 * std::max(1, cfg_.lease_after);
+        } else if (p.expect >= 1) {
+            // Not what we asked for (e.g. spilled): give it back.
+            for (int i = 0; i < p.expect; i++) {
+                if (!p.have[i]) continue;
+                Msg f;
+                std::memset(&f, 0, sizeof(f));
+                f.type = MSG_DO_FREE;
+                f.status = MSG_REQUEST;
+                f.rank = rank_;
+                f.u.region = p.extents[i];
+                send_rank(p.extents[i].owner_rank, f);
+            }
+            Msg fr;
+            std::memset(&fr, 0, sizeof(fr));
+            fr.type = MSG_FREED;
+            fr.u.region.alloc_id = p.alloc_id;
+            send_rank(0, fr);
+        }
+        pending_.erase(seq);
+        return;
+    }
     if (p.err) {
         // Roll back the extents that did get memory.
         for (int i = 0; i < p.expect; i++) {
@@ -1173,6 +1217,10 @@ void Daemon::finish_alloc(Pending &p) {
     oa.bytes = p.total_bytes;
     oa.extents = p.extents;
     const uint64_t id = p.alloc_id;
+    if (oa.extents.size() == 1 && cfg_.lease_bytes && oa.extents[0].owner_rank != rank_ &&
+        (oa.extents[0].tier == TIER_GPU || (cfg_.lease_host && oa.extents[0].tier == TIER_HOST)) &&
+        !(oa.extents[0].flags & REGION_SPILLED) && ++lease_demand_[oa.extents[0].owner_rank] >= cfg_.lease_after)
+        request_lease(oa.extents[0].owner_rank, oa.extents[0].tier);
     origin_allocs_[id] = oa;
     n_alloc_++;
     pending_.erase(seq);
@@ -1213,6 +1261,22 @@ void Daemon::start_free(uint64_t alloc_id, pid_t reply_pid, uint64_t reply_seq) 
     origin_allocs_.erase(it);
     if (!oa.remote) {
         n_free_++;
+        return;
+    }
+    if (oa.lease >= 0 && oa.lease < (int)leases_.size() && leases_[oa.lease]) {
+        Lease &l = *leases_[oa.lease];
+        l.ra.free(oa.extents[0].offset - l.base.offset);
+        n_free_++;
+        if (reply_pid && apps_.count(reply_pid)) {
+            Msg r;
+            std::memset(&r, 0, sizeof(r));
+            r.type = MSG_RELEASE_APP;
+            r.status = MSG_RESPONSE;
+            r.pid = reply_pid;
+            r.rank = rank_;
+            r.seq = reply_seq;
+            send_app(reply_pid, r);
+        }
         return;
     }
     Pending p;
@@ -1307,6 +1371,9 @@ void Daemon::fail_pending_on(int rank) {
 
 void Daemon::peer_lost(int rank) {
     OCM_WARN("rank %d: lost link to rank %d", rank_, rank);
+    for (auto &l : leases_)
+        if (l && l->owner == rank) l.reset();  // its memory died with it
+    lease_inflight_.erase(rank);
     if (tick_) tick_->abort();  // the dead rank will never join another tick
     if (gov_) gov_->mark_dead(rank);
     fail_pending_on(rank);
@@ -1403,6 +1470,102 @@ void Daemon::on_tick() {
     if (tick_->failed()) {
         for (TickRecord &rec : tick_->take_unsent()) send_tcp(rec.dest, rec.msg);
     }
+}
+
+int Daemon::preferred_owner() const {
+    // The governor's first choice for a single-extent remote allocation:
+    // the next live same-host peer in ring order, (rank + d) % N.
+    for (int d = 1; d < n_; d++) {
+        const int k = (rank_ + d) % n_;
+        if (!joined_[k] || peer_fd_[k] < 0) continue;
+        if (std::strncmp(table_[k].host, table_[rank_].host, sizeof(table_[k].host)) != 0) continue;
+        return k;
+    }
+    return -1;
+}
+
+void Daemon::request_lease(int owner, uint32_t tier) {
+    if (!cfg_.lease_bytes || lease_inflight_.count(owner)) return;
+    lease_inflight_.insert(owner);
+    Pending p;
+    p.seq = next_seq();
+    p.pid = 0;
+    p.type = MSG_REQ_ALLOC;
+    p.kind = OCM_REMOTE_GPU;
+    p.total_bytes = cfg_.lease_bytes;
+    p.lease_owner = owner;
+    p.lease_tier = tier;
+    p.t0_ms = now_ms();
+    p.awaiting.insert(0);
+    pending_[p.seq] = p;
+    Msg f;
+    std::memset(&f, 0, sizeof(f));
+    f.type = MSG_REQ_ALLOC;
+    f.status = MSG_REQUEST;
+    f.rank = rank_;
+    f.seq = p.seq;
+    f.u.req.orig_rank = rank_;
+    f.u.req.remote_rank = owner;
+    f.u.req.bytes = cfg_.lease_bytes;
+    f.u.req.kind = OCM_REMOTE_GPU;
+    f.u.req.flags = OCM_ALLOC_NO_SPILL | (tier == TIER_HOST ? OCM_ALLOC_HOST_TIER : 0);
+    f.u.req.app_pid = 0;
+    send_rank(0, f);
+}
+
+bool Daemon::try_lease_alloc(Msg &m) {
+    const AllocReq &req = m.u.req;
+    if (!cfg_.lease_bytes || leases_.empty()) return false;
+    if (req.flags & (OCM_ALLOC_LOOPBACK | OCM_ALLOC_STRIPE | OCM_ALLOC_ZERO)) return false;
+    const uint32_t want_tier = (req.flags & OCM_ALLOC_HOST_TIER) ? TIER_HOST : TIER_GPU;
+    if (req.bytes > cfg_.lease_bytes / 4) return false;
+    // Policy-faithful: only requests the governor would place as ONE extent on
+    // the ring successor (ring, or stripe with bytes <= stripe unit).
+    if (cfg_.policy == Policy::LeastLoaded || cfg_.policy == Policy::Loopback) return false;
+    const uint64_t unit = req.stripe_unit ? req.stripe_unit : cfg_.stripe_unit;
+    if (cfg_.policy == Policy::Stripe && req.bytes > unit) return false;
+    const int owner = preferred_owner();
+    if (owner < 0 || (req.remote_rank >= 0 && req.remote_rank != owner)) return false;
+    for (size_t i = 0; i < leases_.size(); i++) {
+        Lease *l = leases_[i].get();
+        if (!l || l->owner != owner || l->tier != want_tier) continue;
+        uint64_t off = 0;
+        if (!l->ra.alloc(req.bytes, 4096, &off)) continue;
+        Region rg = l->base;
+        rg.alloc_id = (1ull << 62) | ((uint64_t)rank_ << 40) | (++lease_ids_);
+        rg.offset = l->base.offset + off;
+        rg.bytes = req.bytes;
+        rg.stripe_unit = 0;
+        rg.extent_idx = 0;
+        rg.n_extents = 1;
+        rg.orig_rank = rank_;
+        rg.flags = (uint16_t)(rg.flags & ~REGION_DEDICATED);  // importers keep the chunk mapped
+        OriginAlloc oa;
+        oa.pid = m.pid;
+        oa.remote = true;
+        oa.bytes = req.bytes;
+        oa.lease = (int)i;
+        oa.extents.push_back(rg);
+        origin_allocs_[rg.alloc_id] = oa;
+        n_alloc_++;
+        n_lease_allocs_++;
+        // Top up before the chunk runs dry.
+        if (l->ra.largest_free() < cfg_.lease_bytes / 4) request_lease(owner, want_tier);
+        Msg h;
+        std::memset(&h, 0, sizeof(h));
+        h.type = MSG_RELEASE_APP;
+        h.status = MSG_RESPONSE;
+        h.pid = m.pid;
+        h.rank = rank_;
+        h.seq = m.seq;
+        h.u.region = rg;
+        send_app(m.pid, h);
+        Msg e = h;
+        e.type = MSG_EXTENT;
+        send_app(m.pid, e);
+        return true;
+    }
+    return false;
 }
 
 }  // namespace ocm

@@ -1027,6 +1027,8 @@ int ocm_stats(int rank, struct ocm_daemon_stats *out) {
     out->n_spilled = c.n_spilled;
     out->n_slabs = c.n_slabs;
     out->ctrl_ticks = c.ticks;
+    out->n_leases = c.n_leases;
+    out->lease_allocs = c.lease_allocs;
     return 0;
 }
 

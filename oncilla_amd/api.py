@@ -104,7 +104,9 @@ class OcmDaemonStats(ctypes.Structure):
         ("n_spilled", ctypes.c_uint64),
         ("n_slabs", ctypes.c_uint64),
         ("ctrl_ticks", ctypes.c_uint64),
-        ("reserved", ctypes.c_uint64 * 3),
+        ("n_leases", ctypes.c_uint64),
+        ("lease_allocs", ctypes.c_uint64),
+        ("reserved", ctypes.c_uint64 * 1),
     ]
 
     def as_dict(self) -> dict:

@@ -1,0 +1,88 @@
+"""Capacity leases: after a few placements on an owner, the origin daemon
+leases a chunk there and serves later small allocations from it locally (no
+rank0 / owner round trip); frees and crash reclaim stay local too."""
+import os
+import signal
+import subprocess
+import sys
+import textwrap
+import time
+
+import pytest
+
+from oncilla_amd import api
+from oncilla_amd.models import workloads as wl
+
+LEASE_ENV = {"OCM_LEASE_HOST": "1", "OCM_LEASE_BYTES": str(64 << 20)}
+
+
+@pytest.fixture(autouse=True)
+def _cpu_app(monkeypatch):
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+
+
+def test_leased_allocations_roundtrip_and_accounting(mesh_factory):
+    m = mesh_factory(3, env=LEASE_ENV)
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        allocs = [c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20) for _ in range(2)]
+        deadline = time.time() + 5
+        while c.stats(0)["n_leases"] == 0 and time.time() < deadline:
+            time.sleep(0.01)
+        st0 = c.stats(0)
+        assert st0["n_leases"] == 1
+        # the owner (ring successor) handed out the lease chunk
+        assert c.stats(1)["host_used"] == (64 << 20) + 2 * (1 << 20)
+        more = [c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20) for _ in range(8)]
+        assert c.stats(0)["lease_allocs"] == 8
+        assert c.stats(1)["host_used"] == (64 << 20) + 2 * (1 << 20)  # leased allocs cost the owner nothing new
+        for i, a in enumerate(more):
+            assert a.remote_info()["extents"][0]["owner_rank"] == 1
+            a.fill(seed=40 + i)
+            a.put(0, 0, 1 << 20)
+        for i, a in enumerate(more):
+            a.fill(seed=0)
+            a.get(0, 0, 1 << 20)
+            assert a.check(seed=40 + i) == 0, f"leased allocation {i} overlaps another"
+        for a in more + allocs:
+            a.free()
+        assert c.stats(1)["host_used"] == 64 << 20  # only the lease itself remains
+
+
+def test_lease_latency_is_local(mesh_factory):
+    m = mesh_factory(4, env=LEASE_ENV)
+    with api.Client(daemon_rank=2, ns=m.ns) as c:
+        wl.alloc_latency(c, api.OCM_REMOTE_RDMA, 5, local_bytes=4096, remote_bytes=1 << 20)  # trigger the lease
+        time.sleep(0.1)
+        lat = wl.alloc_latency(c, api.OCM_REMOTE_RDMA, 100, local_bytes=4096, remote_bytes=1 << 20)
+        loc = wl.alloc_latency(c, api.OCM_LOCAL_HOST, 100, local_bytes=4096)
+        assert c.stats(2)["lease_allocs"] >= 100
+        # a leased remote alloc costs about what a local one does (one mailbox round trip)
+        assert lat["alloc_p50_us"] < 3 * loc["alloc_p50_us"] + 20, (lat, loc)
+
+
+def test_crash_reclaims_leased_ranges(mesh_factory):
+    m = mesh_factory(2, env=LEASE_ENV)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent(f"""
+        import os, signal, sys, time
+        sys.path.insert(0, {repo!r})
+        from oncilla_amd import api
+        c = api.Client(daemon_rank=0, ns={m.ns!r}); c.init()
+        keep = [c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=16 << 20) for _ in range(2)]
+        time.sleep(0.2)
+        keep += [c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=16 << 20) for _ in range(3)]
+        print(c.stats(0)["lease_allocs"], flush=True)
+        os.kill(os.getpid(), signal.SIGKILL)
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, OCM_NO_GPU="1"))
+    assert r.returncode == -signal.SIGKILL and int(r.stdout.split()[0]) == 3, r.stderr
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        time.sleep(0.2)
+        # the three leased ranges are back: a 48 MiB leased allocation fits again
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=16 << 20)
+        b = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=16 << 20)
+        assert c.stats(0)["lease_allocs"] >= 2
+        assert c.stats(1)["host_used"] == 64 << 20
+        a.free()
+        b.free()
