@@ -232,8 +232,10 @@ hipError_t xfer_launch(const XferArgs &in, const XferTuning &t, hipStream_t stre
     int variant = t.variant;
     if (variant == XFER_AUTO) variant = XFER_REG;
     if (a.tile_shift != kTileShift) variant = XFER_REG;  // LDS path is built for 32 KiB tiles
-    // Enough workgroups to cover every CU several times over, never more than tiles.
-    int cap = t.max_blocks > 0 ? t.max_blocks : num_cus() * (variant == XFER_LDS ? 2 : 4);
+    // Grid caps from the round-1 sweep (profiles/ksweep_r01.json): LDS-DMA
+    // peaks at 4 blocks per CU (2 resident, 64 KiB LDS each), the register
+    // path at 2 per CU; never more blocks than tiles.
+    int cap = t.max_blocks > 0 ? t.max_blocks : num_cus() * (variant == XFER_LDS ? 4 : 2);
     const unsigned grid = (unsigned)(ntiles < (uint64_t)cap ? ntiles : (uint64_t)cap);
     if (variant == XFER_LDS) {
         if (t.nontemporal)

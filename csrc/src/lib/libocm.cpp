@@ -460,7 +460,16 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
             if (sh < 0) OCM_FAIL(-1, "stripe unit %llu is not a power of two", (unsigned long long)a->stripe_unit);
             x.unit_shift = (uint32_t)sh;
         }
-        err = xfer_launch(x, s.tuning, s.stream);
+        XferTuning t = s.tuning;
+        if (t.variant == XFER_AUTO) {
+            // Measured (profiles/ksweep_r01.json): LDS-DMA staging wins HBM->HBM
+            // copies up to ~256 MiB on the same GPU; everything else (peer HBM
+            // over xGMI, host-mapped memory, huge copies) uses the register path.
+            bool same_gpu = lloc == LOC_DEVICE;
+            for (auto &e : a->ext) same_gpu &= e.r.tier == TIER_GPU && e.r.owner_gpu == s.device;
+            t.variant = (same_gpu && len <= (256ull << 20)) ? XFER_LDS : XFER_REG;
+        }
+        err = xfer_launch(x, t, s.stream);
     } else {
         service_park();
         segments(a, rem_off, len, segs);
@@ -499,10 +508,14 @@ int copy_local(void *dst, Loc dl, const void *src, Loc sl, size_t n) {
     }
     DeviceGuard g(s.device);
     hipError_t e;
-    if (dl == LOC_DEVICE && sl == LOC_DEVICE)
-        e = xfer_copy(dst, src, n, s.tuning, s.stream);
-    else
+    if (dl == LOC_DEVICE && sl == LOC_DEVICE) {
+        XferTuning t = s.tuning;
+        if (t.variant == XFER_AUTO) t.variant = n <= (256ull << 20) ? XFER_LDS : XFER_REG;
+        e = xfer_copy(dst, src, n, t, s.stream);
+    } else
+    {
         e = hipMemcpyAsync(dst, src, n, hipMemcpyDefault, s.stream);
+    }
     if (e != hipSuccess) OCM_FAIL(-1, "local copy failed: %s", hipGetErrorString(e));
     return sync_stream();
 }
