@@ -298,6 +298,40 @@ class Allocation:
             raise OcmError("pattern check failed")
         return int(bad)
 
+    # --- zero-copy torch views ---
+    def _view(self, ptr: int, nbytes: int, dtype, on_device: bool):
+        import torch
+
+        class _Iface:  # __cuda_array_interface__ v3 (torch consumes it on ROCm too)
+            def __init__(self, p, n):
+                self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (p, False), "version": 3,
+                                                 "strides": None, "stream": None}
+
+        if on_device:
+            t = torch.as_tensor(_Iface(ptr, nbytes), device=f"cuda:{self._c.device}")
+        else:
+            import ctypes as C
+
+            buf = (C.c_uint8 * nbytes).from_address(ptr)
+            t = torch.frombuffer(buf, dtype=torch.uint8)
+        return t.view(dtype) if dtype is not None and dtype != torch.uint8 else t
+
+    def local_tensor(self, dtype=None):
+        """The local half as a tensor (on the app's GPU for GPU kinds, CPU otherwise). No copy."""
+        ptr, n = self.localbuf()
+        on_dev = self._c.device >= 0 and self.kind in (OCM_LOCAL_GPU, OCM_REMOTE_GPU)
+        return self._view(ptr, n, dtype, on_dev)
+
+    def remote_tensor(self, dtype=None):
+        """The remote half (single extent) as a tensor on this process's GPU: torch kernels then
+        read/write peer HBM directly over xGMI (or the pinned host tier over PCIe). No copy."""
+        p = self._c.lib.ocm_remotebuf(self.handle)
+        if not p:
+            raise OcmError("remote_tensor needs a single-extent remote allocation")
+        if self._c.device < 0:
+            return self._view(p, self.remote_size(), dtype, False)
+        return self._view(p, self.remote_size(), dtype, True)
+
     def free(self) -> None:
         if self.handle.value:
             rc = self._c.lib.ocm_free(self.handle)

@@ -147,3 +147,23 @@ def test_copy_service_small_ops(mesh_factory, policy):
             assert a.check(seed=7 + k, nbytes=4096) == 0
         assert api.counters()["n_put"] > before["n_put"]
         a.free()
+
+
+def test_tensor_views_on_peer_memory(mesh_factory):
+    """Zero-copy torch views: compute directly on the remote half (another
+    daemon's HBM via IPC) and move it with one-sided ops."""
+    m = mesh_factory(2, gpus=[0, 0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 1 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=4 * n, remote_bytes=4 * n)
+        loc = a.local_tensor(torch.float32)
+        rem = a.remote_tensor(torch.float32)
+        assert loc.device.type == "cuda" and rem.numel() == n
+        loc.copy_(torch.arange(n, dtype=torch.float32, device="cuda:0"))
+        a.put(0, 0, 4 * n)
+        torch.cuda.synchronize()
+        rem.mul_(2.0)                              # a torch kernel on peer memory
+        torch.cuda.synchronize()
+        a.get(0, 0, 4 * n)
+        assert torch.equal(loc, 2.0 * torch.arange(n, dtype=torch.float32, device="cuda:0"))
+        a.free()

@@ -83,3 +83,20 @@ def test_daemon_rejects_unknown_app_and_bad_requests(one, monkeypatch):
             c.alloc(99, local_bytes=4096)
         with pytest.raises(api.OcmError):
             c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 50)  # exceeds every tier
+
+
+def test_tensor_views_cpu(one, monkeypatch):
+    import torch
+
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    with api.Client(daemon_rank=0, ns=one.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=4096)
+        loc = a.local_tensor(torch.int32)
+        loc.copy_(torch.arange(1024, dtype=torch.int32))
+        a.put(0, 0, 4096)
+        rem = a.remote_tensor(torch.int32)
+        assert torch.equal(rem, torch.arange(1024, dtype=torch.int32))
+        rem.add_(5)
+        a.get(0, 0, 4096)
+        assert int(loc[10]) == 15
+        a.free()
