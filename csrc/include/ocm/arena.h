@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 
 #include "ocm/msg.h"
@@ -50,10 +51,13 @@ public:
     int free(uint32_t slab_id, uint64_t offset);
     uint64_t used(uint32_t tier) const;
     uint64_t capacity(uint32_t tier) const;
-    size_t num_slabs() const { return slabs_.size(); }
+    size_t num_slabs() const;
     const ArenaConfig &config() const { return cfg_; }
     // Raw pointer for daemon-side verification / tests.
     void *resolve(uint32_t slab_id, uint64_t offset) const;
+    // Thread-safe bounds check for the network data server: [offset, +len)
+    // inside slab `slab_id`; returns its address and tier.
+    bool locate(uint32_t slab_id, uint64_t offset, uint64_t len, void **p, uint32_t *tier) const;
 
 private:
     Slab *new_slab(uint32_t tier, uint64_t bytes, bool dedicated, int *err);
@@ -62,6 +66,7 @@ private:
     uint32_t next_slab_ = 1;
     uint64_t used_gpu_ = 0, used_host_ = 0;
     std::map<uint32_t, std::unique_ptr<Slab>> slabs_;
+    mutable std::mutex mu_;  // the event loop mutates, data-server threads locate()
 };
 
 }  // namespace ocm

@@ -24,6 +24,7 @@
 #include "ocm/arena.h"
 #include "ocm/governor.h"
 #include "ocm/msg.h"
+#include "ocm/netdata.h"
 #include "ocm/nodefile.h"
 #include "ocm/pmsg.h"
 #include "ocm/sock.h"
@@ -52,6 +53,7 @@ struct DaemonConfig {
     uint64_t lease_bytes = 1ull << 30;  // HBM leased per owner for local sub-allocation (0 = off)
     int lease_after = 2;             // normal placements on an owner before leasing there
     bool lease_host = false;         // also lease host-tier capacity (tests; OCM_LEASE_HOST=1)
+    std::string host_alias;          // report this host name (tests: pretend daemons are on other nodes)
 };
 
 int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err);
@@ -163,6 +165,7 @@ private:
     bool try_lease_alloc(Msg &m);
     void request_lease(int owner, uint32_t tier);
     int preferred_owner() const;
+    bool cross_host(int a, int b) const;
     void start_tick(const uint8_t *id);
     void on_tick();
     void send_tcp(int r, Msg &m);
@@ -194,6 +197,7 @@ private:
     uint64_t seq_ = 0, local_ids_ = 0;
     int request_timeout_ms_ = 30000;
     std::unique_ptr<TickTransport> tick_;
+    std::unique_ptr<DataServer> data_;  // network tier: serves PUT/GET from other nodes
     std::vector<std::unique_ptr<Lease>> leases_;
     std::map<int, int> lease_demand_;   // owner -> normal placements seen
     std::set<int> lease_inflight_;      // owners with an outstanding lease request

@@ -9,7 +9,9 @@
 //   * policies: ring (reference), least_loaded, stripe (one allocation spread
 //     over several peers so put/get use several xGMI links), loopback;
 //   * spill to the host tier when HBM is exhausted, ENOMEM when both are;
-//   * an allocation table keyed by alloc_id for free/crash reclaim.
+//   * an allocation table keyed by alloc_id for free/crash reclaim;
+//   * peers on the origin's host first; other hosts only when the origin's
+//     host has none (or one is named), through the network tier (netdata.h).
 // Pure logic (no I/O) so it is unit-tested on CPU.
 #pragma once
 #include <cstdint>
@@ -41,6 +43,7 @@ struct PlacedExtent {
     uint32_t tier = TIER_NONE;
     uint64_t bytes = 0;
     bool spilled = false;
+    bool net = false;      // owner on another host: reached through the network tier
 };
 
 struct PlaceRequest {
@@ -97,7 +100,8 @@ public:
 private:
     bool fits(const NodeState &n, uint32_t tier, uint64_t bytes) const;
     void reserve(int rank, uint32_t tier, uint64_t bytes, int sign);
-    std::vector<int> candidates(const PlaceRequest &r) const;
+    std::vector<int> candidates(const PlaceRequest &r) const;         // same-host peers, ring order
+    std::vector<int> remote_candidates(const PlaceRequest &r) const;  // other hosts, ring order
     bool place_one(int preferred, uint64_t bytes, uint32_t want_tier, bool allow_spill,
                    const std::vector<int> &fallback, const std::vector<int> &spill_to, PlacedExtent *out);
 

@@ -67,6 +67,7 @@ struct AllocReq {
 enum RegionFlags : uint16_t {
     REGION_DEDICATED = 1u << 0,  // slab holds only this extent: importer unmaps it on free
     REGION_SPILLED = 1u << 1,    // placed in the host tier because HBM was exhausted
+    REGION_NET = 1u << 2,        // owner on another node: handle = "net:<ip>:<port>" (netdata.h)
 };
 
 struct Region {

@@ -113,6 +113,8 @@ struct ocm_remote_info {
     uint64_t stripe_unit;
     uint64_t alloc_id;
     uint64_t remote_bytes;
+    uint32_t net_mask;   /* bit i: extent i is on another node (network tier) */
+    uint32_t reserved;
 };
 
 struct ocm_daemon_stats {

@@ -98,9 +98,20 @@ void Governor::reserve(int rank, uint32_t tier, uint64_t bytes, int sign) {
         slot = slot >= bytes ? slot - bytes : 0;
 }
 
+std::vector<int> Governor::remote_candidates(const PlaceRequest &r) const {
+    std::vector<int> out;
+    const int n = (int)nodes_.size();
+    const std::string &home = nodes_[r.orig_rank].host;
+    for (int d = 1; d < n; d++) {
+        int k = (r.orig_rank + d) % n;
+        if (nodes_[k].alive && nodes_[k].joined && nodes_[k].host != home) out.push_back(k);
+    }
+    return out;
+}
+
 std::vector<int> Governor::candidates(const PlaceRequest &r) const {
-    // Peers on the origin's host only: the data plane maps owner memory into
-    // the app (IPC for HBM, /proc/<pid>/fd for host slabs), which needs one node.
+    // Peers on the origin's host: the data plane maps their memory into the
+    // app (IPC over xGMI for HBM, /proc/<pid>/fd for host slabs).
     std::vector<int> out;
     const int n = (int)nodes_.size();
     const std::string &home = nodes_[r.orig_rank].host;
@@ -162,15 +173,15 @@ Placement Governor::place(const PlaceRequest &r) {
             p.err = r.remote_rank >= n ? EINVAL : EHOSTDOWN;
             return p;
         }
-        if (nodes_[r.remote_rank].host != nodes_[r.orig_rank].host) {
-            p.err = EXDEV;  // another node: not reachable by the xGMI/PCIe data plane
-            return p;
-        }
         owners.push_back(r.remote_rank);
         explicit_owner = true;
     } else if ((r.flags & OCM_ALLOC_LOOPBACK) || policy_ == Policy::Loopback) {
         owners.push_back(r.orig_rank);
         explicit_owner = true;
+    } else if (peers.empty() && !remote_candidates(r).empty()) {
+        // One daemon on this host, others elsewhere (the reference's layout):
+        // ring to the next node, through the network tier.
+        owners.push_back(remote_candidates(r)[0]);
     } else if (peers.empty()) {
         // Single daemon: no peer HBM exists, the remote half lives in the host tier
         // (the reference coerced every request to host memory here, src/alloc.c:82-83).
@@ -219,6 +230,7 @@ Placement Governor::place(const PlaceRequest &r) {
             p.err = ENOMEM;
             return p;
         }
+        e.net = nodes_[e.owner].host != nodes_[r.orig_rank].host;
         p.extents.push_back(e);
     }
     p.stripe_unit = unit;

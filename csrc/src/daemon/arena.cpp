@@ -24,7 +24,26 @@ Arena::~Arena() {
     slabs_.clear();
 }
 
-uint64_t Arena::used(uint32_t tier) const { return tier == TIER_GPU ? used_gpu_ : used_host_; }
+uint64_t Arena::used(uint32_t tier) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return tier == TIER_GPU ? used_gpu_ : used_host_;
+}
+
+size_t Arena::num_slabs() const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return slabs_.size();
+}
+
+bool Arena::locate(uint32_t slab_id, uint64_t offset, uint64_t len, void **p, uint32_t *tier) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = slabs_.find(slab_id);
+    if (it == slabs_.end() || !it->second->base) return false;
+    const Slab &s = *it->second;
+    if (offset > s.bytes || len > s.bytes - offset) return false;
+    *p = static_cast<char *>(s.base) + offset;
+    *tier = s.tier;
+    return true;
+}
 
 uint64_t Arena::capacity(uint32_t tier) const {
     return tier == TIER_GPU ? (cfg_.gpu >= 0 ? cfg_.gpu_capacity : 0) : cfg_.host_capacity;
@@ -100,9 +119,10 @@ void Arena::destroy_slab(Slab *s) {
 }
 
 int Arena::alloc(uint32_t tier, uint64_t bytes, Region *out) {
+    std::lock_guard<std::mutex> lk(mu_);
     if (bytes == 0) return EINVAL;
     if (tier != TIER_GPU && tier != TIER_HOST) return EINVAL;
-    if (used(tier) + bytes > capacity(tier)) return ENOMEM;
+    if ((tier == TIER_GPU ? used_gpu_ : used_host_) + bytes > capacity(tier)) return ENOMEM;
     const uint64_t slab_default = tier == TIER_GPU ? cfg_.slab_bytes : std::min<uint64_t>(cfg_.slab_bytes, 256ull << 20);
     Slab *slab = nullptr;
     uint64_t off = 0;
@@ -149,6 +169,7 @@ int Arena::alloc(uint32_t tier, uint64_t bytes, Region *out) {
 }
 
 int Arena::free(uint32_t slab_id, uint64_t offset) {
+    std::lock_guard<std::mutex> lk(mu_);
     auto it = slabs_.find(slab_id);
     if (it == slabs_.end()) return ENOENT;
     Slab *s = it->second.get();
@@ -165,6 +186,7 @@ int Arena::free(uint32_t slab_id, uint64_t offset) {
 }
 
 void *Arena::resolve(uint32_t slab_id, uint64_t offset) const {
+    std::lock_guard<std::mutex> lk(mu_);
     auto it = slabs_.find(slab_id);
     if (it == slabs_.end() || offset >= it->second->bytes) return nullptr;
     return static_cast<char *>(it->second->base) + offset;

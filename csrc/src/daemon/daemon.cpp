@@ -83,6 +83,7 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
     if (const char *v = env("OCM_LEASE_BYTES")) cfg->lease_bytes = parse_bytes(v);
     if (const char *v = env("OCM_LEASE_AFTER")) cfg->lease_after = std::atoi(v);
     if (env("OCM_LEASE_HOST")) cfg->lease_host = true;
+    if (const char *v = env("OCM_HOST_ALIAS")) cfg->host_alias = v;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto val = [&](std::string *out) {
@@ -130,6 +131,8 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
                 *err = "--ctrl must be tcp, rccl or socket";
                 return -1;
             }
+        } else if (a == "--host-alias") {
+            if (!val(&cfg->host_alias)) return -1;
         } else if (a == "--lease-bytes") {
             if (!val(&v)) return -1;
             cfg->lease_bytes = parse_bytes(v);
@@ -178,7 +181,10 @@ void Daemon::ep_del(int fd) { epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr); }
 NodeConfig Daemon::my_config() const {
     NodeConfig c;
     std::memset(&c, 0, sizeof(c));
-    gethostname(c.host, sizeof(c.host) - 1);
+    if (!cfg_.host_alias.empty())
+        std::snprintf(c.host, sizeof(c.host), "%s", cfg_.host_alias.c_str());
+    else
+        gethostname(c.host, sizeof(c.host) - 1);
     c.rank = rank_;
     c.gpu = gpu_;
     c.num_gpu = num_gpu_;
@@ -258,6 +264,11 @@ int Daemon::init() {
                            ? cfg_.host_capacity
                            : (uint64_t)((double)mem_available() * cfg_.host_fraction / std::max(1, local_daemons));
     arena_ = std::make_unique<Arena>(ac);
+    data_ = std::make_unique<DataServer>(arena_.get(), gpu_);
+    if (data_->start(cfg_.bind_ip.empty() ? "0.0.0.0" : cfg_.bind_ip) != 0) {
+        OCM_WARN("rank %d: network data server unavailable; cross-node placement disabled here", rank_);
+        data_.reset();
+    }
     if (rank_ == 0) gov_ = std::make_unique<Governor>(n_, cfg_.policy, cfg_.stripe_unit);
     table_.assign(n_, NodeConfig{});
     joined_.assign(n_, false);
@@ -377,6 +388,10 @@ void Daemon::shutdown() {
     if (tick_) {
         tick_->stop();
         tick_.reset();
+    }
+    if (data_) {
+        data_->stop();
+        data_.reset();
     }
     for (auto &kv : apps_) {
         if (kv.second.pidfd >= 0) close(kv.second.pidfd);
@@ -994,7 +1009,7 @@ void Daemon::r0_req_alloc(Msg &m) {
         rg.owner_rank = e.owner;
         rg.orig_rank = m.rank;
         rg.tier = (uint16_t)e.tier;
-        rg.flags = e.spilled ? REGION_SPILLED : 0;
+        rg.flags = (uint16_t)((e.spilled ? REGION_SPILLED : 0) | (cross_host(m.rank, e.owner) ? REGION_NET : 0));
         rg.extent_idx = (uint16_t)i;
         rg.n_extents = (uint16_t)p.extents.size();
         send_rank(e.owner, d);
@@ -1011,7 +1026,8 @@ void Daemon::r0_place_fail(Msg &m) {
         d.err = 0;
         d.u.region.owner_rank = e.owner;
         d.u.region.tier = (uint16_t)e.tier;
-        d.u.region.flags = e.spilled ? REGION_SPILLED : 0;
+        d.u.region.flags =
+            (uint16_t)((e.spilled ? REGION_SPILLED : 0) | (cross_host(m.rank, e.owner) ? REGION_NET : 0));
         OCM_LOG("re-placing alloc %llu extent %d on rank %d tier %u", (unsigned long long)rg.alloc_id,
                 rg.extent_idx, e.owner, e.tier);
         send_rank(e.owner, d);
@@ -1071,6 +1087,23 @@ void Daemon::owner_do_alloc(Msg &m) {
         return;
     }
     rg.owner_rank = rank_;
+    if (rg.flags & REGION_NET) {
+        if (!data_) {
+            arena_->free(rg.slab_id, rg.offset);
+            Msg f = m;
+            f.type = MSG_PLACE_FAIL;
+            f.status = MSG_REQUEST;
+            f.err = ENETUNREACH;
+            f.u.region.owner_rank = rank_;
+            send_rank(0, f);
+            return;
+        }
+        // Other node: the app streams through our data server instead of mapping the slab.
+        std::memset(rg.handle, 0, sizeof(rg.handle));
+        std::snprintf(reinterpret_cast<char *>(rg.handle), sizeof(rg.handle), "net:%s:%d", nf_.nodes[rank_].ip.c_str(),
+                      data_->port());
+        rg.flags = (uint16_t)(rg.flags & ~REGION_DEDICATED);
+    }
     OwnedExtent oe;
     oe.slab_id = rg.slab_id;
     oe.offset = rg.offset;
@@ -1219,7 +1252,8 @@ void Daemon::finish_alloc(Pending &p) {
     const uint64_t id = p.alloc_id;
     if (oa.extents.size() == 1 && cfg_.lease_bytes && oa.extents[0].owner_rank != rank_ &&
         (oa.extents[0].tier == TIER_GPU || (cfg_.lease_host && oa.extents[0].tier == TIER_HOST)) &&
-        !(oa.extents[0].flags & REGION_SPILLED) && ++lease_demand_[oa.extents[0].owner_rank] >= cfg_.lease_after)
+        !(oa.extents[0].flags & (REGION_SPILLED | REGION_NET)) &&
+        ++lease_demand_[oa.extents[0].owner_rank] >= cfg_.lease_after)
         request_lease(oa.extents[0].owner_rank, oa.extents[0].tier);
     origin_allocs_[id] = oa;
     n_alloc_++;
@@ -1566,6 +1600,11 @@ bool Daemon::try_lease_alloc(Msg &m) {
         return true;
     }
     return false;
+}
+
+bool Daemon::cross_host(int a, int b) const {
+    if (a < 0 || b < 0 || a >= n_ || b >= n_) return false;
+    return std::strncmp(table_[a].host, table_[b].host, sizeof(table_[a].host)) != 0;
 }
 
 }  // namespace ocm

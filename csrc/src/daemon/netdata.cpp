@@ -1,0 +1,140 @@
+#include "ocm/netdata.h"
+
+#include <hip/hip_runtime_api.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+
+#include "ocm/arena.h"
+#include "ocm/log.h"
+#include "ocm/sock.h"
+
+namespace ocm {
+
+bool parse_net_handle(const uint8_t *handle, std::string *ip, int *port) {
+    char buf[65] = {0};
+    std::memcpy(buf, handle, 64);
+    char host[64] = {0};
+    int p = 0;
+    if (std::sscanf(buf, "net:%63[^:]:%d", host, &p) != 2 || p <= 0) return false;
+    *ip = host;
+    *port = p;
+    return true;
+}
+
+DataServer::DataServer(Arena *arena, int gpu) : arena_(arena), gpu_(gpu) {}
+
+DataServer::~DataServer() { stop(); }
+
+int DataServer::start(const std::string &bind_ip) {
+    listen_fd_ = tcp_listen(bind_ip, 0, 64);
+    if (listen_fd_ < 0) return -1;
+    struct sockaddr_in a;
+    socklen_t l = sizeof(a);
+    if (getsockname(listen_fd_, (struct sockaddr *)&a, &l) != 0) return -1;
+    port_ = ntohs(a.sin_port);
+    acceptor_ = std::thread([this] { accept_loop(); });
+    return 0;
+}
+
+void DataServer::stop() {
+    if (!acceptor_.joinable()) return;
+    stop_ = true;
+    shutdown(listen_fd_, SHUT_RDWR);
+    acceptor_.join();
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (int fd : conns_) shutdown(fd, SHUT_RDWR);
+    }
+    for (auto &t : workers_)
+        if (t.joinable()) t.join();
+    close(listen_fd_);
+    listen_fd_ = -1;
+}
+
+void DataServer::accept_loop() {
+    while (!stop_) {
+        struct pollfd p = {listen_fd_, POLLIN, 0};
+        int rc = poll(&p, 1, 200);
+        if (rc <= 0) continue;
+        int fd = tcp_accept(listen_fd_);
+        if (fd < 0) continue;
+        std::lock_guard<std::mutex> lk(mu_);
+        conns_.push_back(fd);
+        workers_.emplace_back([this, fd] { serve(fd); });
+    }
+}
+
+void DataServer::serve(int fd) {
+    void *stage = nullptr;
+    if (gpu_ >= 0) {
+        (void)hipSetDevice(gpu_);
+        if (hipHostMalloc(&stage, kNetChunk, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            stage = nullptr;
+        }
+    }
+    std::vector<char> sink;
+    NetReq q;
+    while (!stop_ && recv_all(fd, &q, sizeof(q)) == 1) {
+        NetResp r{kNetMagic, 0, q.len};
+        if (q.magic != kNetMagic) break;
+        void *mem = nullptr;
+        uint32_t tier = 0;
+        if (q.op == NET_PING) {
+            r.len = 0;
+            if (send_all(fd, &r, sizeof(r)) != 1) break;
+            continue;
+        }
+        if (!arena_->locate(q.slab_id, q.offset, q.len, &mem, &tier)) r.err = EFAULT;
+        if (tier == TIER_GPU && !stage) r.err = r.err ? r.err : ENOMEM;
+        bool ok = true;
+        if (q.op == NET_PUT) {
+            for (uint64_t done = 0; ok && done < q.len;) {
+                const size_t n = (size_t)std::min<uint64_t>(kNetChunk, q.len - done);
+                if (r.err) {
+                    sink.resize(n);
+                    ok = recv_all(fd, sink.data(), n) == 1;  // keep the stream in sync
+                } else if (tier == TIER_HOST) {
+                    ok = recv_all(fd, static_cast<char *>(mem) + done, n) == 1;
+                } else {
+                    ok = recv_all(fd, stage, n) == 1 &&
+                         hipMemcpy(static_cast<char *>(mem) + done, stage, n, hipMemcpyHostToDevice) == hipSuccess;
+                }
+                done += n;
+            }
+            if (!ok || send_all(fd, &r, sizeof(r)) != 1) break;
+        } else if (q.op == NET_GET) {
+            if (r.err) r.len = 0;
+            if (send_all(fd, &r, sizeof(r)) != 1) break;
+            for (uint64_t done = 0; ok && !r.err && done < q.len;) {
+                const size_t n = (size_t)std::min<uint64_t>(kNetChunk, q.len - done);
+                if (tier == TIER_HOST) {
+                    ok = send_all(fd, static_cast<char *>(mem) + done, n) == 1;
+                } else {
+                    ok = hipMemcpy(stage, static_cast<char *>(mem) + done, n, hipMemcpyDeviceToHost) == hipSuccess &&
+                         send_all(fd, stage, n) == 1;
+                }
+                done += n;
+            }
+            if (!ok) break;
+        } else {
+            break;
+        }
+    }
+    if (stage) (void)hipHostFree(stage);
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto it = conns_.begin(); it != conns_.end(); ++it)
+        if (*it == fd) {
+            conns_.erase(it);
+            break;
+        }
+    close(fd);
+}
+
+}  // namespace ocm

@@ -32,7 +32,9 @@
 #include "oncillamem.h"
 #include "ocm/log.h"
 #include "ocm/msg.h"
+#include "ocm/netdata.h"
 #include "ocm/pmsg.h"
+#include "ocm/sock.h"
 #include "ocm/trace.h"
 #include "ocm/xfer.h"
 
@@ -47,6 +49,8 @@ struct Extent {
     char *dptr = nullptr;  // device-usable address of the extent start (nullptr: none)
     char *hptr = nullptr;  // host address (host tier only)
     bool dev_ok = false;   // a kernel on this process's GPU can access dptr
+    bool net = false;      // owner on another node: streamed through its data server
+    std::string ep;        // "ip:port" of that data server
 };
 
 }  // namespace
@@ -64,6 +68,7 @@ struct lib_alloc {
     bool all_gpu = false;
     bool any_gpu = false;
     bool all_dev_ok = false;  // every extent reachable by a kernel on this GPU
+    bool any_net = false;     // some extent lives on another node
     bool async_pending = false;
 };
 
@@ -113,6 +118,9 @@ struct State {
     unsigned long long svc_seq = 0;
     uint64_t svc_max = 128ull << 10;  // measured: launches win above ~128 KiB
     unsigned long long svc_idle_ticks = 200000ull;  // 2 ms at 100 MHz: live only during bursts of small ops
+    // network tier
+    std::map<std::string, int> net_conns;  // "ip:port" -> connected socket
+    void *net_stage = nullptr;             // pinned staging buffer (device-side local halves)
     hipEvent_t done = nullptr;
     int rpc_timeout_ms = 60000;
 };
@@ -194,6 +202,18 @@ bool is_pair(enum ocm_kind k) { return k == OCM_REMOTE_GPU || k == OCM_REMOTE_RD
 int import_extent(Extent &e) {
     State &s = S();
     const Region &r = e.r;
+    if (r.flags & REGION_NET) {
+        char buf[65] = {0};
+        std::memcpy(buf, r.handle, 64);
+        char host[64] = {0};
+        int port = 0;
+        if (std::sscanf(buf, "net:%63[^:]:%d", host, &port) != 2 || port <= 0)
+            OCM_FAIL(-1, "bad network-tier handle '%s'", buf);
+        e.net = true;
+        e.dev_ok = false;
+        e.ep = std::string(host) + ":" + std::to_string(port);
+        return 0;
+    }
     SlabKey key{r.owner_rank, r.tier, r.slab_id};
     auto it = s.imports.find(key);
     if (it != s.imports.end() && std::memcmp(it->second.handle, r.handle, kHandleBytes) != 0) {
@@ -254,6 +274,7 @@ int import_extent(Extent &e) {
 
 void release_extent(const Extent &e, bool force) {
     State &s = S();
+    if (e.net) return;
     SlabKey key{e.r.owner_rank, e.r.tier, e.r.slab_id};
     auto it = s.imports.find(key);
     if (it == s.imports.end()) return;
@@ -406,11 +427,113 @@ int service_xfer(XferArgs x) {
     }
 }
 
+// ---- network tier client ----
+
+int net_conn(const std::string &ep) {
+    State &s = S();
+    auto it = s.net_conns.find(ep);
+    if (it != s.net_conns.end()) return it->second;
+    const size_t colon = ep.rfind(':');
+    int fd = tcp_connect(ep.substr(0, colon), std::atoi(ep.c_str() + colon + 1), 10000);
+    if (fd < 0) OCM_FAIL(-1, "cannot reach data server %s", ep.c_str());
+    s.net_conns[ep] = fd;
+    return fd;
+}
+
+void net_drop(const std::string &ep) {
+    State &s = S();
+    auto it = s.net_conns.find(ep);
+    if (it == s.net_conns.end()) return;
+    close(it->second);
+    s.net_conns.erase(it);
+}
+
+// Blocking one-sided PUT/GET of one contiguous piece over TCP. Device-side
+// local memory is staged through a pinned buffer, kNetChunk at a time.
+int net_piece(const Extent &e, bool put, char *lin, Loc lloc, uint64_t ext_off, uint64_t len) {
+    State &s = S();
+    int fd = net_conn(e.ep);
+    if (fd < 0) return -1;
+    NetReq q{kNetMagic, put ? (uint32_t)NET_PUT : (uint32_t)NET_GET, e.r.slab_id, e.r.tier, e.r.offset + ext_off, len};
+    const bool dev = lloc == LOC_DEVICE;
+    if (dev && !s.net_stage) {
+        DeviceGuard g(s.device);
+        if (hipHostMalloc(&s.net_stage, kNetChunk, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            s.net_stage = nullptr;
+            OCM_FAIL(-1, "no pinned staging buffer for the network tier");
+        }
+    }
+    auto fail = [&](const char *what) {
+        net_drop(e.ep);
+        set_last_error("network tier %s with %s failed", what, e.ep.c_str());
+        return -1;
+    };
+    if (send_all(fd, &q, sizeof(q)) != 1) return fail("request");
+    NetResp r;
+    if (put) {
+        for (uint64_t done = 0; done < len;) {
+            const size_t n = (size_t)std::min<uint64_t>(kNetChunk, len - done);
+            const char *src = lin + done;
+            if (dev) {
+                DeviceGuard g(s.device);
+                if (hipMemcpy(s.net_stage, lin + done, n, hipMemcpyDeviceToHost) != hipSuccess) return fail("staging");
+                src = static_cast<const char *>(s.net_stage);
+            }
+            if (send_all(fd, src, n) != 1) return fail("payload");
+            done += n;
+        }
+        if (recv_all(fd, &r, sizeof(r)) != 1 || r.magic != kNetMagic) return fail("response");
+        if (r.err) OCM_FAIL(-1, "remote PUT refused: %s", strerror(r.err));
+        return 0;
+    }
+    if (recv_all(fd, &r, sizeof(r)) != 1 || r.magic != kNetMagic) return fail("response");
+    if (r.err) OCM_FAIL(-1, "remote GET refused: %s", strerror(r.err));
+    for (uint64_t done = 0; done < len;) {
+        const size_t n = (size_t)std::min<uint64_t>(kNetChunk, len - done);
+        char *dst = dev ? static_cast<char *>(s.net_stage) : lin + done;
+        if (recv_all(fd, dst, n) != 1) return fail("payload");
+        if (dev) {
+            DeviceGuard g(s.device);
+            if (hipMemcpy(lin + done, s.net_stage, n, hipMemcpyHostToDevice) != hipSuccess) return fail("staging");
+        }
+        done += n;
+    }
+    return 0;
+}
+
 // One-sided transfer between the linear buffer `lin` (location `lloc`) and the
 // remote half of `a` at striped offset `rem_off`.
 int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async) {
     State &s = S();
     if (len == 0) return 0;
+    if (a->any_net) {
+        // Another node: stream every piece through its owner's data server (blocking).
+        std::vector<Seg> segs;
+        segments(a, rem_off, len, segs);
+        if (a->async_pending && sync_stream() != 0) return -1;
+        a->async_pending = false;
+        for (auto &g : segs) {
+            const Extent &e = a->ext[g.ext];
+            if (e.net) {
+                if (net_piece(e, put, lin + g.lin_off, lloc, g.ext_off, g.len) != 0) return -1;
+                continue;
+            }
+            // mixed placement: this piece is on this node
+            char *r = (lloc == LOC_DEVICE || e.r.tier == TIER_GPU) ? e.dptr : e.hptr;
+            r += g.ext_off;
+            if (s.device < 0 || (lloc != LOC_DEVICE && e.r.tier != TIER_GPU)) {
+                std::memcpy(put ? r : lin + g.lin_off, put ? lin + g.lin_off : r, g.len);
+            } else {
+                DeviceGuard dg(s.device);
+                if ((put ? hipMemcpyAsync(r, lin + g.lin_off, g.len, hipMemcpyDefault, s.stream)
+                         : hipMemcpyAsync(lin + g.lin_off, r, g.len, hipMemcpyDefault, s.stream)) != hipSuccess)
+                    OCM_FAIL(-1, "transfer launch failed");
+                if (sync_stream() != 0) return -1;
+            }
+        }
+        return 0;
+    }
     std::vector<Seg> segs;
     if (s.device < 0) {
         segments(a, rem_off, len, segs);
@@ -673,6 +796,13 @@ int ocm_tini(void) {
     }
     s.imports.clear();
     service_stop();
+    for (auto &kv : s.net_conns) close(kv.second);
+    s.net_conns.clear();
+    if (s.net_stage) {
+        DeviceGuard g(s.device);
+        (void)hipHostFree(s.net_stage);
+        s.net_stage = nullptr;
+    }
     if (s.stream) {
         DeviceGuard g(s.device);
         (void)hipStreamDestroy(s.stream);
@@ -766,7 +896,12 @@ static ocm_alloc_t alloc_impl(ocm_alloc_param_t p, const struct ocm_alloc_ex_par
             }
             a->all_gpu = all;
             a->all_dev_ok = true;
-            for (auto &e : a->ext) a->all_dev_ok &= e.dev_ok;
+            for (auto &e : a->ext) {
+                a->all_dev_ok &= e.dev_ok;
+                a->any_net |= e.net;
+                if (e.net) a->all_gpu = false;
+            }
+            a->any_gpu = a->any_gpu && !a->any_net;
             Loc want = kind == OCM_REMOTE_GPU ? LOC_DEVICE : LOC_PINNED;
             ok = alloc_local_half(a, p->local_alloc_bytes, want) == 0;
         }
@@ -961,6 +1096,18 @@ static int copy_impl(ocm_alloc_t dst, ocm_alloc_t src, ocm_param_t p) {
     // remote -> remote (not supported by the reference): direct, no staging.
     if (!range_ok(q.src_offset, n, src->remote_bytes) || !range_ok(q.dest_offset, n, dst->remote_bytes))
         OCM_FAIL(-1, "ocm_copy: range out of bounds");
+    if (src->any_net || dst->any_net) {
+        // A side on another node: bounce through host memory, 64 MiB at a time.
+        const uint64_t chunk = std::min<uint64_t>(n, 64ull << 20);
+        std::vector<char> tmp(chunk);
+        for (uint64_t done = 0; done < n;) {
+            const uint64_t k = std::min(chunk, n - done);
+            if (xfer(src, false, tmp.data(), LOC_HOST, q.src_offset + done, k, false) != 0) return -1;
+            if (xfer(dst, true, tmp.data(), LOC_HOST, q.dest_offset + done, k, false) != 0) return -1;
+            done += k;
+        }
+        return 0;
+    }
     std::vector<Seg> ss;
     segments(src, q.src_offset, n, ss);
     for (auto &g : ss) {
@@ -1006,12 +1153,13 @@ int ocm_remote_info(ocm_alloc_t a, struct ocm_remote_info *info) {
         info->owner_rank[i] = a->ext[i].r.owner_rank;
         info->owner_gpu[i] = a->ext[i].r.owner_gpu;
         info->extent_bytes[i] = a->ext[i].r.bytes;
+        if (a->ext[i].net) info->net_mask |= 1u << i;
     }
     return a->remote ? 0 : -1;
 }
 
 void *ocm_remotebuf(ocm_alloc_t a) {
-    if (!a || a->ext.size() != 1) return nullptr;
+    if (!a || a->ext.size() != 1 || a->ext[0].net) return nullptr;
     return S().device >= 0 ? a->ext[0].dptr : a->ext[0].hptr;
 }
 

@@ -209,8 +209,22 @@ static void t_governor_hosts() {
     pr.orig_rank = 3;
     p = gov.place(pr);
     CHECK(p.err == 0 && p.extents.size() == 1 && p.extents[0].owner == 2);
-    pr.remote_rank = 0;
-    CHECK(gov.place(pr).err == EXDEV);
+    CHECK(!p.extents[0].net);
+    pr.remote_rank = 0;  // explicit owner on the other host: network tier
+    p = gov.place(pr);
+    CHECK(p.err == 0 && p.extents[0].owner == 0 && p.extents[0].net);
+    // one daemon per host (the reference layout): ring to the next node
+    Governor g2(2, Policy::Ring, 1 << 20);
+    for (int r = 0; r < 2; r++) {
+        NodeConfig c = cfg(r, 8 * G, G);
+        std::snprintf(c.host, sizeof(c.host), "host%d", r);
+        g2.add_node(c);
+    }
+    PlaceRequest q;
+    q.orig_rank = 1;
+    q.bytes = 1 << 20;
+    p = g2.place(q);
+    CHECK(p.err == 0 && p.extents[0].owner == 0 && p.extents[0].net && p.extents[0].tier == TIER_GPU);
 }
 
 static void t_stripe_geometry() {

@@ -85,6 +85,8 @@ class OcmRemoteInfo(ctypes.Structure):
         ("stripe_unit", ctypes.c_uint64),
         ("alloc_id", ctypes.c_uint64),
         ("remote_bytes", ctypes.c_uint64),
+        ("net_mask", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -241,7 +243,7 @@ class Allocation:
             "stripe_unit": info.stripe_unit,
             "extents": [
                 {"owner_rank": info.owner_rank[i], "owner_gpu": info.owner_gpu[i], "tier": info.tier[i],
-                 "bytes": info.extent_bytes[i]}
+                 "bytes": info.extent_bytes[i], "net": bool(info.net_mask >> i & 1)}
                 for i in range(n)
             ],
         }

@@ -167,3 +167,30 @@ def test_tensor_views_on_peer_memory(mesh_factory):
         a.get(0, 0, 4 * n)
         assert torch.equal(loc, 2.0 * torch.arange(n, dtype=torch.float32, device="cuda:0"))
         a.free()
+
+
+def test_network_tier_hbm_owner(mesh_factory):
+    # two "nodes" (host aliases) sharing the MI355X: rank1's HBM is reached through its
+    # data server, the app's local half is device memory staged through pinned buffers
+    m = mesh_factory(2, gpus=[0, 0], rank_env={0: {"OCM_HOST_ALIAS": "nodeA"}, 1: {"OCM_HOST_ALIAS": "nodeB"}})
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = (24 << 20) + 4096
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n)
+        e = a.remote_info()["extents"][0]
+        assert e["owner_rank"] == 1 and e["tier"] == api.OCM_TIER_GPU and e["net"]
+        a.fill(seed=17)
+        a.put(0, 0, n)
+        a.fill(seed=0)
+        a.get(0, 0, n)
+        assert a.check(seed=17) == 0
+        t = torch.arange(n // 4, dtype=torch.int32, device="cuda:0")
+        a.local_tensor(torch.int32)[: n // 4].copy_(t)
+        torch.cuda.synchronize()
+        a.put(0, 4096, n - 4096)
+        a.local_tensor(torch.int32).zero_()
+        torch.cuda.synchronize()
+        a.get(0, 4096, n - 4096)
+        torch.cuda.synchronize()
+        assert torch.equal(a.local_tensor(torch.int32)[: (n - 4096) // 4], t[: (n - 4096) // 4])
+        assert c.stats(1)["gpu_used"] >= n
+        a.free()

@@ -1,0 +1,85 @@
+"""Network tier: remote memory on another node.
+
+Daemons started with different host aliases (OCM_HOST_ALIAS) behave as if on
+different nodes: the governor keeps placements on the origin's host when it has
+peers there, places on the next node otherwise (or when the app names a remote
+rank explicitly), and such extents are reached through the owner's data
+server (PUT/GET records over TCP) instead of an IPC/memfd mapping.
+
+Parity: reference src/rdma.c / src/extoll.c one-sided verbs to another host;
+the reference's test 3/4 (cross-node RDMA/RMA) — SURVEY §4.
+"""
+import pytest
+
+from oncilla_amd import api
+
+
+@pytest.fixture(autouse=True)
+def _cpu_app(monkeypatch):
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+
+
+def hosts(*names):
+    return {r: {"OCM_HOST_ALIAS": h} for r, h in enumerate(names)}
+
+
+def test_two_nodes_remote_is_network(mesh_factory):
+    m = mesh_factory(2, rank_env=hosts("nodeA", "nodeB"))
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=8 << 20, remote_bytes=8 << 20)
+        ext = a.remote_info()["extents"]
+        assert len(ext) == 1 and ext[0]["owner_rank"] == 1 and ext[0]["net"]
+        a.fill(seed=7)
+        a.put(0, 0, 8 << 20)
+        a.fill(seed=0)
+        a.get(0, 0, 8 << 20)
+        assert a.check(seed=7) == 0
+        # unaligned pieces through the same connection
+        a.fill(seed=9)
+        a.put(124, 4567, 1 << 20)
+        a.fill(seed=0)
+        a.get(124, 4567, 1 << 20)
+        assert a.check(seed=9, offset=124, nbytes=1 << 20) == 0
+        assert c.stats(1)["host_used"] >= 8 << 20
+        a.free()
+        assert c.stats(1)["host_used"] == 0
+
+
+def test_same_host_preferred_over_network(mesh_factory):
+    m = mesh_factory(4, rank_env=hosts("nodeA", "nodeA", "nodeB", "nodeB"))
+    with api.Client(daemon_rank=2, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)
+        ext = a.remote_info()["extents"][0]
+        assert ext["owner_rank"] == 3 and not ext["net"]
+        # an explicit cross-node owner is honoured and goes over the network
+        b = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20, remote_rank=0)
+        ext = b.remote_info()["extents"][0]
+        assert ext["owner_rank"] == 0 and ext["net"]
+        b.fill(seed=3)
+        b.put(0, 0, 1 << 20)
+        # remote -> remote copy between a same-node and a cross-node allocation
+        api.copy(a, b, 1 << 20)  # remote -> remote: network source, same-node destination
+        a.fill(seed=0)
+        a.get(0, 0, 1 << 20)
+        assert a.check(seed=3) == 0
+        a.free()
+        b.free()
+
+
+def test_ocm_test_suite_across_nodes(mesh_factory, tool, native):
+    m = mesh_factory(2, rank_env=hosts("nodeA", "nodeB"))
+    for args in (["1", "1", "2", "3"], ["1", "1", "2", "4"], ["2", "4", "8"], ["3", "4", "4"], ["4", "1", "2", "4"]):
+        rc, out = tool([f"{native}/ocm_test", *args], env=dict(m.client_env(0), OCM_NO_GPU="1"))
+        assert rc == 0, out
+
+
+def test_owner_loss_fails_network_ops(mesh_factory):
+    m = mesh_factory(2, rank_env=hosts("nodeA", "nodeB"))
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)
+        a.put(0, 0, 4096)
+        m.kill(1)
+        with pytest.raises(api.OcmError):
+            for _ in range(50):  # the first op may still drain into the socket buffer
+                a.put(0, 0, 1 << 20)
+                a.get(0, 0, 1 << 20)
