@@ -25,7 +25,7 @@ struct ArenaConfig {
     int gpu = -1;                    // -1: CPU-only daemon, no GPU tier
     uint64_t gpu_capacity = 0;       // max bytes handed out from HBM
     uint64_t host_capacity = 0;      // max bytes handed out from the host tier
-    uint64_t slab_bytes = 1ull << 30;
+    uint64_t slab_bytes = 4ull << 30;  // HBM slab: requests < 2 GiB carve from resident slabs
     uint64_t align = 4096;           // sub-allocation alignment
     bool zero_on_alloc = false;
 };

@@ -39,7 +39,7 @@ struct DaemonConfig {
     std::string ns;
     Policy policy = Policy::Ring;
     uint64_t stripe_unit = 1ull << 20;
-    uint64_t slab_bytes = 1ull << 30;
+    uint64_t slab_bytes = 4ull << 30;  // HBM slab: requests < 2 GiB carve from resident slabs
     uint64_t gpu_capacity = 0;       // 0: fraction of free HBM
     double gpu_fraction = 0.75;
     uint64_t host_capacity = 0;      // 0: fraction of MemAvailable

@@ -4,6 +4,7 @@
 #include <sys/mman.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
@@ -123,7 +124,9 @@ int Arena::alloc(uint32_t tier, uint64_t bytes, Region *out) {
     if (bytes == 0) return EINVAL;
     if (tier != TIER_GPU && tier != TIER_HOST) return EINVAL;
     if ((tier == TIER_GPU ? used_gpu_ : used_host_) + bytes > capacity(tier)) return ENOMEM;
-    const uint64_t slab_default = tier == TIER_GPU ? cfg_.slab_bytes : std::min<uint64_t>(cfg_.slab_bytes, 256ull << 20);
+    uint64_t slab_default = tier == TIER_GPU ? cfg_.slab_bytes : std::min<uint64_t>(cfg_.slab_bytes, 256ull << 20);
+    // Never map more than the tier may hand out (small capacities in tests / shared GPUs).
+    slab_default = std::max(kHugeAlign, std::min(slab_default, (capacity(tier) + kHugeAlign - 1) & ~(kHugeAlign - 1)));
     Slab *slab = nullptr;
     uint64_t off = 0;
     int err = 0;

@@ -70,6 +70,7 @@ struct lib_alloc {
     bool all_dev_ok = false;  // every extent reachable by a kernel on this GPU
     bool any_net = false;     // some extent lives on another node
     bool async_pending = false;
+    bool pooled = false;      // local half from the stream-ordered pool
 };
 
 namespace {
@@ -121,6 +122,11 @@ struct State {
     // network tier
     std::map<std::string, int> net_conns;  // "ip:port" -> connected socket
     void *net_stage = nullptr;             // pinned staging buffer (device-side local halves)
+    // Local GPU halves: stream-ordered pool (no device-wide sync in free, freed
+    // blocks reused without a new VA mapping). Reference K8: cudaMalloc/cudaFree.
+    hipMemPool_t pool = nullptr;
+    bool pool_tried = false;
+    uint64_t pool_keep = 8ull << 30;       // bytes kept reserved across frees
     hipEvent_t done = nullptr;
     int rpc_timeout_ms = 60000;
 };
@@ -656,10 +662,51 @@ Loc pointer_loc(const void *p) {
     return LOC_HOST;
 }
 
+hipMemPool_t local_pool() {
+    State &s = S();
+    if (s.pool_tried) return s.pool;
+    s.pool_tried = true;
+    if (s.device < 0 || !env_int("OCM_LOCAL_POOL", 1)) return nullptr;
+    DeviceGuard g(s.device);
+    hipMemPoolProps props;
+    std::memset(&props, 0, sizeof(props));
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = s.device;
+    if (hipMemPoolCreate(&s.pool, &props) != hipSuccess) {
+        (void)hipGetLastError();
+        OCM_WARN("hipMemPoolCreate on device %d failed; local halves use hipMalloc", s.device);
+        s.pool = nullptr;
+        return nullptr;
+    }
+    if (const char *k = std::getenv("OCM_LOCAL_POOL_KEEP")) s.pool_keep = std::strtoull(k, nullptr, 0);
+    uint64_t keep = s.pool_keep;
+    (void)hipMemPoolSetAttribute(s.pool, hipMemPoolAttrReleaseThreshold, &keep);
+    // Peers read/write the local half too (SDMA from peer engines, torch on another GPU).
+    int ndev = 0;
+    (void)hipGetDeviceCount(&ndev);
+    for (int p = 0; p < ndev; p++) {
+        int can = 0;
+        if (p == s.device || hipDeviceCanAccessPeer(&can, p, s.device) != hipSuccess || !can) continue;
+        hipMemAccessDesc d;
+        d.location.type = hipMemLocationTypeDevice;
+        d.location.id = p;
+        d.flags = hipMemAccessFlagsProtReadWrite;
+        if (hipMemPoolSetAccess(s.pool, &d, 1) != hipSuccess) (void)hipGetLastError();
+    }
+    return s.pool;
+}
+
 int free_local_half(lib_alloc *a) {
     State &s = S();
     if (!a->local) return 0;
-    if (a->loc == LOC_DEVICE) {
+    if (a->pooled) {
+        DeviceGuard g(s.device);
+        // Ordered after every transfer queued on s.stream; the block returns to the pool.
+        if (hipFreeAsync(a->local, s.stream) != hipSuccess) (void)hipGetLastError();
+        a->pooled = false;
+    } else if (a->loc == LOC_DEVICE) {
         DeviceGuard g(s.device);
         (void)hipFree(a->local);
     } else if (a->loc == LOC_PINNED) {
@@ -677,7 +724,17 @@ int alloc_local_half(lib_alloc *a, size_t bytes, Loc want) {
     a->local_bytes = bytes;
     if (bytes == 0) return 0;
     if (want != LOC_HOST && s.device < 0) want = LOC_HOST;
-    if (want == LOC_DEVICE) {
+    if (want == LOC_DEVICE && local_pool()) {
+        DeviceGuard g(s.device);
+        hipError_t e = hipMallocFromPoolAsync(&a->local, bytes, s.pool, s.stream);
+        // The app may touch the buffer from any stream as soon as ocm_alloc returns.
+        if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            OCM_FAIL(-1, "pool allocation of %zu bytes for local half: %s", bytes, hipGetErrorString(e));
+        }
+        a->pooled = true;
+    } else if (want == LOC_DEVICE) {
         DeviceGuard g(s.device);
         hipError_t e = hipMalloc(&a->local, bytes);
         if (e != hipSuccess) {
@@ -805,9 +862,16 @@ int ocm_tini(void) {
     }
     if (s.stream) {
         DeviceGuard g(s.device);
+        (void)hipStreamSynchronize(s.stream);
         (void)hipStreamDestroy(s.stream);
         s.stream = nullptr;
     }
+    if (s.pool) {
+        DeviceGuard g(s.device);
+        (void)hipMemPoolDestroy(s.pool);
+        s.pool = nullptr;
+    }
+    s.pool_tried = false;
     s.chan.close();
     s.inited = false;
     trace_flush("app");
