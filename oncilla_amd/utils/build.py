@@ -21,12 +21,18 @@ def _env() -> dict:
     return env
 
 
-def build(jobs: int | None = None, sanitize: bool = False, verbose: bool = False) -> str:
-    """Configure (once) and build every native target. Returns the build dir."""
+def build(jobs: int | None = None, sanitize: bool | str = False, verbose: bool = False) -> str:
+    """Configure (once) and build every native target. Returns the build dir.
+
+    sanitize: False, True / "address" (ASan+UBSan, ``build-asan``) or
+    "thread" (TSan, ``build-tsan``); host code only.
+    """
     jobs = jobs or min(16, os.cpu_count() or 8)
     env = _env()
     gen = ["-G", "Ninja"] if shutil.which("ninja", path=env["PATH"]) else []
-    bdir = BUILD_DIR if not sanitize else BUILD_DIR + "-asan"
+    if sanitize is True:
+        sanitize = "address"
+    bdir = BUILD_DIR if not sanitize else BUILD_DIR + ("-tsan" if sanitize == "thread" else "-asan")
     if not os.path.exists(os.path.join(bdir, "CMakeCache.txt")):
         cmd = [
             "cmake", "-S", REPO, "-B", bdir, *gen,
@@ -36,7 +42,7 @@ def build(jobs: int | None = None, sanitize: bool = False, verbose: bool = False
             "-DCMAKE_BUILD_TYPE=Release",
         ]
         if sanitize:
-            cmd.append("-DOCM_SANITIZE=ON")
+            cmd.append("-DOCM_SANITIZE=" + ("thread" if sanitize == "thread" else "ON"))
         subprocess.run(cmd, check=True, env=env, capture_output=not verbose)
     subprocess.run(["cmake", "--build", bdir, "-j", str(jobs)], check=True, env=env,
                    capture_output=not verbose)

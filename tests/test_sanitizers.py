@@ -38,3 +38,26 @@ def test_mesh_under_asan(asan_bin):
         m.stop()
     logs = m.logs()
     assert not any(b in logs for b in BAD), logs
+
+
+@pytest.fixture(scope="module")
+def tsan_bin():
+    return os.path.join(build(sanitize="thread"), "bin")
+
+
+def test_threads_under_tsan(tsan_bin):
+    # Threads in the daemon: the tick transport thread (socket collective) and
+    # the network-tier data server (rank 2 is alone on "node B", so its app's
+    # remote halves live on node A and are streamed through rank 0/1 servers).
+    env = {"OCM_NO_GPU": "1", "TSAN_OPTIONS": "halt_on_error=0"}
+    hosts = {0: {"OCM_HOST_ALIAS": "A"}, 1: {"OCM_HOST_ALIAS": "A"}, 2: {"OCM_HOST_ALIAS": "B"}}
+    m = Mesh(3, bin_dir=tsan_bin, env=env, extra_args=["--ctrl", "socket"], rank_env=hosts).start(timeout=120)
+    try:
+        for args in (["1", "1", "2", "3"], ["2", "4", "8"], ["3", "2", "4"], ["4", "1", "2", "2"]):
+            r = subprocess.run([f"{tsan_bin}/ocm_test", *args], capture_output=True, text=True, timeout=300,
+                               env=dict(m.client_env(2), **env))
+            assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, f"{args}\n{r.stdout}\n{r.stderr}"
+    finally:
+        m.stop()
+    logs = m.logs()
+    assert "WARNING: ThreadSanitizer" not in logs, logs
