@@ -54,6 +54,8 @@ struct DaemonConfig {
     int lease_after = 2;             // normal placements on an owner before leasing there
     bool lease_host = false;         // also lease host-tier capacity (tests; OCM_LEASE_HOST=1)
     std::string host_alias;          // report this host name (tests: pretend daemons are on other nodes)
+    std::string state_file;          // rank0: directory checkpoint (resume after a rank0 restart)
+    int state_interval_ms = 20;      // max staleness of that checkpoint while the directory changes
 };
 
 int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err);
@@ -118,6 +120,11 @@ private:
         uint32_t tier = 0;
         int orig_rank = -1;
         uint64_t bytes = 0;
+        // what rank0 needs to rebuild its directory entry after a restart
+        int app_pid = 0;
+        uint16_t flags = 0;
+        uint16_t n_extents = 1;
+        uint64_t stripe_unit = 0;
     };
 
     int init();
@@ -150,7 +157,10 @@ private:
     void app_req_alloc(Msg &m);
     void app_req_free(Msg &m);
     void app_stats(Msg &m);
-    void r0_add_node(const NodeConfig &cfg);
+    void r0_add_node(const NodeConfig &cfg, uint64_t boot_id);
+    void join_rank0();                   // ADD_NODE + OWNED report (boot and rejoin)
+    void try_rejoin_rank0();             // survivors: reconnect to a restarted rank0
+    void save_checkpoint(bool force);
     void r0_req_alloc(Msg &m);
     void r0_place_fail(Msg &m);
     void owner_do_alloc(Msg &m);
@@ -206,6 +216,13 @@ private:
     int fault_alloc_fail_ = 0, fault_drop_alloc_ = 0, fault_crash_after_ = -1;
     void parse_faults();
     uint64_t n_alloc_ = 0, n_free_ = 0, n_reclaimed_ = 0, n_spilled_ = 0;
+    // checkpoint / resume
+    uint64_t boot_id_ = 0;               // this process lifetime
+    bool resumed_ = false;               // rank0 restored its directory from state_file
+    uint64_t saved_version_ = 0;
+    long last_save_ms_ = 0;
+    bool r0_lost_ = false;               // survivors: link to rank0 down, retrying
+    long next_rejoin_ms_ = 0;
 };
 
 }  // namespace ocm

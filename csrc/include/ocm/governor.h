@@ -36,6 +36,7 @@ struct NodeState {
     uint64_t gpu_capacity = 0, gpu_reserved = 0;
     uint64_t host_capacity = 0, host_reserved = 0;
     std::string host;
+    uint64_t boot_id = 0;      // identifies one ocmd process lifetime (resume: same id = memory survived)
 };
 
 struct PlacedExtent {
@@ -44,6 +45,7 @@ struct PlacedExtent {
     uint64_t bytes = 0;
     bool spilled = false;
     bool net = false;      // owner on another host: reached through the network tier
+    bool held = true;      // capacity reserved in the directory (false while unconfirmed after a resume)
 };
 
 struct PlaceRequest {
@@ -68,7 +70,11 @@ struct Placement {
 class Governor {
 public:
     Governor(int num_nodes, Policy policy, uint64_t default_stripe_unit);
-    void add_node(const NodeConfig &cfg);       // ADD_NODE
+    // ADD_NODE. A node that comes back with the same boot id kept its memory:
+    // its extents stay in the directory, unconfirmed until it reports them
+    // (confirm_extent ... end_reconcile). Any other (re)join drops what the
+    // directory thought it owned.
+    void add_node(const NodeConfig &cfg, uint64_t boot_id = 0);
     void mark_dead(int rank);
     const NodeState &node(int rank) const { return nodes_.at(rank); }
     int num_nodes() const { return static_cast<int>(nodes_.size()); }
@@ -87,6 +93,21 @@ public:
     std::vector<uint64_t> allocations_from(int orig_rank) const;
     size_t live_allocations() const { return table_.size(); }
     uint64_t spilled_count() const { return n_spilled_; }
+
+    // ---- checkpoint / resume (persist the rank0 directory) ----
+    // An owner's report of one extent it holds (OWNED): confirms a restored
+    // entry or adds one placed after the last checkpoint; re-reserves capacity.
+    void confirm_extent(int owner, const Region &r, int app_pid);
+    // End of that owner's report (OWNED_DONE): extents still unconfirmed on it
+    // were freed while rank0 was away. Returns how many were dropped.
+    int end_reconcile(int owner);
+    // Text snapshot of the directory (entries, id counter, node boot ids).
+    std::string checkpoint() const;
+    // Load a snapshot into an empty governor: entries start unconfirmed and
+    // reserve nothing until their owners rejoin. Returns entries or -1.
+    int restore(const std::string &text, std::string *err);
+    // Bumped by every directory mutation (the daemon checkpoints when it moves).
+    uint64_t version() const { return version_; }
 
     struct Entry {
         int orig_rank;
@@ -110,6 +131,7 @@ private:
     uint64_t default_stripe_unit_;
     uint64_t next_id_ = 1;
     uint64_t n_spilled_ = 0;
+    uint64_t version_ = 0;
     std::map<uint64_t, Entry> table_;
 };
 

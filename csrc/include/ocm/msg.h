@@ -22,7 +22,7 @@ enum MsgType : uint32_t {
     MSG_CONNECT,          // app -> daemon
     MSG_CONNECT_CONFIRM,  // daemon -> app (carries node config of the daemon)
     MSG_DISCONNECT,       // app -> daemon
-    MSG_ADD_NODE,         // daemon -> rank0 on boot (node config)
+    MSG_ADD_NODE,         // daemon -> rank0 on boot / rejoin (node config; seq = boot id)
     MSG_REQ_ALLOC,        // app -> daemon -> rank0
     MSG_DO_ALLOC,         // rank0 -> owner; owner -> origin daemon (response)
     MSG_REQ_FREE,         // app -> daemon
@@ -40,6 +40,8 @@ enum MsgType : uint32_t {
     MSG_PING,             // liveness / latency probe
     MSG_TICK_START,       // rank0 -> all (TCP): start the tick transport; u.raw = ncclUniqueId
     MSG_TICK_WAKE,        // any -> all (TCP): join tick number u.req.bytes
+    MSG_OWNED,            // daemon -> rank0 after ADD_NODE: one extent it holds (u.region, pid = app)
+    MSG_OWNED_DONE,       // daemon -> rank0: end of that report
     MSG_MAX
 };
 

@@ -2,6 +2,10 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstring>
+#include <iterator>
+#include <map>
+#include <sstream>
 
 #include "../../include/oncillamem.h"
 #include "ocm/log.h"
@@ -41,28 +45,42 @@ Governor::Governor(int num_nodes, Policy policy, uint64_t default_stripe_unit)
     for (int i = 0; i < num_nodes; i++) nodes_[i].rank = i;
 }
 
-void Governor::add_node(const NodeConfig &cfg) {
+void Governor::add_node(const NodeConfig &cfg, uint64_t boot_id) {
     if (cfg.rank < 0 || cfg.rank >= (int)nodes_.size()) {
         OCM_WARN("ADD_NODE for rank %d outside nodefile (%zu nodes)", cfg.rank, nodes_.size());
         return;
     }
+    version_++;
     NodeState &n = nodes_[cfg.rank];
-    if (n.joined) {
-        // A restarted daemon lost its memory: forget what it owned.
-        OCM_WARN("rank %d re-joined; dropping its previous allocations", cfg.rank);
+    const bool same = boot_id != 0 && n.boot_id == boot_id;
+    if (same) {
+        // The same process reconnected (link loss, or rank0 restarted): its memory is
+        // intact. Un-reserve its extents until its OWNED report confirms them.
+        for (auto &kv : table_)
+            for (auto &e : kv.second.placement.extents)
+                if (e.owner == cfg.rank && e.held) {
+                    reserve(e.owner, e.tier, e.bytes, -1);
+                    e.held = false;
+                }
+    } else {
+        // A new process (or an unknown one) lost whatever the directory says it owned.
+        size_t dropped = 0;
         for (auto it = table_.begin(); it != table_.end();) {
             bool owned = false;
             for (auto &e : it->second.placement.extents) owned |= e.owner == cfg.rank;
             if (owned) {
                 for (auto &e : it->second.placement.extents)
-                    if (e.owner != cfg.rank) reserve(e.owner, e.tier, e.bytes, -1);
+                    if (e.owner != cfg.rank && e.held) reserve(e.owner, e.tier, e.bytes, -1);
                 it = table_.erase(it);
+                dropped++;
             } else {
                 ++it;
             }
         }
+        if (dropped) OCM_WARN("rank %d re-joined as a new process; dropped %zu allocations it owned", cfg.rank, dropped);
         n.gpu_reserved = n.host_reserved = 0;
     }
+    n.boot_id = boot_id;
     n.joined = true;
     n.alive = true;
     n.gpu = cfg.gpu;
@@ -71,8 +89,134 @@ void Governor::add_node(const NodeConfig &cfg) {
     n.host = std::string(cfg.host, strnlen(cfg.host, sizeof(cfg.host)));
 }
 
+void Governor::confirm_extent(int owner, const Region &r, int app_pid) {
+    if (owner < 0 || owner >= (int)nodes_.size()) return;
+    version_++;
+    const int n_ext = std::max<int>(1, r.n_extents);
+    auto it = table_.find(r.alloc_id);
+    if (it == table_.end()) {
+        // Placed after the last checkpoint: rebuild the entry from the owners' reports.
+        Entry ent{r.orig_rank, app_pid, Placement{}, {}, 0};
+        ent.placement.alloc_id = r.alloc_id;
+        ent.placement.stripe_unit = r.stripe_unit;
+        ent.placement.extents.assign(n_ext, PlacedExtent{-1, TIER_NONE, 0, false, false, false});
+        it = table_.emplace(r.alloc_id, ent).first;
+    }
+    auto &ext = it->second.placement.extents;
+    if ((int)ext.size() <= r.extent_idx) ext.resize(r.extent_idx + 1, PlacedExtent{-1, TIER_NONE, 0, false, false, false});
+    PlacedExtent &e = ext[r.extent_idx];
+    if (e.held) reserve(e.owner, e.tier, e.bytes, -1);
+    e.owner = owner;
+    e.tier = r.tier;
+    e.bytes = r.bytes;
+    e.spilled = (r.flags & REGION_SPILLED) != 0;
+    e.net = (r.flags & REGION_NET) != 0;
+    e.held = true;
+    reserve(owner, e.tier, e.bytes, +1);
+    if (r.alloc_id < (1ull << 62)) next_id_ = std::max(next_id_, r.alloc_id + 1);  // rank0-issued ids only
+}
+
+int Governor::end_reconcile(int owner) {
+    int dropped = 0;
+    for (auto it = table_.begin(); it != table_.end();) {
+        bool any = false;
+        for (auto &e : it->second.placement.extents) {
+            if (e.owner == owner && !e.held) {
+                e = PlacedExtent{-1, TIER_NONE, 0, false, false, false};
+                dropped++;
+            }
+            any |= e.owner >= 0;
+        }
+        it = any ? std::next(it) : table_.erase(it);
+    }
+    if (dropped) version_++;
+    return dropped;
+}
+
+std::string Governor::checkpoint() const {
+    std::ostringstream o;
+    o << "ocm-directory 1\n" << "next_id " << next_id_ << "\n" << "spilled " << n_spilled_ << "\n";
+    for (auto &n : nodes_)
+        if (n.boot_id) o << "node " << n.rank << " " << n.boot_id << "\n";
+    for (auto &kv : table_) {
+        const Entry &e = kv.second;
+        o << "entry " << kv.first << " " << e.orig_rank << " " << e.pid << " " << e.placement.stripe_unit << " "
+          << e.placement.extents.size() << "\n";
+        for (auto &x : e.placement.extents)
+            o << "ext " << x.owner << " " << x.tier << " " << x.bytes << " " << (int)x.spilled << " " << (int)x.net
+              << "\n";
+    }
+    o << "end\n";
+    return o.str();
+}
+
+int Governor::restore(const std::string &text, std::string *err) {
+    std::istringstream in(text);
+    std::string tag;
+    int version = 0;
+    if (!(in >> tag >> version) || tag != "ocm-directory" || version != 1) {
+        *err = "not an ocm directory checkpoint";
+        return -1;
+    }
+    std::map<uint64_t, Entry> table;
+    uint64_t next_id = 1, spilled = 0;
+    std::vector<uint64_t> boots(nodes_.size(), 0);
+    Entry *cur = nullptr;
+    bool complete = false;
+    while (in >> tag) {
+        if (tag == "next_id") {
+            in >> next_id;
+        } else if (tag == "spilled") {
+            in >> spilled;
+        } else if (tag == "node") {
+            int r = -1;
+            uint64_t b = 0;
+            in >> r >> b;
+            if (r >= 0 && r < (int)boots.size()) boots[r] = b;
+        } else if (tag == "entry") {
+            uint64_t id = 0, unit = 0;
+            int orig = 0, pid = 0;
+            size_t n_ext = 0;
+            in >> id >> orig >> pid >> unit >> n_ext;
+            Entry e{orig, pid, Placement{}, {}, 0};
+            e.placement.alloc_id = id;
+            e.placement.stripe_unit = unit;
+            cur = &(table[id] = e);
+        } else if (tag == "ext") {
+            PlacedExtent x;
+            int sp = 0, net = 0;
+            in >> x.owner >> x.tier >> x.bytes >> sp >> net;
+            x.spilled = sp;
+            x.net = net;
+            x.held = false;  // reserved again once the owner confirms it
+            if (cur) cur->placement.extents.push_back(x);
+        } else if (tag == "end") {
+            complete = true;
+            break;
+        } else {
+            *err = "unexpected token '" + tag + "'";
+            return -1;
+        }
+        if (!in) {
+            *err = "truncated checkpoint";
+            return -1;
+        }
+    }
+    if (!complete) {
+        *err = "truncated checkpoint";
+        return -1;
+    }
+    table_ = std::move(table);
+    next_id_ = std::max(next_id_, next_id);
+    n_spilled_ = spilled;
+    for (size_t r = 0; r < nodes_.size(); r++) nodes_[r].boot_id = boots[r];
+    version_++;
+    return (int)table_.size();
+}
+
 void Governor::mark_dead(int rank) {
     if (rank >= 0 && rank < (int)nodes_.size()) nodes_[rank].alive = false;
+    version_++;
 }
 
 int Governor::num_alive() const {
@@ -236,6 +380,7 @@ Placement Governor::place(const PlaceRequest &r) {
     p.stripe_unit = unit;
     p.alloc_id = next_id_++;
     table_[p.alloc_id] = Entry{r.orig_rank, r.app_pid, p, {}, 0};
+    version_++;
     return p;
 }
 
@@ -244,7 +389,9 @@ bool Governor::replace_extent(uint64_t alloc_id, int idx, int failed_owner, Plac
     if (it == table_.end() || idx < 0 || idx >= (int)it->second.placement.extents.size()) return false;
     Entry &ent = it->second;
     PlacedExtent &old = ent.placement.extents[idx];
-    reserve(old.owner, old.tier, old.bytes, -1);
+    version_++;
+    if (old.held) reserve(old.owner, old.tier, old.bytes, -1);
+    old.held = false;
     // Never retry an (owner, tier) that already refused this allocation, and
     // bound the retries: the directory's view can be wrong (HBM used by other
     // processes, fragmentation), the owner's arena is authoritative.
@@ -296,8 +443,9 @@ bool Governor::release(uint64_t alloc_id) {
     auto it = table_.find(alloc_id);
     if (it == table_.end()) return false;
     for (auto &e : it->second.placement.extents)
-        if (e.owner >= 0 && e.tier != TIER_NONE) reserve(e.owner, e.tier, e.bytes, -1);
+        if (e.owner >= 0 && e.held) reserve(e.owner, e.tier, e.bytes, -1);
     table_.erase(it);
+    version_++;
     return true;
 }
 

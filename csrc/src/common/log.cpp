@@ -71,6 +71,8 @@ const char *msg_type_str(uint32_t t) {
     case MSG_PING: return "MSG_PING";
     case MSG_TICK_START: return "MSG_TICK_START";
     case MSG_TICK_WAKE: return "MSG_TICK_WAKE";
+    case MSG_OWNED: return "MSG_OWNED";
+    case MSG_OWNED_DONE: return "MSG_OWNED_DONE";
     default: return "INVALID MSG TYPE";
     }
 }

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <sstream>
 
 #include "../../include/oncillamem.h"
 #include "ocm/log.h"
@@ -84,6 +85,8 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
     if (const char *v = env("OCM_LEASE_AFTER")) cfg->lease_after = std::atoi(v);
     if (env("OCM_LEASE_HOST")) cfg->lease_host = true;
     if (const char *v = env("OCM_HOST_ALIAS")) cfg->host_alias = v;
+    if (const char *v = env("OCM_STATE_FILE")) cfg->state_file = v;
+    if (const char *v = env("OCM_STATE_INTERVAL_MS")) cfg->state_interval_ms = std::atoi(v);
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto val = [&](std::string *out) {
@@ -133,6 +136,8 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
             }
         } else if (a == "--host-alias") {
             if (!val(&cfg->host_alias)) return -1;
+        } else if (a == "--state-file") {
+            if (!val(&cfg->state_file)) return -1;
         } else if (a == "--lease-bytes") {
             if (!val(&v)) return -1;
             cfg->lease_bytes = parse_bytes(v);
@@ -269,7 +274,30 @@ int Daemon::init() {
         OCM_WARN("rank %d: network data server unavailable; cross-node placement disabled here", rank_);
         data_.reset();
     }
-    if (rank_ == 0) gov_ = std::make_unique<Governor>(n_, cfg_.policy, cfg_.stripe_unit);
+    {
+        std::ifstream ur("/dev/urandom", std::ios::binary);
+        ur.read(reinterpret_cast<char *>(&boot_id_), sizeof(boot_id_));
+        if (!boot_id_) boot_id_ = ((uint64_t)getpid() << 32) ^ (uint64_t)now_ms();
+    }
+    if (rank_ == 0) {
+        gov_ = std::make_unique<Governor>(n_, cfg_.policy, cfg_.stripe_unit);
+        std::ifstream sf(cfg_.state_file.empty() ? std::string() : cfg_.state_file);
+        if (sf) {
+            // Resume: reload the directory; survivors rejoin and confirm what they hold.
+            std::stringstream buf;
+            buf << sf.rdbuf();
+            std::string err;
+            int n = gov_->restore(buf.str(), &err);
+            if (n < 0) {
+                OCM_WARN("rank 0: ignoring directory checkpoint %s: %s", cfg_.state_file.c_str(), err.c_str());
+            } else {
+                resumed_ = true;
+                OCM_INFO("rank 0: resuming directory from %s (%d allocations, awaiting owner reports)",
+                         cfg_.state_file.c_str(), n);
+            }
+        }
+        saved_version_ = gov_->version();
+    }
     table_.assign(n_, NodeConfig{});
     joined_.assign(n_, false);
     peer_fd_.assign(n_, -1);
@@ -339,17 +367,100 @@ int Daemon::init() {
         conns_[fd] = std::move(c);
     }
     // Join: report our configuration to rank0 (reference notify_rank0, src/main.c:143-160).
+    join_rank0();
+    OCM_INFO("ocmd rank %d/%d up: gpu %d (%d visible), hbm capacity %.1f GiB, host tier %.1f GiB, policy %s, ns %s",
+             rank_, n_, gpu_, num_gpu_, (double)arena_->capacity(TIER_GPU) / (1 << 30),
+             (double)arena_->capacity(TIER_HOST) / (1 << 30), policy_name(cfg_.policy), ns_.c_str());
+    return 0;
+}
+
+void Daemon::join_rank0() {
     Msg add;
     std::memset(&add, 0, sizeof(add));
     add.type = MSG_ADD_NODE;
     add.status = MSG_REQUEST;
     add.rank = rank_;
+    add.seq = boot_id_;
     add.u.node = my_config();
     send_rank(0, add);
-    OCM_INFO("ocmd rank %d/%d up: gpu %d (%d visible), hbm capacity %.1f GiB, host tier %.1f GiB, policy %s, ns %s",
-             rank_, n_, gpu_, num_gpu_, (double)arena_->capacity(TIER_GPU) / (1 << 30),
-             (double)arena_->capacity(TIER_HOST) / (1 << 30), policy_name(cfg_.policy), ns_.c_str());
-    return 0;
+    // What we hold (empty on first boot): lets a restarted rank0 rebuild its directory.
+    for (auto &kv : owned_) {
+        const OwnedExtent &oe = kv.second;
+        Msg o;
+        std::memset(&o, 0, sizeof(o));
+        o.type = MSG_OWNED;
+        o.status = MSG_REQUEST;
+        o.rank = rank_;
+        o.pid = oe.app_pid;
+        Region &rg = o.u.region;
+        rg.alloc_id = kv.first.first;
+        rg.extent_idx = (uint16_t)kv.first.second;
+        rg.n_extents = oe.n_extents;
+        rg.bytes = oe.bytes;
+        rg.offset = oe.offset;
+        rg.slab_id = oe.slab_id;
+        rg.stripe_unit = oe.stripe_unit;
+        rg.owner_rank = rank_;
+        rg.orig_rank = oe.orig_rank;
+        rg.tier = (uint16_t)oe.tier;
+        rg.flags = oe.flags;
+        send_rank(0, o);
+    }
+    Msg done;
+    std::memset(&done, 0, sizeof(done));
+    done.type = MSG_OWNED_DONE;
+    done.status = MSG_REQUEST;
+    done.rank = rank_;
+    done.seq = owned_.size();
+    send_rank(0, done);
+}
+
+void Daemon::try_rejoin_rank0() {
+    const long now = now_ms();
+    if (now < next_rejoin_ms_) return;
+    next_rejoin_ms_ = now + 100;
+    const NodeEntry &ne = nf_.nodes[0];
+    int fd = tcp_connect(ne.ip, ne.ocm_port, 50);
+    if (fd < 0) return;
+    Msg hello;
+    std::memset(&hello, 0, sizeof(hello));
+    hello.type = MSG_HELLO;
+    hello.src_rank = rank_;
+    hello.rank = rank_;
+    send_all(fd, &hello, sizeof(hello));
+    set_nonblocking(fd, true);
+    auto c = std::make_unique<Conn>();
+    c->fd = fd;
+    c->peer_rank = 0;
+    peer_fd_[0] = fd;
+    ep_add(fd, EPOLLIN, tag(T_CONN, (uint64_t)fd));
+    conns_[fd] = std::move(c);
+    r0_lost_ = false;
+    OCM_INFO("rank %d: reconnected to rank 0; reporting %zu owned extents", rank_, owned_.size());
+    join_rank0();
+}
+
+void Daemon::save_checkpoint(bool force) {
+    if (!gov_ || cfg_.state_file.empty()) return;
+    const uint64_t v = gov_->version();
+    if (v == saved_version_) return;
+    const long now = now_ms();
+    if (!force && now - last_save_ms_ < cfg_.state_interval_ms) return;
+    const std::string tmp = cfg_.state_file + ".tmp";
+    {
+        std::ofstream f(tmp, std::ios::trunc);
+        f << gov_->checkpoint();
+        if (!f) {
+            OCM_WARN("rank 0: cannot write directory checkpoint %s", tmp.c_str());
+            return;
+        }
+    }
+    if (rename(tmp.c_str(), cfg_.state_file.c_str()) != 0) {
+        OCM_WARN("rank 0: cannot publish directory checkpoint %s: %s", cfg_.state_file.c_str(), strerror(errno));
+        return;
+    }
+    saved_version_ = v;
+    last_save_ms_ = now;
 }
 
 void Daemon::check_ready() {
@@ -358,8 +469,8 @@ void Daemon::check_ready() {
         if (!joined_[r]) return;
     ready_ = true;
     OCM_LOG("rank %d: mesh complete (%d nodes)", rank_, n_);
-    if (rank_ == 0 && cfg_.ctrl != "tcp") {
-        // Bootstrap the tick transport: rank0 picks the RCCL id and tells everybody over TCP.
+    if (rank_ == 0 && cfg_.ctrl != "tcp" && !resumed_) {
+        // Bootstrap the tick transport (not after a resume: survivors stay on TCP): rank0 picks the RCCL id and tells everybody over TCP.
         Msg t;
         std::memset(&t, 0, sizeof(t));
         t.type = MSG_TICK_START;
@@ -385,6 +496,7 @@ void Daemon::check_ready() {
 
 void Daemon::shutdown() {
     if (ep_ < 0) return;
+    save_checkpoint(true);
     if (tick_) {
         tick_->stop();
         tick_.reset();
@@ -434,7 +546,12 @@ int Daemon::loop() {
             handle_mesh_msg(m, -1);
         }
         if (stop_) break;
-        int n = epoll_wait(ep_, evs, 64, self_q_.empty() ? 1000 : 0);
+        save_checkpoint(false);
+        if (r0_lost_) try_rejoin_rank0();
+        int timeout = 1000;
+        if (r0_lost_) timeout = 100;
+        if (gov_ && !cfg_.state_file.empty() && gov_->version() != saved_version_) timeout = cfg_.state_interval_ms;
+        int n = epoll_wait(ep_, evs, 64, self_q_.empty() ? timeout : 0);
         sweep_timeouts();
         if (n < 0) {
             if (errno == EINTR) continue;
@@ -870,7 +987,18 @@ void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
         break;
     }
     case MSG_ADD_NODE:
-        if (rank_ == 0) r0_add_node(m.u.node);
+        if (rank_ == 0) r0_add_node(m.u.node, m.seq);
+        break;
+    case MSG_OWNED:
+        if (rank_ == 0 && gov_) gov_->confirm_extent(m.src_rank, m.u.region, m.pid);
+        break;
+    case MSG_OWNED_DONE:
+        if (rank_ == 0 && gov_) {
+            int dropped = gov_->end_reconcile(m.src_rank);
+            if (m.seq || dropped)
+                OCM_INFO("rank 0: rank %d confirmed %llu extents (%d stale entries dropped)", m.src_rank,
+                         (unsigned long long)m.seq, dropped);
+        }
         break;
     case MSG_NODE_TABLE: {
         const NodeConfig &c = m.u.node;
@@ -938,9 +1066,9 @@ void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
     }
 }
 
-void Daemon::r0_add_node(const NodeConfig &cfg) {
+void Daemon::r0_add_node(const NodeConfig &cfg, uint64_t boot_id) {
     if (cfg.rank < 0 || cfg.rank >= n_) return;
-    gov_->add_node(cfg);
+    gov_->add_node(cfg, boot_id);
     table_[cfg.rank] = cfg;
     joined_[cfg.rank] = true;
     // Fan the directory out: the newcomer gets the whole table, everybody else the newcomer.
@@ -1110,6 +1238,10 @@ void Daemon::owner_do_alloc(Msg &m) {
     oe.tier = rg.tier;
     oe.orig_rank = rg.orig_rank;
     oe.bytes = rg.bytes;
+    oe.app_pid = m.pid;
+    oe.flags = rg.flags;
+    oe.n_extents = rg.n_extents ? rg.n_extents : 1;
+    oe.stripe_unit = rg.stripe_unit;
     owned_[{rg.alloc_id, (int)rg.extent_idx}] = oe;
     if (rg.flags & REGION_SPILLED) n_spilled_++;
     Msg r = m;
@@ -1405,6 +1537,11 @@ void Daemon::fail_pending_on(int rank) {
 
 void Daemon::peer_lost(int rank) {
     OCM_WARN("rank %d: lost link to rank %d", rank_, rank);
+    if (rank == 0 && rank_ != 0) {
+        // Keep serving (data plane, leases, frees to owners) and wait for a restarted rank0.
+        r0_lost_ = true;
+        next_rejoin_ms_ = now_ms() + 50;
+    }
     for (auto &l : leases_)
         if (l && l->owner == rank) l.reset();  // its memory died with it
     lease_inflight_.erase(rank);

@@ -227,6 +227,47 @@ static void t_governor_hosts() {
     CHECK(p.err == 0 && p.extents[0].owner == 0 && p.extents[0].net && p.extents[0].tier == TIER_GPU);
 }
 
+static void t_governor_checkpoint() {
+    const uint64_t G = 1ull << 30;
+    Governor gov(3, Policy::Ring, 1 << 20);
+    for (int r = 0; r < 3; r++) gov.add_node(cfg(r, 4 * G, G), 100 + r);
+    PlaceRequest pr;
+    pr.orig_rank = 1;
+    pr.bytes = G;
+    Placement a = gov.place(pr), b = gov.place(pr);
+    CHECK(a.err == 0 && b.err == 0 && a.extents[0].owner == 2 && b.extents[0].owner == 2);
+    const std::string snap = gov.checkpoint();
+    std::string err;
+    // a truncated file is refused, not half-loaded
+    Governor bad(3, Policy::Ring, 1 << 20);
+    CHECK(bad.restore(snap.substr(0, snap.size() - 4), &err) < 0);
+    CHECK(bad.restore("garbage", &err) < 0);
+    // resume: rank 2 rejoins with the same boot id and confirms only `a`
+    Governor g2(3, Policy::Ring, 1 << 20);
+    CHECK(g2.restore(snap, &err) == 2);
+    g2.add_node(cfg(0, 4 * G, G), 999);  // rank0 restarted
+    g2.add_node(cfg(1, 4 * G, G), 101);
+    g2.add_node(cfg(2, 4 * G, G), 102);
+    CHECK(g2.node(2).gpu_reserved == 0);  // nothing held until confirmed
+    Region r{};
+    r.alloc_id = a.alloc_id;
+    r.bytes = G;
+    r.orig_rank = 1;
+    r.tier = TIER_GPU;
+    r.n_extents = 1;
+    g2.confirm_extent(2, r, 77);
+    CHECK(g2.node(2).gpu_reserved == G);
+    CHECK(g2.end_reconcile(2) == 1);  // b was freed while rank0 was away
+    CHECK(g2.find(a.alloc_id) && !g2.find(b.alloc_id));
+    // new ids continue after the restored ones
+    Placement c = g2.place(pr);
+    CHECK(c.err == 0 && c.alloc_id > b.alloc_id && g2.node(2).gpu_reserved == 2 * G);
+    CHECK(g2.release(a.alloc_id) && g2.node(2).gpu_reserved == G);
+    // an owner that comes back as a new process lost its memory
+    g2.add_node(cfg(2, 4 * G, G), 555);
+    CHECK(!g2.find(c.alloc_id) && g2.node(2).gpu_reserved == 0);
+}
+
 static void t_stripe_geometry() {
     for (uint64_t total : {1ull, 4095ull, 4096ull, 1000000ull, (3ull << 20) + 7}) {
         for (int n = 1; n <= 8; n++) {
@@ -271,6 +312,7 @@ int main() {
         std::function<void()> fn;
     } tests[] = {{"layout", t_layout},           {"nodefile", t_nodefile}, {"range_alloc", t_range_alloc},
                  {"governor", t_governor},       {"governor_hosts", t_governor_hosts},
+                 {"governor_checkpoint", t_governor_checkpoint},
                  {"stripe_geometry", t_stripe_geometry},
                  {"arena_host", t_arena_host}};
     for (auto &t : tests) {

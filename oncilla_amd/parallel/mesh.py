@@ -91,29 +91,31 @@ class Mesh:
         env.update({"OCM_NS": self.ns, "OCM_DAEMON_RANK": str(rank)})
         return env
 
-    def start(self, timeout: float = 60.0) -> "Mesh":
-        write_nodefile(self.nodefile, self.ports, self.gpus)
-        for r in self.ranks:
-            ready = os.path.join(self.workdir, f"ready.{r}.json")
-            log = os.path.join(self.workdir, f"ocmd.{r}.log")
-            args = [self.ocmd, self.nodefile, "--rank", str(r), "--ns", self.ns, "--policy", self.policy,
-                    "--ready-file", ready, "--bind", "127.0.0.1"]
-            if self.gpus[r] is None:
-                args += ["--gpu", "none"]
-            else:
-                args += ["--gpu", str(self.gpus[r])]
-            if self.watch:
-                args += ["--watch-pid", str(os.getpid())]
-            args += self.extra_args
-            env = dict(os.environ)
-            env.update(self.env)
-            env.update(self.rank_env.get(r, {}))
-            env["OCM_NS"] = self.ns
-            with open(log, "w") as lf:
-                proc = subprocess.Popen(args, stdout=lf, stderr=subprocess.STDOUT, env=env, start_new_session=True)
-            self.daemons.append(Daemon(r, proc, ready, log))
+    def _spawn(self, r: int) -> Daemon:
+        ready = os.path.join(self.workdir, f"ready.{r}.json")
+        log = os.path.join(self.workdir, f"ocmd.{r}.log")
+        if os.path.exists(ready):
+            os.unlink(ready)
+        args = [self.ocmd, self.nodefile, "--rank", str(r), "--ns", self.ns, "--policy", self.policy,
+                "--ready-file", ready, "--bind", "127.0.0.1"]
+        if self.gpus[r] is None:
+            args += ["--gpu", "none"]
+        else:
+            args += ["--gpu", str(self.gpus[r])]
+        if self.watch:
+            args += ["--watch-pid", str(os.getpid())]
+        args += self.extra_args
+        env = dict(os.environ)
+        env.update(self.env)
+        env.update(self.rank_env.get(r, {}))
+        env["OCM_NS"] = self.ns
+        with open(log, "a") as lf:
+            proc = subprocess.Popen(args, stdout=lf, stderr=subprocess.STDOUT, env=env, start_new_session=True)
+        return Daemon(r, proc, ready, log)
+
+    def _wait_ready(self, daemons, timeout: float) -> None:
         deadline = time.time() + timeout
-        for d in self.daemons:
+        for d in daemons:
             while not os.path.exists(d.ready_file):
                 if not d.alive():
                     raise RuntimeError(f"ocmd rank {d.rank} exited ({d.proc.returncode}):\n{d.log()}")
@@ -121,7 +123,26 @@ class Mesh:
                     self.stop()
                     raise TimeoutError(f"ocmd rank {d.rank} not ready after {timeout}s:\n{d.log()}")
                 time.sleep(0.02)
+
+    def start(self, timeout: float = 60.0) -> "Mesh":
+        write_nodefile(self.nodefile, self.ports, self.gpus)
+        for r in self.ranks:
+            log = os.path.join(self.workdir, f"ocmd.{r}.log")
+            open(log, "w").close()
+            self.daemons.append(self._spawn(r))
+        self._wait_ready(self.daemons, timeout)
         return self
+
+    def restart(self, rank: int, timeout: float = 60.0) -> None:
+        """Start a dead rank again with the same arguments (e.g. rank0 resuming its directory)."""
+        for i, d in enumerate(self.daemons):
+            if d.rank == rank:
+                if d.alive():
+                    raise RuntimeError(f"ocmd rank {rank} is still running")
+                self.daemons[i] = self._spawn(rank)
+                self._wait_ready([self.daemons[i]], timeout)
+                return
+        raise KeyError(rank)
 
     def ready_info(self) -> list[dict]:
         out = []
