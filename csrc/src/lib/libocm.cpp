@@ -71,6 +71,8 @@ struct lib_alloc {
     bool any_net = false;     // some extent lives on another node
     bool async_pending = false;
     bool pooled = false;      // local half from the stream-ordered pool
+    int lane = -1;            // async ops: index into State::lanes (per-allocation ordering)
+    hipEvent_t ev = nullptr;  // completion of the last async op (ocm_wait)
 };
 
 namespace {
@@ -125,6 +127,10 @@ struct State {
     // Local GPU halves: stream-ordered pool (no device-wide sync in free, freed
     // blocks reused without a new VA mapping). Reference K8: cudaMalloc/cudaFree.
     hipMemPool_t pool = nullptr;
+    // Async one-sided ops run on lane streams, one lane per allocation (round
+    // robin), so ops on different allocations (different peers / links) overlap.
+    std::vector<hipStream_t> lanes;
+    int n_lanes = 4, next_lane = 0;
     bool pool_tried = false;
     uint64_t pool_keep = 8ull << 30;       // bytes kept reserved across frees
     hipEvent_t done = nullptr;
@@ -327,6 +333,57 @@ int log2_exact(uint64_t v) {
     return __builtin_ctzll(v);
 }
 
+int wait_event(hipEvent_t ev) {
+    State &s = S();
+    hipError_t e = hipSuccess;
+    if (s.sync_mode == 1) {
+        while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
+        }
+    } else {
+        e = hipEventSynchronize(ev);
+    }
+    if (e != hipSuccess) OCM_FAIL(-1, "event wait: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// Completion of `a`'s queued async ops (its lane up to the recorded event).
+int wait_alloc(lib_alloc *a) {
+    State &s = S();
+    if (!a || !a->async_pending) return 0;
+    a->async_pending = false;
+    if (!a->ev) return 0;
+    DeviceGuard g(s.device);
+    return wait_event(a->ev);
+}
+
+hipStream_t lane_stream(lib_alloc *a) {
+    State &s = S();
+    if (a->lane < 0) {
+        if (s.lanes.empty()) {
+            DeviceGuard g(s.device);
+            for (int i = 0; i < std::max(1, s.n_lanes); i++) {
+                hipStream_t st = nullptr;
+                if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+                    (void)hipGetLastError();
+                    break;
+                }
+                s.lanes.push_back(st);
+            }
+        }
+        if (s.lanes.empty()) return s.stream;
+        a->lane = s.next_lane++ % (int)s.lanes.size();
+    }
+    if (!a->ev) {
+        DeviceGuard g(s.device);
+        if (hipEventCreateWithFlags(&a->ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            a->ev = nullptr;
+            return s.stream;
+        }
+    }
+    return s.lanes[a->lane];
+}
+
 int sync_stream() {
     State &s = S();
     if (!s.stream) return 0;
@@ -517,8 +574,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         // Another node: stream every piece through its owner's data server (blocking).
         std::vector<Seg> segs;
         segments(a, rem_off, len, segs);
-        if (a->async_pending && sync_stream() != 0) return -1;
-        a->async_pending = false;
+        if (wait_alloc(a) != 0) return -1;
         for (auto &g : segs) {
             const Extent &e = a->ext[g.ext];
             if (e.net) {
@@ -569,12 +625,15 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         x.len = len;
         x.put = put ? 1 : 0;
         if (x.n_ext > 1) x.unit_shift = (uint32_t)log2_exact(a->stripe_unit);
-        if (a->async_pending && sync_stream() != 0) return -1;  // keep program order with queued async ops
-        a->async_pending = false;
+        if (wait_alloc(a) != 0) return -1;  // keep program order with queued async ops
         if (service_xfer(x) == 0) return 0;
         OCM_WARN("copy service failed (%s); falling back to launches", last_error());
         s.svc_max = 0;
     }
+    // Async ops queue on the allocation's lane; blocking ops on the library stream
+    // after the allocation's queued async work.
+    if (!async && wait_alloc(a) != 0) return -1;
+    hipStream_t st = async ? lane_stream(a) : s.stream;
     if (use_kernel) {
         XferArgs x;
         std::memset(&x, 0, sizeof(x));
@@ -598,7 +657,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
             for (auto &e : a->ext) same_gpu &= e.r.tier == TIER_GPU && e.r.owner_gpu == s.device;
             t.variant = (same_gpu && len <= (256ull << 20)) ? XFER_LDS : XFER_REG;
         }
-        err = xfer_launch(x, t, s.stream);
+        err = xfer_launch(x, t, st);
     } else {
         service_park();
         segments(a, rem_off, len, segs);
@@ -614,14 +673,20 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
                     std::memcpy(lin + g.lin_off, r, g.len);
                 continue;
             }
-            err = put ? hipMemcpyAsync(r, lin + g.lin_off, g.len, hipMemcpyDefault, s.stream)
-                      : hipMemcpyAsync(lin + g.lin_off, r, g.len, hipMemcpyDefault, s.stream);
+            err = put ? hipMemcpyAsync(r, lin + g.lin_off, g.len, hipMemcpyDefault, st)
+                      : hipMemcpyAsync(lin + g.lin_off, r, g.len, hipMemcpyDefault, st);
             if (err != hipSuccess) break;
         }
     }
     if (err != hipSuccess) OCM_FAIL(-1, "transfer launch failed: %s", hipGetErrorString(err));
     if (async) {
-        a->async_pending = true;
+        if (st != s.stream && a->ev) {
+            err = hipEventRecord(a->ev, st);
+            if (err != hipSuccess) OCM_FAIL(-1, "event record failed: %s", hipGetErrorString(err));
+        } else if (a->ev == nullptr && sync_stream() != 0) {
+            return -1;  // no lane available: complete it now
+        }
+        a->async_pending = a->ev != nullptr;
         return 0;
     }
     return sync_stream();
@@ -824,6 +889,7 @@ int ocm_init(void) {
         }
     }
     s.sync_mode = env_int("OCM_SYNC_MODE", 1);
+    s.n_lanes = env_int("OCM_ASYNC_LANES", 4);
     if (const char *sm = std::getenv("OCM_SERVICE_MAX")) s.svc_max = std::strtoull(sm, nullptr, 0);
     s.tuning = xfer_tuning_from_env();
     const char *he = std::getenv("OCM_HOST_ENGINE");
@@ -860,6 +926,13 @@ int ocm_tini(void) {
         (void)hipHostFree(s.net_stage);
         s.net_stage = nullptr;
     }
+    for (auto st : s.lanes) {
+        DeviceGuard g(s.device);
+        (void)hipStreamSynchronize(st);
+        (void)hipStreamDestroy(st);
+    }
+    s.lanes.clear();
+    s.next_lane = 0;
     if (s.stream) {
         DeviceGuard g(s.device);
         (void)hipStreamSynchronize(s.stream);
@@ -1025,7 +1098,12 @@ static int free_impl(ocm_alloc_t a) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (!a || !s.allocs.count(a)) OCM_FAIL(-1, "ocm_free: unknown allocation");
-    if (a->async_pending) ocm_wait(a);
+    wait_alloc(a);
+    if (a->ev) {
+        DeviceGuard g(s.device);
+        (void)hipEventDestroy(a->ev);
+        a->ev = nullptr;
+    }
     // Unmap dedicated remote slabs before the owner frees them.
     for (auto &e : a->ext) release_extent(e, false);
     free_local_half(a);
@@ -1099,8 +1177,13 @@ int ocm_copy_onesided_async(ocm_alloc_t a, ocm_param_t p) { return ocm_copy_ones
 int ocm_wait(ocm_alloc_t a) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
-    if (a) a->async_pending = false;
-    return sync_stream();
+    if (a) {
+        if (!s.allocs.count(a)) OCM_FAIL(-1, "ocm_wait: unknown allocation");
+        return wait_alloc(a);
+    }
+    int rc = 0;  // NULL: every allocation
+    for (auto *x : s.allocs) rc |= wait_alloc(x);
+    return rc | sync_stream();
 }
 
 static bool range_ok(uint64_t off, uint64_t n, uint64_t cap) { return off <= cap && n <= cap - off; }
@@ -1124,6 +1207,7 @@ static int copy_impl(ocm_alloc_t dst, ocm_alloc_t src, ocm_param_t p) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (!dst || !src || !p) OCM_FAIL(-1, "ocm_copy: NULL argument");
+    if (wait_alloc(dst) != 0 || wait_alloc(src) != 0) return -1;  // their queued async ops come first
     // A read (op_flag == 0) is the write with the roles swapped (reference src/lib.c:511-515).
     struct ocm_params q = *p;
     if (!q.op_flag) {
@@ -1191,6 +1275,7 @@ int ocm_copy_in(ocm_alloc_t dst, void *src) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (!dst || !src) OCM_FAIL(-1, "ocm_copy_in: NULL argument");
+    if (wait_alloc(dst) != 0) return -1;
     const Loc sl = pointer_loc(src);
     if (dst->remote) return xfer(dst, true, static_cast<char *>(src), sl, 0, dst->remote_bytes, false);
     return copy_local(dst->local, dst->loc, src, sl, dst->local_bytes);
@@ -1200,6 +1285,7 @@ int ocm_copy_out(void *dst, ocm_alloc_t src) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (!dst || !src) OCM_FAIL(-1, "ocm_copy_out: NULL argument");
+    if (wait_alloc(src) != 0) return -1;
     const Loc dl = pointer_loc(dst);
     if (src->remote) return xfer(src, false, static_cast<char *>(dst), dl, 0, src->remote_bytes, false);
     return copy_local(dst, dl, src->local, src->loc, src->local_bytes);

@@ -194,3 +194,37 @@ def test_network_tier_hbm_owner(mesh_factory):
         assert torch.equal(a.local_tensor(torch.int32)[: (n - 4096) // 4], t[: (n - 4096) // 4])
         assert c.stats(1)["gpu_used"] >= n
         a.free()
+
+
+def test_async_lanes_per_allocation(mesh_factory):
+    # async ops queue per allocation (lane streams): ops on different allocations
+    # overlap, ocm_wait(a) waits for a only, blocking ops keep program order.
+    m = mesh_factory(3, gpus=[0, 0, 0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 32 << 20
+        allocs = [c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n) for _ in range(6)]
+        for i, a in enumerate(allocs):
+            a.fill(seed=30 + i)
+        for a in allocs:
+            a.put(0, 0, n, async_=True)
+        for a in reversed(allocs):
+            a.wait()
+        for a in allocs:
+            a.fill(seed=0)
+        for a in allocs:
+            a.get(0, 0, n, async_=True)
+        for i, a in enumerate(allocs):
+            a.wait()
+            assert a.check(seed=30 + i) == 0, i
+        # async put, then a blocking get of the other half: the get waits for the put
+        a = allocs[0]
+        a.fill(seed=77)
+        a.put(0, 0, n, async_=True)
+        a.get(0, n // 2, n // 2)
+        assert a.check(seed=77, offset=0, nbytes=n // 2, first_word=n // 8) == 0
+        # NULL wait: everything
+        for a in allocs:
+            a.put(0, 0, n, async_=True)
+        assert c.lib.ocm_wait(None) == 0
+        for a in allocs:
+            a.free()
