@@ -4,6 +4,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config"}
@@ -25,11 +27,14 @@ def test_bench_single(native):
     assert res["alloc_p50_us"] > 0 and res["config"]["remote_tier"] == "host"
 
 
-def test_bench_two_ranks(native):
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(REPO, "bench.py"),
-                        "--gpus", "2", "--device", "cpu", "--steps", "2", "--warmup", "1", "--max-bytes",
-                        str(1 << 20), "--alloc-samples", "20"], capture_output=True, text=True, timeout=300, cwd="/tmp")
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_multi_rank(native, n):
+    # the driver's multi-GPU launch shape (torch.distributed.run, one daemon per rank), on gloo + CPU daemons
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+                        "--master-addr", "127.0.0.1", "--master-port", str(29533 + n), os.path.join(REPO, "bench.py"),
+                        "--gpus", str(n), "--device", "cpu", "--steps", "2", "--warmup", "1", "--max-bytes",
+                        str(4 << 20), "--alloc-samples", "20"], capture_output=True, text=True, timeout=300, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
     res = _last_json(r.stdout)
-    assert res["n_gpus"] == 2 and res["value"] > 0 and res["config"]["parallelism"] == "stripe2"
+    assert res["n_gpus"] == n and res["value"] > 0 and res["config"]["parallelism"] == f"stripe{n}"
+    assert res["config"]["extents_per_pair"] == n - 1  # 8 MiB+1 pair = 9 stripe units: every peer gets one
