@@ -52,6 +52,7 @@ struct DaemonConfig {
     int watch_pid = 0;               // exit when this process (the launcher) exits
     uint64_t lease_bytes = 1ull << 30;  // HBM leased per owner for local sub-allocation (0 = off)
     int lease_after = 2;             // normal placements on an owner before leasing there
+    int lease_idle_ms = 2000;        // give an empty lease back after this long (capacity is not stranded)
     bool lease_host = false;         // also lease host-tier capacity (tests; OCM_LEASE_HOST=1)
     std::string host_alias;          // report this host name (tests: pretend daemons are on other nodes)
     std::string state_file;          // rank0: directory checkpoint (resume after a rank0 restart)
@@ -106,6 +107,7 @@ private:
         uint32_t tier = TIER_GPU;
         Region base;               // the chunk as the owner exported it
         RangeAllocator ra;
+        long idle_since_ms = 0;    // last time it became empty
     };
     struct OriginAlloc {
         pid_t pid = 0;
@@ -174,6 +176,7 @@ private:
     void sweep_timeouts();
     bool try_lease_alloc(Msg &m);
     void request_lease(int owner, uint32_t tier);
+    void return_idle_leases();
     int preferred_owner() const;
     bool cross_host(int a, int b) const;
     void start_tick(const uint8_t *id);

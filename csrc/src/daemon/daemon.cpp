@@ -84,6 +84,7 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
     if (const char *v = env("OCM_LEASE_BYTES")) cfg->lease_bytes = parse_bytes(v);
     if (const char *v = env("OCM_LEASE_AFTER")) cfg->lease_after = std::atoi(v);
     if (env("OCM_LEASE_HOST")) cfg->lease_host = true;
+    if (const char *v = env("OCM_LEASE_IDLE_MS")) cfg->lease_idle_ms = std::atoi(v);
     if (const char *v = env("OCM_HOST_ALIAS")) cfg->host_alias = v;
     if (const char *v = env("OCM_STATE_FILE")) cfg->state_file = v;
     if (const char *v = env("OCM_STATE_INTERVAL_MS")) cfg->state_interval_ms = std::atoi(v);
@@ -553,6 +554,7 @@ int Daemon::loop() {
         if (gov_ && !cfg_.state_file.empty() && gov_->version() != saved_version_) timeout = cfg_.state_interval_ms;
         int n = epoll_wait(ep_, evs, 64, self_q_.empty() ? timeout : 0);
         sweep_timeouts();
+        return_idle_leases();
         if (n < 0) {
             if (errno == EINTR) continue;
             OCM_ERR("epoll_wait: %s", strerror(errno));
@@ -1316,6 +1318,7 @@ void Daemon::finish_alloc(Pending &p) {
             l->tier = p.lease_tier;
             l->base = p.extents[0];
             l->ra.reset(l->base.bytes);
+            l->idle_since_ms = now_ms();
             OCM_LOG("rank %d: leased %llu bytes of rank %d HBM", rank_, (unsigned long long)l->base.bytes, owner);
             leases_.push_back(std::move(l));
         } else if (p.err) {
@@ -1432,6 +1435,7 @@ void Daemon::start_free(uint64_t alloc_id, pid_t reply_pid, uint64_t reply_seq) 
     if (oa.lease >= 0 && oa.lease < (int)leases_.size() && leases_[oa.lease]) {
         Lease &l = *leases_[oa.lease];
         l.ra.free(oa.extents[0].offset - l.base.offset);
+        if (l.ra.used() == 0) l.idle_since_ms = now_ms();
         n_free_++;
         if (reply_pid && apps_.count(reply_pid)) {
             Msg r;
@@ -1653,6 +1657,32 @@ int Daemon::preferred_owner() const {
         return k;
     }
     return -1;
+}
+
+void Daemon::return_idle_leases() {
+    if (leases_.empty() || cfg_.lease_idle_ms < 0) return;
+    const long now = now_ms();
+    for (auto &lp : leases_) {
+        if (!lp || lp->ra.used() != 0 || now - lp->idle_since_ms < cfg_.lease_idle_ms) continue;
+        // Nothing carved from it for a while: the owner gets the chunk back.
+        Msg f;
+        std::memset(&f, 0, sizeof(f));
+        f.type = MSG_DO_FREE;
+        f.status = MSG_REQUEST;
+        f.rank = rank_;
+        f.seq = 0;  // no answer needed
+        f.u.region = lp->base;
+        send_rank(lp->owner, f);
+        Msg fr;
+        std::memset(&fr, 0, sizeof(fr));
+        fr.type = MSG_FREED;
+        fr.u.region.alloc_id = lp->base.alloc_id;
+        send_rank(0, fr);
+        OCM_LOG("rank %d: returned idle lease of %llu bytes on rank %d", rank_, (unsigned long long)lp->base.bytes,
+                lp->owner);
+        lease_demand_[lp->owner] = 0;
+        lp.reset();  // slot stays: OriginAlloc::lease indices remain valid
+    }
 }
 
 void Daemon::request_lease(int owner, uint32_t tier) {

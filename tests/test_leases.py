@@ -86,3 +86,30 @@ def test_crash_reclaims_leased_ranges(mesh_factory):
         assert c.stats(1)["host_used"] == 64 << 20
         a.free()
         b.free()
+
+
+def test_idle_lease_goes_back_to_owner(mesh_factory):
+    m = mesh_factory(2, env=dict(LEASE_ENV, OCM_LEASE_IDLE_MS="200"))
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        allocs = [c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20) for _ in range(2)]
+        assert _wait_for(lambda: c.stats(0)["n_leases"] == 1)
+        leased = [c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20) for _ in range(3)]
+        assert c.stats(0)["lease_allocs"] == 3
+        for a in allocs + leased:
+            a.free()
+        # empty for > 200 ms: returned; the owner holds nothing any more
+        assert _wait_for(lambda: c.stats(0)["n_leases"] == 0 and c.stats(1)["host_used"] == 0, timeout=5)
+        # demand builds a new lease later
+        more = [c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20) for _ in range(2)]
+        assert _wait_for(lambda: c.stats(0)["n_leases"] == 1)
+        for a in more:
+            a.free()
+
+
+def _wait_for(pred, timeout=5.0):
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        if pred():
+            return True
+        time.sleep(0.01)
+    return False
