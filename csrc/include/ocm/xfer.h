@@ -54,6 +54,50 @@ hipError_t xfer_copy(void *dst, const void *src, uint64_t bytes, const XferTunin
 // Default tuning from the environment (OCM_XFER_VARIANT, OCM_XFER_BLOCKS, OCM_XFER_NT).
 XferTuning xfer_tuning_from_env();
 
+// ---- batched one-sided ops (scatter/gather lists) ----
+// Many ops on one remote pair in ONE launch. The batch is cut into 4 KiB
+// wave-tiles (smaller when the stripe unit is): the host prefix-sums each op's
+// tile count into `first_tile`, sizes the grid, and gives every wave a
+// contiguous tile range plus the op its first tile belongs to (`wave_op`), so
+// waves never search; they walk forward through the ops they cover. Small
+// batches travel in the kernel arguments, large ones in a device buffer.
+struct XferBatchOp {
+    uint64_t lin_off;     // offset in the linear buffer
+    uint64_t rem_off;     // offset in striped coordinates
+    uint64_t len;
+    uint64_t first_tile;  // exclusive prefix sum of the ops' tile counts
+    uint32_t put;         // 1: lin -> striped, 0: striped -> lin
+    uint32_t pad;
+};
+static_assert(sizeof(XferBatchOp) == 40, "batch op layout");
+
+constexpr int kXferInlineOps = 48;  // ops carried in the kernarg segment
+
+struct XferBatchArgs {
+    char *lin;
+    char *ext[kXferMaxExtents];
+    uint32_t unit_shift;
+    uint32_t n_ext;
+    uint32_t tile_shift;
+    uint32_t n_ops;
+    uint64_t total_tiles;
+    uint32_t grid;                        // workgroups (4 waves each)
+    uint32_t pad;
+    const XferBatchOp *ops;               // device copy when n_ops > kXferInlineOps
+    const uint32_t *wave_op;              // device: first op of each wave (n_ops > kXferInlineOps)
+    XferBatchOp inline_ops[kXferInlineOps];
+};
+
+// Host-side plan. Fills first_tile, returns total tiles.
+uint64_t xfer_batch_plan(XferBatchOp *ops, uint32_t n, uint32_t tile_shift);
+// Workgroups for `total_tiles` (4 waves each, capped for residency).
+uint32_t xfer_batch_grid(uint64_t total_tiles);
+// wave_op[w] for every wave of `grid` workgroups (4 * grid entries).
+void xfer_batch_wave_ops(const XferBatchOp *ops, uint32_t n, uint64_t total_tiles, uint32_t grid, uint32_t *out);
+// tile shift for a remote layout: 4 KiB wave-tiles, or the stripe unit when smaller.
+uint32_t xfer_batch_tile_shift(uint32_t n_ext, uint32_t unit_shift);
+hipError_t xfer_batch_launch(const XferBatchArgs &a, const XferTuning &t, hipStream_t stream);
+
 // ---- persistent copy service (low-latency small one-sided ops) ----
 // One resident workgroup polls a doorbell in host-pinned coherent memory. The
 // host writes the transfer arguments, then bumps `seq` (release); the kernel

@@ -136,6 +136,13 @@ ocm_alloc_t ocm_alloc_ex(ocm_alloc_param_t alloc_param, const struct ocm_alloc_e
 /* Non-blocking variants: enqueue on the allocation's stream; ocm_wait() completes them. */
 int ocm_copy_onesided_async(ocm_alloc_t a, ocm_param_t options);
 int ocm_wait(ocm_alloc_t a);
+/* Batched one-sided copies on one remote pair: n_ops records with the
+ * ocm_copy_onesided meaning (op_flag 1 = put local[src_offset] -> remote[dest_offset],
+ * 0 = get), puts and gets mixed, run as ONE gfx950 kernel launch (scatter/gather
+ * lists). Ops of one batch run concurrently: overlapping destinations have no
+ * defined order. flags: OCM_BATCH_ASYNC completes later (ocm_wait). */
+#define OCM_BATCH_ASYNC 1
+int ocm_copy_onesided_batch(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, int flags);
 int ocm_remote_info(ocm_alloc_t a, struct ocm_remote_info *info);
 /* Device pointer of the remote half when it is a single extent (NULL if striped). */
 void *ocm_remotebuf(ocm_alloc_t a);

@@ -79,29 +79,40 @@ struct TileSpan {
     uint64_t n;
 };
 
-__device__ __forceinline__ TileSpan tile_span(const XferArgs &a, uint64_t ti, uint64_t first_tile) {
-    const uint64_t tile = 1ull << a.tile_shift;
-    const uint64_t r0 = a.rem_off, r1 = a.rem_off + a.len;
-    const uint64_t lo = first_tile + (ti << a.tile_shift);
+// Span of tile `ti` of a transfer of [rem_off, rem_off + len) in striped
+// coordinates. `E` holds the extent bases (`E::ext[]`); it is read in place
+// (kernarg segment or LDS): copying it to a local array would put the
+// dynamically indexed array in scratch.
+template <class E>
+__device__ __forceinline__ TileSpan tile_span_of(const E &x, uint32_t n_ext, uint32_t unit_shift, uint32_t tile_shift,
+                                                 char *lin, uint64_t rem_off, uint64_t len, uint32_t put, uint64_t ti,
+                                                 uint64_t first_tile) {
+    const uint64_t tile = 1ull << tile_shift;
+    const uint64_t r0 = rem_off, r1 = rem_off + len;
+    const uint64_t lo = first_tile + (ti << tile_shift);
     const uint64_t ts = lo > r0 ? lo : r0;
     const uint64_t te = (lo + tile) < r1 ? (lo + tile) : r1;
     char *rp;
-    if (a.n_ext == 1) {
-        rp = a.ext[0] + ts;
+    if (n_ext == 1) {
+        rp = x.ext[0] + ts;
     } else {
         // Stripe unit u of the address space lives on extent u % n at (u / n) * unit.
-        const uint64_t unit_mask = (1ull << a.unit_shift) - 1;
-        const uint32_t u = (uint32_t)(ts >> a.unit_shift);
-        const uint32_t e = u % a.n_ext;
-        const uint64_t eoff = ((uint64_t)(u / a.n_ext) << a.unit_shift) | (ts & unit_mask);
-        rp = a.ext[e] + eoff;
+        const uint64_t unit_mask = (1ull << unit_shift) - 1;
+        const uint32_t u = (uint32_t)(ts >> unit_shift);
+        const uint32_t e = u % n_ext;
+        const uint64_t eoff = ((uint64_t)(u / n_ext) << unit_shift) | (ts & unit_mask);
+        rp = x.ext[e] + eoff;
     }
-    char *lp = a.lin + (ts - r0);
+    char *lp = lin + (ts - r0);
     TileSpan s;
-    s.dst = a.put ? rp : lp;
-    s.src = a.put ? lp : rp;
+    s.dst = put ? rp : lp;
+    s.src = put ? lp : rp;
     s.n = te - ts;
     return s;
+}
+
+__device__ __forceinline__ TileSpan tile_span(const XferArgs &a, uint64_t ti, uint64_t first_tile) {
+    return tile_span_of(a, a.n_ext, a.unit_shift, a.tile_shift, a.lin, a.rem_off, a.len, a.put, ti, first_tile);
 }
 
 template <bool NT>
@@ -263,6 +274,111 @@ hipError_t xfer_copy(void *dst, const void *src, uint64_t bytes, const XferTunin
     return xfer_launch(a, t, stream);
 }
 
+// ---- batched one-sided ops ----
+
+namespace {
+
+constexpr uint32_t kBatchTileShift = 12;  // 4 KiB per wave-tile: 64 lanes x 16 B x 4 in flight
+constexpr int kBatchUnroll = 4;
+
+// One wave copies n bytes (n <= one wave-tile in the common case; any n works).
+template <bool NT>
+__device__ __forceinline__ void wave_copy(char *__restrict__ dst, const char *__restrict__ src, uint64_t n, int lane) {
+    uint64_t head = (16u - ((uintptr_t)dst & 15u)) & 15u;
+    if (head > n) head = n;
+    if ((uint64_t)lane < head) dst[lane] = src[lane];
+    dst += head;
+    src += head;
+    n -= head;
+    if (((uintptr_t)src & 15u) == 0) {
+        const uint64_t nv = n >> 4;
+        const u32x4 *s = reinterpret_cast<const u32x4 *>(src);
+        u32x4 *d = reinterpret_cast<u32x4 *>(dst);
+        uint64_t i = lane;
+        for (; i + (kBatchUnroll - 1) * 64 < nv; i += kBatchUnroll * 64) {
+            u32x4 v[kBatchUnroll];
+#pragma unroll
+            for (int k = 0; k < kBatchUnroll; k++) v[k] = load16(s + i + k * 64);
+#pragma unroll
+            for (int k = 0; k < kBatchUnroll; k++) store16<NT>(d + i + k * 64, v[k]);
+        }
+        for (; i < nv; i += 64) store16<NT>(d + i, load16(s + i));
+        const uint64_t tail = n & 15u;
+        if ((uint64_t)lane < tail) dst[(nv << 4) + lane] = src[(nv << 4) + lane];
+    } else {
+        for (uint64_t i = lane; i < n; i += 64) dst[i] = src[i];
+    }
+}
+
+template <bool NT>
+__global__ __launch_bounds__(kThreads) void xfer_batch_kernel(XferBatchArgs a) {
+    const int lane = threadIdx.x & 63;
+    // wave index, made scalar: everything below is wave-uniform
+    const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+    const uint64_t waves = (uint64_t)a.grid * kWaves;
+    const uint64_t per = (a.total_tiles + waves - 1) / waves;
+    uint64_t t = (uint64_t)w * per;
+    const uint64_t t1 = t + per < a.total_tiles ? t + per : a.total_tiles;
+    if (t >= t1) return;
+    const bool inl = a.n_ops <= (uint32_t)kXferInlineOps;
+    const XferBatchOp *ops = inl ? a.inline_ops : a.ops;
+    uint32_t i = inl ? 0u : a.wave_op[w];
+    const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
+    for (; t < t1; t++) {
+        while (i + 1 < a.n_ops && ops[i + 1].first_tile <= t) i++;
+        const XferBatchOp &op = ops[i];
+        TileSpan sp = tile_span_of(a, a.n_ext, a.unit_shift, a.tile_shift, a.lin + op.lin_off, op.rem_off, op.len,
+                                   op.put, t - op.first_tile, op.rem_off & ~tile_mask);
+        wave_copy<NT>(sp.dst, sp.src, sp.n, lane);
+    }
+}
+
+}  // namespace
+
+uint32_t xfer_batch_tile_shift(uint32_t n_ext, uint32_t unit_shift) {
+    return (n_ext > 1 && unit_shift < kBatchTileShift) ? unit_shift : kBatchTileShift;
+}
+
+uint64_t xfer_batch_plan(XferBatchOp *ops, uint32_t n, uint32_t tile_shift) {
+    const uint64_t mask = (1ull << tile_shift) - 1;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        ops[i].first_tile = total;
+        if (ops[i].len)
+            total += (((ops[i].rem_off + ops[i].len + mask) & ~mask) - (ops[i].rem_off & ~mask)) >> tile_shift;
+    }
+    return total;
+}
+
+uint32_t xfer_batch_grid(uint64_t total_tiles) {
+    // One wave per tile until the chip holds 8 workgroups (32 waves) per CU.
+    const uint64_t want = (total_tiles + kWaves - 1) / kWaves;
+    const uint64_t cap = (uint64_t)num_cus() * 8;
+    return (uint32_t)(want < cap ? (want ? want : 1) : cap);
+}
+
+void xfer_batch_wave_ops(const XferBatchOp *ops, uint32_t n, uint64_t total_tiles, uint32_t grid, uint32_t *out) {
+    const uint64_t waves = (uint64_t)grid * kWaves;
+    const uint64_t per = (total_tiles + waves - 1) / waves;
+    uint32_t i = 0;
+    for (uint64_t w = 0; w < waves; w++) {
+        const uint64_t t = w * per;
+        while (i + 1 < n && ops[i + 1].first_tile <= t) i++;
+        out[w] = i;
+    }
+}
+
+hipError_t xfer_batch_launch(const XferBatchArgs &a, const XferTuning &t, hipStream_t stream) {
+    if (a.total_tiles == 0 || a.n_ops == 0) return hipSuccess;
+    if (a.n_ext < 1 || a.n_ext > (uint32_t)kXferMaxExtents || a.grid == 0) return hipErrorInvalidValue;
+    if (a.n_ops > (uint32_t)kXferInlineOps && (!a.ops || !a.wave_op)) return hipErrorInvalidValue;
+    if (t.nontemporal)
+        hipLaunchKernelGGL(xfer_batch_kernel<true>, dim3(a.grid), dim3(kThreads), 0, stream, a);
+    else
+        hipLaunchKernelGGL(xfer_batch_kernel<false>, dim3(a.grid), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
 // ---- persistent copy service ----
 
 namespace {
@@ -298,7 +414,7 @@ __global__ __launch_bounds__(kThreads) void service_kernel(ServiceSlot *slot, un
             sh[threadIdx.x] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(&slot->args) + threadIdx.x,
                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __syncthreads();
-        XferArgs a = *reinterpret_cast<const XferArgs *>(sh);
+        const XferArgs &a = *reinterpret_cast<const XferArgs *>(sh);  // read in place (no scratch copy)
         const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
         const uint64_t first = a.rem_off & ~tile_mask;
         const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;

@@ -73,6 +73,10 @@ struct lib_alloc {
     bool pooled = false;      // local half from the stream-ordered pool
     int lane = -1;            // async ops: index into State::lanes (per-allocation ordering)
     hipEvent_t ev = nullptr;  // completion of the last async op (ocm_wait)
+    void *batch_dev = nullptr;  // device copy of large batch descriptor lists
+    void *batch_host = nullptr; // pinned staging for their upload
+    size_t batch_cap = 0;
+    hipEvent_t batch_up = nullptr;  // the last upload out of batch_host finished
 };
 
 namespace {
@@ -1099,6 +1103,15 @@ static int free_impl(ocm_alloc_t a) {
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (!a || !s.allocs.count(a)) OCM_FAIL(-1, "ocm_free: unknown allocation");
     wait_alloc(a);
+    if (a->batch_dev || a->batch_host) {
+        DeviceGuard g(s.device);
+        if (a->batch_up) (void)hipEventSynchronize(a->batch_up);
+        if (a->batch_dev) (void)hipFreeAsync(a->batch_dev, s.stream);
+        if (a->batch_host) (void)hipHostFree(a->batch_host);
+        if (a->batch_up) (void)hipEventDestroy(a->batch_up);
+        a->batch_dev = a->batch_host = nullptr;
+        a->batch_up = nullptr;
+    }
     if (a->ev) {
         DeviceGuard g(s.device);
         (void)hipEventDestroy(a->ev);
@@ -1169,6 +1182,123 @@ static int onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
                  (unsigned long long)p->bytes, a->remote_bytes);
     return xfer(a, p->op_flag != 0, static_cast<char *>(a->local) + p->src_offset, a->loc, p->dest_offset, p->bytes,
                 async);
+}
+
+static int batch_impl(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, int flags, uint64_t *moved);
+
+int ocm_copy_onesided_batch(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, int flags) {
+    TraceRange tr("ocm_batch");
+    const uint64_t t0 = now_ns();
+    uint64_t moved = 0;
+    int rc = batch_impl(a, ops, n_ops, flags, &moved);
+    const uint64_t t1 = now_ns();
+    if (rc == 0) {
+        OpCounters &c = S().ctr;
+        c.n_batch++;
+        c.n_batch_ops += (uint64_t)n_ops;
+        c.bytes_batch += moved;
+        c.ns_batch += t1 - t0;
+    }
+    trace_op("batch", moved, t0, t1, rc);
+    return rc;
+}
+
+static int batch_impl(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, int flags, uint64_t *moved) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!a || (!ops && n_ops)) OCM_FAIL(-1, "ocm_copy_onesided_batch: NULL argument");
+    if (!s.allocs.count(a)) OCM_FAIL(-1, "ocm_copy_onesided_batch: unknown allocation");
+    if (!a->remote) OCM_FAIL(-1, "batched one-sided copies need a remote pair (kind %d)", (int)a->kind);
+    if (n_ops < 0) OCM_FAIL(-1, "ocm_copy_onesided_batch: n_ops < 0");
+    const bool async = (flags & OCM_BATCH_ASYNC) != 0;
+    for (int i = 0; i < n_ops; i++) {
+        const ocm_params &p = ops[i];
+        if (p.src_offset > a->local_bytes || p.bytes > a->local_bytes - p.src_offset)
+            OCM_FAIL(-1, "batch op %d: local range [%llu,+%llu) exceeds %zu bytes", i,
+                     (unsigned long long)p.src_offset, (unsigned long long)p.bytes, a->local_bytes);
+        if (p.dest_offset > a->remote_bytes || p.bytes > a->remote_bytes - p.dest_offset)
+            OCM_FAIL(-1, "batch op %d: remote range [%llu,+%llu) exceeds %zu bytes", i,
+                     (unsigned long long)p.dest_offset, (unsigned long long)p.bytes, a->remote_bytes);
+        *moved += p.bytes;
+    }
+    if (n_ops == 0) return 0;
+    const bool one_kernel = s.device >= 0 && a->loc == LOC_DEVICE && a->all_dev_ok && !a->any_net &&
+                            (a->ext.size() == 1 || log2_exact(a->stripe_unit) >= 4);
+    if (!one_kernel) {
+        // No device-side path (CPU app, network tier, host local half): op by op, in order.
+        for (int i = 0; i < n_ops; i++)
+            if (xfer(a, ops[i].op_flag != 0, static_cast<char *>(a->local) + ops[i].src_offset, a->loc,
+                     ops[i].dest_offset, ops[i].bytes, async) != 0)
+                return -1;
+        return 0;
+    }
+    DeviceGuard guard(s.device);
+    XferBatchArgs args;
+    std::memset(&args, 0, sizeof(args));
+    args.lin = static_cast<char *>(a->local);
+    for (size_t i = 0; i < a->ext.size(); i++) args.ext[i] = a->ext[i].dptr;
+    args.n_ext = (uint32_t)a->ext.size();
+    args.unit_shift = args.n_ext > 1 ? (uint32_t)log2_exact(a->stripe_unit) : 0;
+    args.tile_shift = xfer_batch_tile_shift(args.n_ext, args.unit_shift);
+    args.n_ops = (uint32_t)n_ops;
+    std::vector<XferBatchOp> v((size_t)n_ops);
+    for (int i = 0; i < n_ops; i++) {
+        v[i].lin_off = ops[i].src_offset;
+        v[i].rem_off = ops[i].dest_offset;
+        v[i].len = ops[i].bytes;
+        v[i].put = ops[i].op_flag != 0;
+        v[i].pad = 0;
+    }
+    args.total_tiles = xfer_batch_plan(v.data(), (uint32_t)n_ops, args.tile_shift);
+    if (args.total_tiles == 0) return 0;  // only empty ops
+    args.grid = xfer_batch_grid(args.total_tiles);
+    if (!async && wait_alloc(a) != 0) return -1;
+    hipStream_t st = async ? lane_stream(a) : s.stream;
+    hipError_t err = hipSuccess;
+    if (n_ops <= kXferInlineOps) {
+        std::memcpy(args.inline_ops, v.data(), v.size() * sizeof(XferBatchOp));
+    } else {
+        // descriptors, then the per-wave starting ops, in one upload
+        const size_t dbytes = v.size() * sizeof(XferBatchOp);
+        const size_t need = dbytes + (size_t)args.grid * 4 * sizeof(uint32_t);
+        if (a->batch_up && hipEventSynchronize(a->batch_up) != hipSuccess)  // staging free again
+            OCM_FAIL(-1, "batch staging wait failed");
+        if (a->batch_cap < need) {
+            if (a->batch_dev) (void)hipFreeAsync(a->batch_dev, st);
+            if (a->batch_host) (void)hipHostFree(a->batch_host);
+            a->batch_dev = a->batch_host = nullptr;
+            a->batch_cap = 0;
+            const size_t cap = std::max<size_t>(need, 64 << 10);
+            err = local_pool() ? hipMallocFromPoolAsync(&a->batch_dev, cap, s.pool, st) : hipMallocAsync(&a->batch_dev, cap, st);
+            if (err == hipSuccess) err = hipHostMalloc(&a->batch_host, cap, hipHostMallocDefault);
+            if (err == hipSuccess && !a->batch_up) err = hipEventCreateWithFlags(&a->batch_up, hipEventDisableTiming);
+            if (err != hipSuccess) {
+                (void)hipGetLastError();
+                OCM_FAIL(-1, "batch descriptors: %s", hipGetErrorString(err));
+            }
+            a->batch_cap = cap;
+        }
+        char *up = static_cast<char *>(a->batch_host);
+        std::memcpy(up, v.data(), dbytes);
+        xfer_batch_wave_ops(v.data(), (uint32_t)n_ops, args.total_tiles, args.grid, reinterpret_cast<uint32_t *>(up + dbytes));
+        // Pinned source: a real async DMA; batch_up tells the next batch when `up` is free.
+        err = hipMemcpyAsync(a->batch_dev, up, need, hipMemcpyHostToDevice, st);
+        if (err == hipSuccess) err = hipEventRecord(a->batch_up, st);
+        if (err != hipSuccess) OCM_FAIL(-1, "batch descriptor upload: %s", hipGetErrorString(err));
+        args.ops = static_cast<const XferBatchOp *>(a->batch_dev);
+        args.wave_op = reinterpret_cast<const uint32_t *>(static_cast<char *>(a->batch_dev) + dbytes);
+    }
+    err = xfer_batch_launch(args, s.tuning, st);
+    if (err != hipSuccess) OCM_FAIL(-1, "batch launch failed: %s", hipGetErrorString(err));
+    if (async) {
+        if (st != s.stream && a->ev) {
+            err = hipEventRecord(a->ev, st);
+            if (err != hipSuccess) OCM_FAIL(-1, "event record failed: %s", hipGetErrorString(err));
+            a->async_pending = true;
+            return 0;
+        }
+    }
+    return sync_stream();
 }
 
 int ocm_copy_onesided(ocm_alloc_t a, ocm_param_t p) { return ocm_copy_onesided_impl(a, p, false); }
@@ -1350,11 +1480,12 @@ const char *ocm_last_error(void) { return last_error(); }
 
 // ---------------- internal hooks for tests and benchmarks (not part of the ABI) ----------------
 
-// Per-process operation counters (see ocm/trace.h): 12 x uint64.
-void ocm_x_counters(uint64_t out[12]) {
+// Per-process operation counters (see ocm/trace.h): 16 x uint64.
+void ocm_x_counters(uint64_t out[16]) {
     const OpCounters &c = S().ctr;
-    const uint64_t v[12] = {c.n_put, c.n_get, c.bytes_put, c.bytes_get, c.n_alloc, c.n_free,
-                            c.n_copy, c.bytes_copy, c.ns_put, c.ns_get, c.ns_alloc, c.ns_free};
+    const uint64_t v[16] = {c.n_put,  c.n_get,    c.bytes_put, c.bytes_get,   c.n_alloc,     c.n_free,
+                            c.n_copy, c.bytes_copy, c.ns_put,  c.ns_get,      c.ns_alloc,    c.ns_free,
+                            c.n_batch, c.n_batch_ops, c.bytes_batch, c.ns_batch};
     std::memcpy(out, v, sizeof(v));
 }
 

@@ -151,6 +151,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_copy_onesided": (i32, [vp, ctypes.POINTER(OcmParams)]),
             "ocm_copy_onesided_async": (i32, [vp, ctypes.POINTER(OcmParams)]),
             "ocm_wait": (i32, [vp]),
+            "ocm_copy_onesided_batch": (i32, [vp, ctypes.POINTER(OcmParams), i32, i32]),
             "ocm_remote_info": (i32, [vp, ctypes.POINTER(OcmRemoteInfo)]),
             "ocm_remotebuf": (vp, [vp]),
             "ocm_stats": (i32, [i32, ctypes.POINTER(OcmDaemonStats)]),
@@ -179,12 +180,29 @@ def last_error() -> str:
 
 
 COUNTER_KEYS = ["n_put", "n_get", "bytes_put", "bytes_get", "n_alloc", "n_free", "n_copy", "bytes_copy", "ns_put",
-                "ns_get", "ns_alloc", "ns_free"]
+                "ns_get", "ns_alloc", "ns_free", "n_batch", "n_batch_ops", "bytes_batch", "ns_batch"]
+OCM_BATCH_ASYNC = 1
+
+
+class BatchOps:
+    """A prepared descriptor list for Allocation.batch (ctypes array of ocm_params)."""
+
+    def __init__(self, array, n: int):
+        self.array = array
+        self.n = n
+
+
+def batch_ops(ops) -> BatchOps:
+    ops = list(ops)
+    arr = (OcmParams * max(1, len(ops)))()
+    for i, (flag, loff, roff, n) in enumerate(ops):
+        arr[i] = OcmParams(loff, roff, 0, 0, n, flag)
+    return BatchOps(arr, len(ops))
 
 
 def counters() -> dict:
     """This process's libocm operation counters."""
-    out = (ctypes.c_uint64 * 12)()
+    out = (ctypes.c_uint64 * len(COUNTER_KEYS))()
     load().ocm_x_counters(out)
     return dict(zip(COUNTER_KEYS, [int(v) for v in out]))
 
@@ -266,6 +284,16 @@ class Allocation:
     def wait(self) -> None:
         if self._c.lib.ocm_wait(self.handle) != 0:
             raise OcmError("ocm_wait: " + last_error())
+
+    def batch(self, ops, async_: bool = False) -> None:
+        """Many one-sided ops in one launch (ocm_copy_onesided_batch).
+
+        ops: iterable of (op_flag, local_offset, remote_offset, nbytes) with op_flag 1 = put,
+        0 = get; or a prepared :func:`batch_ops` array (no per-call conversion).
+        """
+        arr = ops if isinstance(ops, BatchOps) else batch_ops(ops)
+        if self._c.lib.ocm_copy_onesided_batch(self.handle, arr.array, arr.n, OCM_BATCH_ASYNC if async_ else 0) != 0:
+            raise OcmError("ocm_copy_onesided_batch: " + last_error())
 
     def time_onesided(self, op_flag: int, nbytes: int, iters: int, local_offset: int = 0, remote_offset: int = 0) -> float:
         """Seconds per blocking one-sided op, timed inside the native library."""
