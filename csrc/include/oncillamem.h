@@ -143,6 +143,12 @@ int ocm_wait(ocm_alloc_t a);
  * defined order. flags: OCM_BATCH_ASYNC completes later (ocm_wait). */
 #define OCM_BATCH_ASYNC 1
 int ocm_copy_onesided_batch(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, int flags);
+/* Stream interop (hipStream_t passed as void*, NULL = legacy default stream):
+ * ocm_stream_wait:   a's next one-sided op starts after the work already queued on `stream`
+ *                    (e.g. torch kernels that wrote the local half).
+ * ocm_stream_signal: work queued on `stream` afterwards starts after a's queued async ops. */
+int ocm_stream_wait(ocm_alloc_t a, void *stream);
+int ocm_stream_signal(ocm_alloc_t a, void *stream);
 int ocm_remote_info(ocm_alloc_t a, struct ocm_remote_info *info);
 /* Device pointer of the remote half when it is a single extent (NULL if striped). */
 void *ocm_remotebuf(ocm_alloc_t a);

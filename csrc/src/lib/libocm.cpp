@@ -77,6 +77,8 @@ struct lib_alloc {
     void *batch_host = nullptr; // pinned staging for their upload
     size_t batch_cap = 0;
     hipEvent_t batch_up = nullptr;  // the last upload out of batch_host finished
+    hipEvent_t dep_ev = nullptr;    // ocm_stream_wait: external work the next op depends on
+    bool dep_pending = false;
 };
 
 namespace {
@@ -350,6 +352,16 @@ int wait_event(hipEvent_t ev) {
     return 0;
 }
 
+// ocm_stream_wait dependency: order it before work on `st` (nullptr: the
+// copy service, which has no stream, so wait on the host).
+int honor_dep(lib_alloc *a, hipStream_t st, bool host_wait) {
+    if (!a->dep_pending) return 0;
+    a->dep_pending = false;
+    hipError_t e = host_wait ? hipEventSynchronize(a->dep_ev) : hipStreamWaitEvent(st, a->dep_ev, 0);
+    if (e != hipSuccess) OCM_FAIL(-1, "stream dependency: %s", hipGetErrorString(e));
+    return 0;
+}
+
 // Completion of `a`'s queued async ops (its lane up to the recorded event).
 int wait_alloc(lib_alloc *a) {
     State &s = S();
@@ -579,6 +591,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         std::vector<Seg> segs;
         segments(a, rem_off, len, segs);
         if (wait_alloc(a) != 0) return -1;
+        if (honor_dep(a, nullptr, true) != 0) return -1;
         for (auto &g : segs) {
             const Extent &e = a->ext[g.ext];
             if (e.net) {
@@ -630,6 +643,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         x.put = put ? 1 : 0;
         if (x.n_ext > 1) x.unit_shift = (uint32_t)log2_exact(a->stripe_unit);
         if (wait_alloc(a) != 0) return -1;  // keep program order with queued async ops
+        if (honor_dep(a, nullptr, true) != 0) return -1;
         if (service_xfer(x) == 0) return 0;
         OCM_WARN("copy service failed (%s); falling back to launches", last_error());
         s.svc_max = 0;
@@ -638,6 +652,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     // after the allocation's queued async work.
     if (!async && wait_alloc(a) != 0) return -1;
     hipStream_t st = async ? lane_stream(a) : s.stream;
+    if (honor_dep(a, st, false) != 0) return -1;
     if (use_kernel) {
         XferArgs x;
         std::memset(&x, 0, sizeof(x));
@@ -1117,6 +1132,11 @@ static int free_impl(ocm_alloc_t a) {
         (void)hipEventDestroy(a->ev);
         a->ev = nullptr;
     }
+    if (a->dep_ev) {
+        DeviceGuard g(s.device);
+        (void)hipEventDestroy(a->dep_ev);
+        a->dep_ev = nullptr;
+    }
     // Unmap dedicated remote slabs before the owner frees them.
     for (auto &e : a->ext) release_extent(e, false);
     free_local_half(a);
@@ -1254,6 +1274,7 @@ static int batch_impl(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, in
     args.grid = xfer_batch_grid(args.total_tiles);
     if (!async && wait_alloc(a) != 0) return -1;
     hipStream_t st = async ? lane_stream(a) : s.stream;
+    if (honor_dep(a, st, false) != 0) return -1;
     hipError_t err = hipSuccess;
     if (n_ops <= kXferInlineOps) {
         std::memcpy(args.inline_ops, v.data(), v.size() * sizeof(XferBatchOp));
@@ -1299,6 +1320,34 @@ static int batch_impl(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, in
         }
     }
     return sync_stream();
+}
+
+int ocm_stream_wait(ocm_alloc_t a, void *stream) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!a || !s.allocs.count(a)) OCM_FAIL(-1, "ocm_stream_wait: unknown allocation");
+    if (s.device < 0) return 0;  // CPU app: every op is synchronous already
+    DeviceGuard g(s.device);
+    if (!a->dep_ev && hipEventCreateWithFlags(&a->dep_ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        a->dep_ev = nullptr;
+        OCM_FAIL(-1, "ocm_stream_wait: no event");
+    }
+    hipError_t e = hipEventRecord(a->dep_ev, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) OCM_FAIL(-1, "ocm_stream_wait: %s", hipGetErrorString(e));
+    a->dep_pending = true;
+    return 0;
+}
+
+int ocm_stream_signal(ocm_alloc_t a, void *stream) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!a || !s.allocs.count(a)) OCM_FAIL(-1, "ocm_stream_signal: unknown allocation");
+    if (s.device < 0 || !a->async_pending || !a->ev) return 0;  // nothing queued: already complete
+    DeviceGuard g(s.device);
+    hipError_t e = hipStreamWaitEvent(static_cast<hipStream_t>(stream), a->ev, 0);
+    if (e != hipSuccess) OCM_FAIL(-1, "ocm_stream_signal: %s", hipGetErrorString(e));
+    return 0;
 }
 
 int ocm_copy_onesided(ocm_alloc_t a, ocm_param_t p) { return ocm_copy_onesided_impl(a, p, false); }

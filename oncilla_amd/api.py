@@ -152,6 +152,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_copy_onesided_async": (i32, [vp, ctypes.POINTER(OcmParams)]),
             "ocm_wait": (i32, [vp]),
             "ocm_copy_onesided_batch": (i32, [vp, ctypes.POINTER(OcmParams), i32, i32]),
+            "ocm_stream_wait": (i32, [vp, vp]),
+            "ocm_stream_signal": (i32, [vp, vp]),
             "ocm_remote_info": (i32, [vp, ctypes.POINTER(OcmRemoteInfo)]),
             "ocm_remotebuf": (vp, [vp]),
             "ocm_stats": (i32, [i32, ctypes.POINTER(OcmDaemonStats)]),
@@ -193,6 +195,23 @@ class BatchOps:
 
 
 def batch_ops(ops) -> BatchOps:
+    """Descriptor list from (op_flag, local_offset, remote_offset, nbytes) tuples, or from an
+    (n, 4) integer array with those columns (vectorised, no per-op Python objects)."""
+    try:
+        import numpy as np
+    except ImportError:  # pragma: no cover
+        np = None
+    if np is not None and isinstance(ops, np.ndarray):
+        n = int(ops.shape[0])
+        mat = np.zeros((max(1, n), 6), dtype=np.uint64)  # struct ocm_params: 6 x u64
+        if n:
+            mat[:n, 0] = ops[:, 1]  # src_offset  (local)
+            mat[:n, 1] = ops[:, 2]  # dest_offset (remote)
+            mat[:n, 4] = ops[:, 3]  # bytes
+            mat[:n, 5] = ops[:, 0]  # op_flag
+        b = BatchOps(mat.ctypes.data_as(ctypes.POINTER(OcmParams)), n)
+        b.keep = mat
+        return b
     ops = list(ops)
     arr = (OcmParams * max(1, len(ops)))()
     for i, (flag, loff, roff, n) in enumerate(ops):
@@ -284,6 +303,28 @@ class Allocation:
     def wait(self) -> None:
         if self._c.lib.ocm_wait(self.handle) != 0:
             raise OcmError("ocm_wait: " + last_error())
+
+    @staticmethod
+    def _stream_handle(stream):
+        if stream is None:
+            import torch
+
+            stream = torch.cuda.current_stream()
+        return ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+
+    def stream_wait(self, stream=None) -> None:
+        """Order this allocation's next op after the work queued on `stream` (default: torch's current stream)."""
+        if self._c.device < 0:
+            return
+        if self._c.lib.ocm_stream_wait(self.handle, self._stream_handle(stream)) != 0:
+            raise OcmError("ocm_stream_wait: " + last_error())
+
+    def stream_signal(self, stream=None) -> None:
+        """Make later work on `stream` (default: torch's current stream) wait for this allocation's async ops."""
+        if self._c.device < 0:
+            return
+        if self._c.lib.ocm_stream_signal(self.handle, self._stream_handle(stream)) != 0:
+            raise OcmError("ocm_stream_signal: " + last_error())
 
     def batch(self, ops, async_: bool = False) -> None:
         """Many one-sided ops in one launch (ocm_copy_onesided_batch).

@@ -1,4 +1,7 @@
-"""Benchmark workloads (BASELINE.json configs #1-#5)."""
+"""Workloads on the runtime: the BASELINE.json configs (#1-#5) and a serving
+use of disaggregated memory (paged KV-cache offload)."""
+from .kv_offload import PagedKVOffload, coalesce
 from .workloads import alloc_latency, characterize, churn, percentile, rw_sweep_step, spill_probe, sweep_sizes
 
-__all__ = ["alloc_latency", "characterize", "churn", "percentile", "rw_sweep_step", "spill_probe", "sweep_sizes"]
+__all__ = ["PagedKVOffload", "alloc_latency", "characterize", "churn", "coalesce", "percentile", "rw_sweep_step",
+           "spill_probe", "sweep_sizes"]
