@@ -34,6 +34,7 @@ int mbox_accept(int listen_fd, pid_t *peer_pid);
 int mbox_connect(const std::string &name, int timeout_ms);
 // Peer pid of a connected mailbox socket (SO_PEERCRED), -1 on error.
 pid_t mbox_peer_pid(int fd);
+int mbox_peer_uid(int fd);  // SO_PEERCRED uid, -1 on error
 // One record. timeout_ms < 0 blocks, 0 polls. Returns 1 ok, 0 timeout / would
 // block, -1 error or peer closed.
 int mbox_send(int fd, const void *msg, size_t size, int timeout_ms);

@@ -227,8 +227,10 @@ int Governor::num_alive() const {
 
 bool Governor::fits(const NodeState &n, uint32_t tier, uint64_t bytes) const {
     if (!n.alive || !n.joined) return false;
-    if (tier == TIER_GPU) return n.gpu >= 0 && n.gpu_reserved + bytes <= n.gpu_capacity;
-    if (tier == TIER_HOST) return n.host_reserved + bytes <= n.host_capacity;
+    // Overflow-safe: `reserved + bytes` would wrap for absurd requests.
+    auto room = [&](uint64_t used, uint64_t cap) { return bytes <= cap && used <= cap - bytes; };
+    if (tier == TIER_GPU) return n.gpu >= 0 && room(n.gpu_reserved, n.gpu_capacity);
+    if (tier == TIER_HOST) return room(n.host_reserved, n.host_capacity);
     return false;
 }
 
@@ -292,6 +294,11 @@ Placement Governor::place(const PlaceRequest &r) {
     Placement p;
     const int n = (int)nodes_.size();
     if (r.bytes == 0 || r.orig_rank < 0 || r.orig_rank >= n) {
+        p.err = EINVAL;
+        return p;
+    }
+    // The data plane addresses stripes with shifts: a unit must be a power of two >= 16.
+    if (r.stripe_unit && (r.stripe_unit < 16 || (r.stripe_unit & (r.stripe_unit - 1)))) {
         p.err = EINVAL;
         return p;
     }

@@ -87,6 +87,13 @@ pid_t mbox_peer_pid(int fd) {
     return cr.pid;
 }
 
+int mbox_peer_uid(int fd) {
+    struct ucred cr;
+    socklen_t l = sizeof(cr);
+    if (getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cr, &l) != 0) return -1;
+    return (int)cr.uid;
+}
+
 int mbox_accept(int listen_fd, pid_t *peer_pid) {
     for (;;) {
         int fd = accept4(listen_fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);

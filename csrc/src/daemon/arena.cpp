@@ -123,7 +123,8 @@ int Arena::alloc(uint32_t tier, uint64_t bytes, Region *out) {
     std::lock_guard<std::mutex> lk(mu_);
     if (bytes == 0) return EINVAL;
     if (tier != TIER_GPU && tier != TIER_HOST) return EINVAL;
-    if ((tier == TIER_GPU ? used_gpu_ : used_host_) + bytes > capacity(tier)) return ENOMEM;
+    const uint64_t cap = capacity(tier), used = tier == TIER_GPU ? used_gpu_ : used_host_;
+    if (bytes > cap || used > cap - bytes) return ENOMEM;  // overflow-safe
     uint64_t slab_default = tier == TIER_GPU ? cfg_.slab_bytes : std::min<uint64_t>(cfg_.slab_bytes, 256ull << 20);
     // Never map more than the tier may hand out (small capacities in tests / shared GPUs).
     slab_default = std::max(kHugeAlign, std::min(slab_default, (capacity(tier) + kHugeAlign - 1) & ~(kHugeAlign - 1)));

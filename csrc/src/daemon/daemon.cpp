@@ -600,6 +600,15 @@ void Daemon::on_mailbox() {
         pid_t peer = -1;
         int fd = mbox_accept(mbox_fd_, &peer);
         if (fd < 0) break;
+        // Abstract sockets carry no file permissions: only our own user (or root)
+        // may attach, allocate, free or stop us (OCM_ALLOW_ANY_UID=1 lifts this).
+        static const bool any_uid = std::getenv("OCM_ALLOW_ANY_UID") != nullptr;
+        const int uid = mbox_peer_uid(fd);
+        if (!any_uid && uid != (int)geteuid() && uid != 0) {
+            OCM_WARN("rank %d: refusing mailbox connection from uid %d (pid %d)", rank_, uid, (int)peer);
+            close(fd);
+            continue;
+        }
         AppConn c;
         c.fd = fd;
         c.peer_pid = peer;

@@ -1,0 +1,125 @@
+"""Daemon robustness against malformed / adversarial mailbox traffic.
+
+Any local process can reach a daemon's mailbox, so records are untrusted:
+random bytes, wrong sizes, requests before CONNECT, absurd sizes (2^63), bad
+stripe units, out-of-range ranks, unknown kinds. After the storm the daemons
+must still be alive and serving; whatever the fuzzer got allocated must be
+reclaimed when its connection closes, and other users must be refused.
+"""
+import os
+import random
+import socket
+import struct
+import subprocess
+import sys
+import textwrap
+import time
+
+import pytest
+
+from oncilla_amd import api
+
+MSG = struct.Struct("<IIiiQii128s")  # type, status, pid, rank, seq, src_rank, err, union
+REQ = struct.Struct("<iiQIIIIQQii")   # orig, remote_rank, bytes, kind, flags, width, tier, unit, alloc_id, pid, n_ext
+SHUTDOWN = 17  # MSG_SHUTDOWN: a legitimate same-user operation, not fuzzed
+
+
+@pytest.fixture(autouse=True)
+def _cpu_app(monkeypatch):
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+
+
+def _connect(ns, rank=0):
+    s = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    s.connect(b"\0" + f"ocm_{ns}_d{rank}".encode())
+    s.setblocking(False)  # (a socket timeout would make every recv wait it out)
+    return s
+
+
+def _req(rng, kind=None):
+    big = rng.choice([0, 1, 4096, 1 << 20, (1 << 63) + 5, (1 << 64) - 1, rng.getrandbits(64)])
+    return REQ.pack(rng.randint(-5, 9), rng.choice([-1, -7, 0, 1, 2, 1 << 30]), big,
+                    kind if kind is not None else rng.randint(0, 9), rng.getrandbits(32), rng.choice([0, 1, 3, 9, 1 << 31]),
+                    rng.randint(0, 5), rng.choice([0, 3, 16, 4096, 1 << 20, rng.getrandbits(64)]), rng.getrandbits(64),
+                    rng.randint(-3, 1 << 30), rng.randint(-2, 1 << 16)).ljust(128, b"\0")
+
+
+def _storm(ns, seed, n=3000):
+    rng = random.Random(seed)
+    s = _connect(ns)
+    for i in range(n):
+        r = rng.random()
+        if r < 0.1:
+            payload = os.urandom(rng.choice([1, 10, 159, 161, 300]))  # wrong sizes
+        elif r < 0.3:
+            payload = os.urandom(160)
+        else:
+            t = rng.choice([1, 2, 3, 5, 7, 9, 15, 16, 18, 19, 20, 0, 99, 1 << 31])
+            if t == SHUTDOWN:
+                continue
+            payload = MSG.pack(t, rng.randint(0, 3), rng.randint(-5, 1 << 30), rng.randint(-3, 9), rng.getrandbits(64),
+                               rng.randint(-3, 9), rng.randint(-3, 200), _req(rng))
+        for _ in range(200):
+            try:
+                s.send(payload)
+                break
+            except BlockingIOError:
+                time.sleep(0.001)  # daemon busy: its receive queue is full
+            except OSError:
+                s.close()
+                s = _connect(ns)  # the daemon dropped us: come back
+                break
+        try:
+            while s.recv(4096):  # drain replies
+                pass
+        except OSError:
+            pass
+    s.close()
+
+
+def test_mailbox_fuzz_daemons_survive(mesh_factory):
+    m = mesh_factory(3, extra_args=["--host-capacity", str(64 << 20)])
+    for seed in range(3):
+        _storm(m.ns, seed)
+    time.sleep(0.3)
+    assert all(d.alive() for d in m.daemons), m.logs()[-4000:]
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        # the fuzzer's connections are gone: anything it obtained was reclaimed
+        deadline = time.time() + 10
+        while time.time() < deadline and any(c.stats(r)["host_used"] for r in range(3)):
+            time.sleep(0.05)
+        assert [c.stats(r)["host_used"] for r in range(3)] == [0, 0, 0], m.logs()[-4000:]
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)
+        a.fill(seed=5)
+        a.put(0, 0, 1 << 20)
+        a.fill(seed=0)
+        a.get(0, 0, 1 << 20)
+        assert a.check(seed=5) == 0
+        a.free()
+        # absurd sizes are refused, not wrapped around
+        with pytest.raises(api.OcmError):
+            c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=(1 << 63) + 4096)
+        with pytest.raises(api.OcmError):
+            c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20, stripe_unit=3000)
+
+
+@pytest.mark.skipif(os.geteuid() != 0, reason="needs root to switch to another uid")
+def test_other_users_are_refused(mesh_factory):
+    m = mesh_factory(1)
+    code = textwrap.dedent(f"""
+        import os, socket, sys
+        os.setgid(65534); os.setuid(65534)
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+        s.connect(b"\\0ocm_{m.ns}_d0")
+        s.settimeout(5)
+        s.send(bytes(160))
+        try:
+            data = s.recv(160)
+        except OSError as e:
+            data = b""
+        print("closed" if data == b"" else "served")
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=30)
+    assert r.stdout.strip() == "closed", r.stdout + r.stderr
+    assert "refusing mailbox connection" in m.logs()
+    assert m.daemons[0].alive()
