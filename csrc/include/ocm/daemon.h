@@ -55,6 +55,7 @@ struct DaemonConfig {
     int lease_idle_ms = 2000;        // give an empty lease back after this long (capacity is not stranded)
     bool lease_host = false;         // also lease host-tier capacity (tests; OCM_LEASE_HOST=1)
     std::string host_alias;          // report this host name (tests: pretend daemons are on other nodes)
+    std::string mesh_key;            // OCM_MESH_KEY: shared secret mixed into the mesh HELLO token
     std::string state_file;          // rank0: directory checkpoint (resume after a rank0 restart)
     int state_interval_ms = 20;      // max staleness of that checkpoint while the directory changes
 };
@@ -221,6 +222,9 @@ private:
     uint64_t n_alloc_ = 0, n_free_ = 0, n_reclaimed_ = 0, n_spilled_ = 0;
     // checkpoint / resume
     uint64_t boot_id_ = 0;               // this process lifetime
+    uint64_t mesh_token_ = 0;            // HELLO must carry it (hash of namespace + mesh key)
+    uint64_t data_token_ = 0;            // network-tier data server: random per boot
+    void send_hello(int fd);
     bool resumed_ = false;               // rank0 restored its directory from state_file
     uint64_t saved_version_ = 0;
     long last_save_ms_ = 0;

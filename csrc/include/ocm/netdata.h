@@ -7,7 +7,7 @@
 // owner daemon runs a data server and the app streams one-sided PUT/GET
 // records to it over TCP. The owner's CPU moves the bytes (like EXTOLL's
 // notification-driven transfers), HBM owners stage through pinned buffers.
-// Extents reached this way carry REGION_NET and "net:<ip>:<port>" as handle.
+// Extents reached this way carry REGION_NET and "net:<ip>:<port>:<token>" as handle.
 #pragma once
 #include <atomic>
 #include <cstdint>
@@ -42,7 +42,9 @@ class Arena;
 
 class DataServer {
 public:
-    DataServer(Arena *arena, int gpu);
+    // `token`: a connection must send these 8 bytes first (apps learn it from
+    // the net: handle their own daemon hands them).
+    DataServer(Arena *arena, int gpu, uint64_t token);
     ~DataServer();
     int start(const std::string &bind_ip);  // ephemeral port
     int port() const { return port_; }
@@ -53,6 +55,7 @@ private:
     void serve(int fd);
     Arena *arena_;
     int gpu_;
+    uint64_t token_;
     int listen_fd_ = -1, port_ = 0;
     std::atomic<bool> stop_{false};
     std::thread acceptor_;
@@ -61,6 +64,7 @@ private:
     std::vector<int> conns_;
 };
 
-bool parse_net_handle(const uint8_t *handle, std::string *ip, int *port);
+// "net:<ip>:<port>:<token hex>"
+bool parse_net_handle(const uint8_t *handle, std::string *ip, int *port, uint64_t *token);
 
 }  // namespace ocm

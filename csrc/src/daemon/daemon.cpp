@@ -87,6 +87,7 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
     if (const char *v = env("OCM_LEASE_IDLE_MS")) cfg->lease_idle_ms = std::atoi(v);
     if (const char *v = env("OCM_HOST_ALIAS")) cfg->host_alias = v;
     if (const char *v = env("OCM_STATE_FILE")) cfg->state_file = v;
+    if (const char *v = env("OCM_MESH_KEY")) cfg->mesh_key = v;
     if (const char *v = env("OCM_STATE_INTERVAL_MS")) cfg->state_interval_ms = std::atoi(v);
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
@@ -270,7 +271,13 @@ int Daemon::init() {
                            ? cfg_.host_capacity
                            : (uint64_t)((double)mem_available() * cfg_.host_fraction / std::max(1, local_daemons));
     arena_ = std::make_unique<Arena>(ac);
-    data_ = std::make_unique<DataServer>(arena_.get(), gpu_);
+    {
+        uint64_t tok = 0;
+        std::ifstream ur("/dev/urandom", std::ios::binary);
+        ur.read(reinterpret_cast<char *>(&tok), sizeof(tok));
+        data_token_ = tok ? tok : ((uint64_t)getpid() << 20) ^ (uint64_t)now_ms();
+    }
+    data_ = std::make_unique<DataServer>(arena_.get(), gpu_, data_token_);
     if (data_->start(cfg_.bind_ip.empty() ? "0.0.0.0" : cfg_.bind_ip) != 0) {
         OCM_WARN("rank %d: network data server unavailable; cross-node placement disabled here", rank_);
         data_.reset();
@@ -279,6 +286,12 @@ int Daemon::init() {
         std::ifstream ur("/dev/urandom", std::ios::binary);
         ur.read(reinterpret_cast<char *>(&boot_id_), sizeof(boot_id_));
         if (!boot_id_) boot_id_ = ((uint64_t)getpid() << 32) ^ (uint64_t)now_ms();
+    }
+    {
+        // FNV-1a over namespace + shared key: strangers on the mesh port cannot join.
+        uint64_t h = 1469598103934665603ull;
+        for (char ch : ns_ + '\x1f' + cfg_.mesh_key) h = (h ^ (uint8_t)ch) * 1099511628211ull;
+        mesh_token_ = h ? h : 1;
     }
     if (rank_ == 0) {
         gov_ = std::make_unique<Governor>(n_, cfg_.policy, cfg_.stripe_unit);
@@ -353,12 +366,7 @@ int Daemon::init() {
             OCM_WARN("rank %d unreachable; continuing without it", r);
             continue;
         }
-        Msg hello;
-        std::memset(&hello, 0, sizeof(hello));
-        hello.type = MSG_HELLO;
-        hello.src_rank = rank_;
-        hello.rank = rank_;
-        send_all(fd, &hello, sizeof(hello));
+        send_hello(fd);
         set_nonblocking(fd, true);
         auto c = std::make_unique<Conn>();
         c->fd = fd;
@@ -373,6 +381,16 @@ int Daemon::init() {
              rank_, n_, gpu_, num_gpu_, (double)arena_->capacity(TIER_GPU) / (1 << 30),
              (double)arena_->capacity(TIER_HOST) / (1 << 30), policy_name(cfg_.policy), ns_.c_str());
     return 0;
+}
+
+void Daemon::send_hello(int fd) {
+    Msg hello;
+    std::memset(&hello, 0, sizeof(hello));
+    hello.type = MSG_HELLO;
+    hello.src_rank = rank_;
+    hello.rank = rank_;
+    hello.seq = mesh_token_;
+    send_all(fd, &hello, sizeof(hello));
 }
 
 void Daemon::join_rank0() {
@@ -423,12 +441,7 @@ void Daemon::try_rejoin_rank0() {
     const NodeEntry &ne = nf_.nodes[0];
     int fd = tcp_connect(ne.ip, ne.ocm_port, 50);
     if (fd < 0) return;
-    Msg hello;
-    std::memset(&hello, 0, sizeof(hello));
-    hello.type = MSG_HELLO;
-    hello.src_rank = rank_;
-    hello.rank = rank_;
-    send_all(fd, &hello, sizeof(hello));
+    send_hello(fd);
     set_nonblocking(fd, true);
     auto c = std::make_unique<Conn>();
     c->fd = fd;
@@ -489,7 +502,7 @@ void Daemon::check_ready() {
         std::string tmp = cfg_.ready_file + ".tmp";
         std::ofstream f(tmp);
         f << "{\"rank\": " << rank_ << ", \"gpu\": " << gpu_ << ", \"pid\": " << getpid() << ", \"nodes\": " << n_
-          << "}\n";
+          << ", \"data_port\": " << (data_ ? data_->port() : 0) << "}\n";
         f.close();
         rename(tmp.c_str(), cfg_.ready_file.c_str());
     }
@@ -705,6 +718,7 @@ void Daemon::on_conn_readable(int fd) {
     std::vector<std::vector<uint8_t>> recs;
     int rc = conn_read_records(*it->second, kMsgBytes, recs);
     for (auto &r : recs) {
+        if (!conns_.count(fd)) return;  // dropped while handling an earlier record
         Msg m;
         std::memcpy(&m, r.data(), kMsgBytes);
         handle_mesh_msg(m, fd);
@@ -984,6 +998,17 @@ void Daemon::app_stats(Msg &m) {
 // ---------------------------------------------------------------- mesh messages
 
 void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
+    if (from_fd >= 0) {
+        // An inbound link is anonymous until its HELLO carries our mesh token.
+        auto it = conns_.find(from_fd);
+        if (it == conns_.end()) return;
+        if (it->second->peer_rank < 0 &&
+            (m.type != MSG_HELLO || m.seq != mesh_token_ || m.src_rank < 0 || m.src_rank >= n_ || m.src_rank == rank_)) {
+            OCM_WARN("rank %d: dropping unauthenticated mesh link (%s)", rank_, msg_type_str(m.type));
+            drop_conn(from_fd);
+            return;
+        }
+    }
     TraceRange tr(msg_type_str(m.type));
     OCM_LOG("rank %d <- rank %d: %s/%s seq %llu", rank_, m.src_rank, msg_type_str(m.type), msg_status_str(m.status),
             (unsigned long long)m.seq);
@@ -1239,8 +1264,8 @@ void Daemon::owner_do_alloc(Msg &m) {
         }
         // Other node: the app streams through our data server instead of mapping the slab.
         std::memset(rg.handle, 0, sizeof(rg.handle));
-        std::snprintf(reinterpret_cast<char *>(rg.handle), sizeof(rg.handle), "net:%s:%d", nf_.nodes[rank_].ip.c_str(),
-                      data_->port());
+        std::snprintf(reinterpret_cast<char *>(rg.handle), sizeof(rg.handle), "net:%s:%d:%llx",
+                      nf_.nodes[rank_].ip.c_str(), data_->port(), (unsigned long long)data_token_);
         rg.flags = (uint16_t)(rg.flags & ~REGION_DEDICATED);
     }
     OwnedExtent oe;

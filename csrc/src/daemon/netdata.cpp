@@ -16,18 +16,20 @@
 
 namespace ocm {
 
-bool parse_net_handle(const uint8_t *handle, std::string *ip, int *port) {
+bool parse_net_handle(const uint8_t *handle, std::string *ip, int *port, uint64_t *token) {
     char buf[65] = {0};
     std::memcpy(buf, handle, 64);
     char host[64] = {0};
     int p = 0;
-    if (std::sscanf(buf, "net:%63[^:]:%d", host, &p) != 2 || p <= 0) return false;
+    unsigned long long t = 0;
+    if (std::sscanf(buf, "net:%63[^:]:%d:%llx", host, &p, &t) != 3 || p <= 0) return false;
     *ip = host;
     *port = p;
+    *token = t;
     return true;
 }
 
-DataServer::DataServer(Arena *arena, int gpu) : arena_(arena), gpu_(gpu) {}
+DataServer::DataServer(Arena *arena, int gpu, uint64_t token) : arena_(arena), gpu_(gpu), token_(token) {}
 
 DataServer::~DataServer() { stop(); }
 
@@ -81,7 +83,10 @@ void DataServer::serve(int fd) {
     }
     std::vector<char> sink;
     NetReq q;
-    while (!stop_ && recv_all(fd, &q, sizeof(q)) == 1) {
+    uint64_t tok = 0;
+    const bool authed = recv_all(fd, &tok, sizeof(tok)) == 1 && tok == token_;
+    if (!authed) OCM_WARN("data server: dropping a connection without the owner's token");
+    while (authed && !stop_ && recv_all(fd, &q, sizeof(q)) == 1) {
         NetResp r{kNetMagic, 0, q.len};
         if (q.magic != kNetMagic) break;
         void *mem = nullptr;

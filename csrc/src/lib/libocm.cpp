@@ -51,6 +51,7 @@ struct Extent {
     bool dev_ok = false;   // a kernel on this process's GPU can access dptr
     bool net = false;      // owner on another node: streamed through its data server
     std::string ep;        // "ip:port" of that data server
+    uint64_t net_token = 0;  // presented first on each connection to it
 };
 
 }  // namespace
@@ -225,11 +226,13 @@ int import_extent(Extent &e) {
         std::memcpy(buf, r.handle, 64);
         char host[64] = {0};
         int port = 0;
-        if (std::sscanf(buf, "net:%63[^:]:%d", host, &port) != 2 || port <= 0)
-            OCM_FAIL(-1, "bad network-tier handle '%s'", buf);
+        unsigned long long tok = 0;
+        if (std::sscanf(buf, "net:%63[^:]:%d:%llx", host, &port, &tok) != 3 || port <= 0)
+            OCM_FAIL(-1, "bad network-tier handle");
         e.net = true;
         e.dev_ok = false;
         e.ep = std::string(host) + ":" + std::to_string(port);
+        e.net_token = tok;
         return 0;
     }
     SlabKey key{r.owner_rank, r.tier, r.slab_id};
@@ -508,13 +511,17 @@ int service_xfer(XferArgs x) {
 
 // ---- network tier client ----
 
-int net_conn(const std::string &ep) {
+int net_conn(const std::string &ep, uint64_t token) {
     State &s = S();
     auto it = s.net_conns.find(ep);
     if (it != s.net_conns.end()) return it->second;
     const size_t colon = ep.rfind(':');
     int fd = tcp_connect(ep.substr(0, colon), std::atoi(ep.c_str() + colon + 1), 10000);
     if (fd < 0) OCM_FAIL(-1, "cannot reach data server %s", ep.c_str());
+    if (send_all(fd, &token, sizeof(token)) != 1) {
+        close(fd);
+        OCM_FAIL(-1, "data server %s refused the connection", ep.c_str());
+    }
     s.net_conns[ep] = fd;
     return fd;
 }
@@ -531,7 +538,7 @@ void net_drop(const std::string &ep) {
 // local memory is staged through a pinned buffer, kNetChunk at a time.
 int net_piece(const Extent &e, bool put, char *lin, Loc lloc, uint64_t ext_off, uint64_t len) {
     State &s = S();
-    int fd = net_conn(e.ep);
+    int fd = net_conn(e.ep, e.net_token);
     if (fd < 0) return -1;
     NetReq q{kNetMagic, put ? (uint32_t)NET_PUT : (uint32_t)NET_GET, e.r.slab_id, e.r.tier, e.r.offset + ext_off, len};
     const bool dev = lloc == LOC_DEVICE;

@@ -123,3 +123,61 @@ def test_other_users_are_refused(mesh_factory):
     assert r.stdout.strip() == "closed", r.stdout + r.stderr
     assert "refusing mailbox connection" in m.logs()
     assert m.daemons[0].alive()
+
+
+def test_mesh_port_rejects_strangers(mesh_factory):
+    # The daemon<->daemon TCP port: without a HELLO carrying the mesh token
+    # nothing is processed - not even SHUTDOWN.
+    m = mesh_factory(2)
+    port = m.ports[0]
+    rng = random.Random(7)
+    for attempt in range(3):
+        s = socket.create_connection(("127.0.0.1", port), timeout=5)
+        if attempt == 0:
+            recs = [MSG.pack(SHUTDOWN, 1, 0, 0, 0, 1, 0, bytes(128))]
+        elif attempt == 1:
+            recs = [MSG.pack(12, 1, 0, 1, 0xBAD, 1, 0, bytes(128)), MSG.pack(SHUTDOWN, 1, 0, 0, 0, 1, 0, bytes(128))]
+        else:
+            recs = [os.urandom(160) for _ in range(50)]
+        for r in recs:
+            try:
+                s.sendall(r)
+            except OSError:
+                break
+        s.settimeout(5)
+        try:
+            assert s.recv(160) == b""  # dropped
+        except ConnectionResetError:
+            pass
+        s.close()
+    time.sleep(0.2)
+    assert all(d.alive() for d in m.daemons), m.logs()[-3000:]
+    assert "dropping unauthenticated mesh link" in m.logs()
+    with api.Client(daemon_rank=1, ns=m.ns) as c:  # the real mesh still works
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20)
+        assert a.remote_info()["extents"][0]["owner_rank"] == 0
+        a.free()
+
+
+def test_data_server_requires_token(mesh_factory):
+    m = mesh_factory(2, rank_env={0: {"OCM_HOST_ALIAS": "A"}, 1: {"OCM_HOST_ALIAS": "B"}})
+    port = m.ready_info()[1]["data_port"]
+    assert port > 0
+    s = socket.create_connection(("127.0.0.1", port), timeout=5)
+    get = struct.pack("<IIIIQQ", 0x4F434E44, 2, 1, 1, 0, 4096)  # a well-formed GET, but no token first
+    s.sendall(get)
+    try:
+        assert s.recv(64) == b""
+    except ConnectionResetError:
+        pass
+    s.close()
+    # apps get the token with the handle from their own daemon: the network tier works
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)
+        assert a.remote_info()["extents"][0]["net"]
+        a.fill(seed=3)
+        a.put(0, 0, 1 << 20)
+        a.fill(seed=0)
+        a.get(0, 0, 1 << 20)
+        assert a.check(seed=3) == 0
+        a.free()
