@@ -149,6 +149,19 @@ int ocm_copy_onesided_batch(ocm_alloc_t a, const struct ocm_params *ops, int n_o
  * ocm_stream_signal: work queued on `stream` afterwards starts after a's queued async ops. */
 int ocm_stream_wait(ocm_alloc_t a, void *stream);
 int ocm_stream_signal(ocm_alloc_t a, void *stream);
+
+/* Transfer plans: a fixed sequence of batch stages (each stage = one
+ * ocm_copy_onesided_batch list on one allocation, run after the previous
+ * stage), validated, planned and uploaded once, then captured into a HIP
+ * graph. Every ocm_plan_launch replays the whole schedule as one graph launch
+ * (data is read at replay time; the op lists are fixed). stream NULL: the
+ * library stream, blocking; otherwise queued on `stream` (hipStream_t).
+ * Allocations used by a plan cannot be freed before ocm_plan_destroy. */
+typedef struct ocm_plan *ocm_plan_t;
+ocm_plan_t ocm_plan_create(void);
+int ocm_plan_add(ocm_plan_t p, ocm_alloc_t a, const struct ocm_params *ops, int n_ops);
+int ocm_plan_launch(ocm_plan_t p, void *stream);
+int ocm_plan_destroy(ocm_plan_t p);
 int ocm_remote_info(ocm_alloc_t a, struct ocm_remote_info *info);
 /* Device pointer of the remote half when it is a single extent (NULL if striped). */
 void *ocm_remotebuf(ocm_alloc_t a);

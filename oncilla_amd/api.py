@@ -153,6 +153,10 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_wait": (i32, [vp]),
             "ocm_copy_onesided_batch": (i32, [vp, ctypes.POINTER(OcmParams), i32, i32]),
             "ocm_stream_wait": (i32, [vp, vp]),
+            "ocm_plan_create": (vp, []),
+            "ocm_plan_add": (i32, [vp, vp, ctypes.POINTER(OcmParams), i32]),
+            "ocm_plan_launch": (i32, [vp, vp]),
+            "ocm_plan_destroy": (i32, [vp]),
             "ocm_stream_signal": (i32, [vp, vp]),
             "ocm_remote_info": (i32, [vp, ctypes.POINTER(OcmRemoteInfo)]),
             "ocm_remotebuf": (vp, [vp]),
@@ -184,6 +188,45 @@ def last_error() -> str:
 COUNTER_KEYS = ["n_put", "n_get", "bytes_put", "bytes_get", "n_alloc", "n_free", "n_copy", "bytes_copy", "ns_put",
                 "ns_get", "ns_alloc", "ns_free", "n_batch", "n_batch_ops", "bytes_batch", "ns_batch"]
 OCM_BATCH_ASYNC = 1
+
+
+class Plan:
+    """A fixed transfer schedule replayed as one HIP graph launch (ocm_plan_*).
+
+    plan.add(alloc, ops) appends a stage (ops as for Allocation.batch); stages run in order.
+    plan.launch() blocks; plan.launch(stream) queues on a torch stream / hipStream_t handle.
+    """
+
+    def __init__(self, client: "Client"):
+        self._c = client
+        self.handle = client.lib.ocm_plan_create()
+        if not self.handle:
+            raise OcmError("ocm_plan_create: " + last_error())
+        self._keep = []
+
+    def add(self, alloc: "Allocation", ops) -> "Plan":
+        arr = ops if isinstance(ops, BatchOps) else batch_ops(ops)
+        if self._c.lib.ocm_plan_add(self.handle, alloc.handle, arr.array, arr.n) != 0:
+            raise OcmError("ocm_plan_add: " + last_error())
+        return self
+
+    def launch(self, stream=None) -> None:
+        h = None
+        if stream is not None:
+            h = ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        if self._c.lib.ocm_plan_launch(self.handle, h) != 0:
+            raise OcmError("ocm_plan_launch: " + last_error())
+
+    def close(self) -> None:
+        if self.handle:
+            self._c.lib.ocm_plan_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self) -> "Plan":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
 
 
 class BatchOps:
@@ -460,6 +503,10 @@ class Client:
     @property
     def device(self) -> int:
         return int(self.lib.ocm_device())
+
+    def plan(self) -> Plan:
+        """A new transfer plan (hipGraph replay of fixed batch schedules)."""
+        return Plan(self)
 
     def alloc(self, kind: int, local_bytes: int = 0, remote_bytes: int = 0, remote_rank: int = -1, flags: int = 0,
               stripe_width: int = 0, stripe_unit: int = 0) -> Allocation:

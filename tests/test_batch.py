@@ -127,3 +127,63 @@ def test_batch_host_tier_gpu(mesh_factory):
         assert a.remote_info()["extents"][0]["tier"] == api.OCM_TIER_HOST
         run_batch_check(a, n, 300, 5000, seed=7)
         a.free()
+
+
+def test_plan_needs_gpu(mesh_factory, cpu_app):
+    m = mesh_factory(1)
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        with pytest.raises(api.OcmError):
+            c.plan()
+
+
+@pytest.mark.gpu
+def test_plan_graph_replay(mesh_factory):
+    # Two pairs, a 3-stage schedule (gather from A, scatter to B, a large-list
+    # stage on A) captured once and replayed with fresh data each time.
+    m = mesh_factory(4, gpus=[0, 0, 0, 0], policy="stripe")
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 8 << 20
+        A = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, stripe_unit=64 << 10)
+        B = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, stripe_unit=64 << 10)
+        rng = np.random.default_rng(11)
+        piece = 4096
+        slots = n // piece
+        gather = [(0, i * piece, int(r) * piece, piece) for i, r in enumerate(rng.choice(slots, 40, replace=False))]
+        scatter = [(1, i * piece, int(r) * piece, piece) for i, r in enumerate(rng.choice(slots, 40, replace=False))]
+        big = [(1, (100 + i) * piece, int(r) * piece, piece) for i, r in enumerate(rng.choice(slots, 900, replace=False))]
+        plan = c.plan().add(A, gather).add(B, scatter).add(A, big)
+        for rep in range(3):
+            a_rem = rng.integers(0, 256, n, dtype=np.uint8)
+            A.local_tensor(torch.uint8).copy_(torch.from_numpy(a_rem).cuda())
+            torch.cuda.synchronize()
+            A.put(0, 0, n)
+            a_loc = rng.integers(0, 256, n, dtype=np.uint8)
+            b_loc = rng.integers(0, 256, n, dtype=np.uint8)
+            A.local_tensor(torch.uint8).copy_(torch.from_numpy(a_loc).cuda())
+            B.local_tensor(torch.uint8).copy_(torch.from_numpy(b_loc).cuda())
+            torch.cuda.synchronize()
+            B.put(0, 0, n)
+            b_rem = b_loc.copy()
+            # model
+            for _, lo, ro, k in gather:
+                a_loc[lo:lo + k] = a_rem[ro:ro + k]
+            for _, lo, ro, k in scatter:
+                b_rem[ro:ro + k] = b_loc[lo:lo + k]
+            for _, lo, ro, k in big:
+                a_rem[ro:ro + k] = a_loc[lo:lo + k]
+            if rep == 1:
+                s = torch.cuda.Stream()
+                plan.launch(s)
+                s.synchronize()
+            else:
+                plan.launch()
+            assert np.array_equal(A.local_tensor(torch.uint8).cpu().numpy(), a_loc), rep
+            A.get(0, 0, n)
+            assert np.array_equal(A.local_tensor(torch.uint8).cpu().numpy(), a_rem), rep
+            B.get(0, 0, n)
+            assert np.array_equal(B.local_tensor(torch.uint8).cpu().numpy(), b_rem), rep
+        with pytest.raises(api.OcmError):
+            A.free()  # still used by the plan
+        plan.close()
+        A.free()
+        B.free()

@@ -33,6 +33,17 @@ def measure(a, nbytes, piece, count, reps=5):
         a.batch(prepared)
         t.append(time.perf_counter() - t0)
     batch_s = float(np.median(t))
+    plan_s = None
+    if a._c.device >= 0:
+        with a._c.plan() as plan:  # the same list as a captured graph: no per-call planning/upload
+            plan.add(a, prepared)
+            plan.launch()
+            tp = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                plan.launch()
+                tp.append(time.perf_counter() - t0)
+            plan_s = float(np.median(tp))
     loop_ops = ops[: min(count, 2000)]
     for f, lo, ro, n in loop_ops[:10]:
         a.get(lo, ro, n)
@@ -43,7 +54,9 @@ def measure(a, nbytes, piece, count, reps=5):
     moved = piece * count
     return {"piece": piece, "count": count, "batch_us": round(batch_s * 1e6, 1), "loop_us": round(loop_s * 1e6, 1),
             "batch_GiBps": round(moved / batch_s / 2**30, 2), "loop_GiBps": round(moved / loop_s / 2**30, 3),
-            "speedup": round(loop_s / batch_s, 1)}
+            "speedup": round(loop_s / batch_s, 1),
+            "plan_us": round(plan_s * 1e6, 1) if plan_s else None,
+            "plan_GiBps": round(moved / plan_s / 2**30, 2) if plan_s else None}
 
 
 def run(mesh_n, label, out):
