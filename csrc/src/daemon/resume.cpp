@@ -1,0 +1,125 @@
+// ocmd checkpoint / resume: mesh HELLO, the join report (ADD_NODE + OWNED
+// extents), survivors reconnecting to a restarted rank0, and rank0's
+// directory checkpoint.
+#include "ocm/daemon.h"
+
+#include <fcntl.h>
+#include <hip/hip_runtime_api.h>
+#include <signal.h>
+#include <sys/epoll.h>
+#include <sys/signalfd.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+#include "../../include/oncillamem.h"
+#include "ocm/log.h"
+#include "ocm/trace.h"
+#include "util.h"
+
+namespace ocm {
+using namespace dm;
+
+void Daemon::send_hello(int fd) {
+    Msg hello;
+    std::memset(&hello, 0, sizeof(hello));
+    hello.type = MSG_HELLO;
+    hello.src_rank = rank_;
+    hello.rank = rank_;
+    hello.seq = mesh_token_;
+    send_all(fd, &hello, sizeof(hello));
+}
+
+void Daemon::join_rank0() {
+    Msg add;
+    std::memset(&add, 0, sizeof(add));
+    add.type = MSG_ADD_NODE;
+    add.status = MSG_REQUEST;
+    add.rank = rank_;
+    add.seq = boot_id_;
+    add.u.node = my_config();
+    send_rank(0, add);
+    // What we hold (empty on first boot): lets a restarted rank0 rebuild its directory.
+    for (auto &kv : owned_) {
+        const OwnedExtent &oe = kv.second;
+        Msg o;
+        std::memset(&o, 0, sizeof(o));
+        o.type = MSG_OWNED;
+        o.status = MSG_REQUEST;
+        o.rank = rank_;
+        o.pid = oe.app_pid;
+        Region &rg = o.u.region;
+        rg.alloc_id = kv.first.first;
+        rg.extent_idx = (uint16_t)kv.first.second;
+        rg.n_extents = oe.n_extents;
+        rg.bytes = oe.bytes;
+        rg.offset = oe.offset;
+        rg.slab_id = oe.slab_id;
+        rg.stripe_unit = oe.stripe_unit;
+        rg.owner_rank = rank_;
+        rg.orig_rank = oe.orig_rank;
+        rg.tier = (uint16_t)oe.tier;
+        rg.flags = oe.flags;
+        send_rank(0, o);
+    }
+    Msg done;
+    std::memset(&done, 0, sizeof(done));
+    done.type = MSG_OWNED_DONE;
+    done.status = MSG_REQUEST;
+    done.rank = rank_;
+    done.seq = owned_.size();
+    send_rank(0, done);
+}
+
+void Daemon::try_rejoin_rank0() {
+    const long now = now_ms();
+    if (now < next_rejoin_ms_) return;
+    next_rejoin_ms_ = now + 100;
+    const NodeEntry &ne = nf_.nodes[0];
+    int fd = tcp_connect(ne.ip, ne.ocm_port, 50);
+    if (fd < 0) return;
+    send_hello(fd);
+    set_nonblocking(fd, true);
+    auto c = std::make_unique<Conn>();
+    c->fd = fd;
+    c->peer_rank = 0;
+    peer_fd_[0] = fd;
+    ep_add(fd, EPOLLIN, tag(T_CONN, (uint64_t)fd));
+    conns_[fd] = std::move(c);
+    r0_lost_ = false;
+    OCM_INFO("rank %d: reconnected to rank 0; reporting %zu owned extents", rank_, owned_.size());
+    join_rank0();
+}
+
+void Daemon::save_checkpoint(bool force) {
+    if (!gov_ || cfg_.state_file.empty()) return;
+    const uint64_t v = gov_->version();
+    if (v == saved_version_) return;
+    const long now = now_ms();
+    if (!force && now - last_save_ms_ < cfg_.state_interval_ms) return;
+    const std::string tmp = cfg_.state_file + ".tmp";
+    {
+        std::ofstream f(tmp, std::ios::trunc);
+        f << gov_->checkpoint();
+        if (!f) {
+            OCM_WARN("rank 0: cannot write directory checkpoint %s", tmp.c_str());
+            return;
+        }
+    }
+    if (rename(tmp.c_str(), cfg_.state_file.c_str()) != 0) {
+        OCM_WARN("rank 0: cannot publish directory checkpoint %s: %s", cfg_.state_file.c_str(), strerror(errno));
+        return;
+    }
+    saved_version_ = v;
+    last_save_ms_ = now;
+}
+
+
+}  // namespace ocm

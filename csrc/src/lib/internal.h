@@ -1,0 +1,222 @@
+// libocm internals shared by the library's translation units (not installed).
+//
+// runtime.cpp  process state, mailbox RPC, IPC/memfd import cache, local halves
+// transfer.cpp copy engine: segments, lanes/events, copy service, xfer, local copies
+// net.cpp      network-tier client (owners on other nodes)
+// batch.cpp    batched one-sided ops, stream interop, transfer plans (hipGraph)
+// libocm.cpp   the C ABI (oncillamem.h)
+#pragma once
+#include <fcntl.h>
+#include <hip/hip_runtime_api.h>
+#include <sys/mman.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "oncillamem.h"
+#include "ocm/log.h"
+#include "ocm/msg.h"
+#include "ocm/netdata.h"
+#include "ocm/pmsg.h"
+#include "ocm/sock.h"
+#include "ocm/trace.h"
+#include "ocm/xfer.h"
+
+
+namespace ocmlib {
+using namespace ocm;
+#pragma GCC visibility push(hidden)
+
+
+enum Loc { LOC_HOST = 0, LOC_PINNED = 1, LOC_DEVICE = 2 };
+
+struct Extent {
+    Region r;
+    char *dptr = nullptr;  // device-usable address of the extent start (nullptr: none)
+    char *hptr = nullptr;  // host address (host tier only)
+    bool dev_ok = false;   // a kernel on this process's GPU can access dptr
+    bool net = false;      // owner on another node: streamed through its data server
+    std::string ep;        // "ip:port" of that data server
+    uint64_t net_token = 0;  // presented first on each connection to it
+};
+
+
+}  // namespace ocmlib
+
+struct lib_alloc {
+    enum ocm_kind kind;
+    uint64_t alloc_id = 0;
+    void *local = nullptr;
+    size_t local_bytes = 0;
+    ocmlib::Loc loc = ocmlib::LOC_HOST;
+    bool remote = false;
+    size_t remote_bytes = 0;
+    uint64_t stripe_unit = 0;
+    std::vector<ocmlib::Extent> ext;
+    bool all_gpu = false;
+    bool any_gpu = false;
+    bool all_dev_ok = false;  // every extent reachable by a kernel on this GPU
+    bool any_net = false;     // some extent lives on another node
+    bool async_pending = false;
+    bool pooled = false;      // local half from the stream-ordered pool
+    int lane = -1;            // async ops: index into State::lanes (per-allocation ordering)
+    hipEvent_t ev = nullptr;  // completion of the last async op (ocm_wait)
+    void *batch_dev = nullptr;  // device copy of large batch descriptor lists
+    void *batch_host = nullptr; // pinned staging for their upload
+    size_t batch_cap = 0;
+    hipEvent_t batch_up = nullptr;  // the last upload out of batch_host finished
+    hipEvent_t dep_ev = nullptr;    // ocm_stream_wait: external work the next op depends on
+    bool dep_pending = false;
+    int plans = 0;                  // ocm_plan stages that reference this allocation
+};
+
+struct ocm_plan {
+    struct Stage {
+        lib_alloc *a = nullptr;
+        ocm::XferBatchArgs args;
+        void *dev = nullptr;  // descriptors + wave table (large lists)
+    };
+    std::vector<Stage> stages;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    uint64_t bytes = 0, n_ops = 0;
+};
+
+
+namespace ocmlib {
+
+struct SlabKey {
+    int owner;
+    uint32_t tier;
+    uint32_t slab;
+    bool operator<(const SlabKey &o) const {
+        return owner != o.owner ? owner < o.owner : tier != o.tier ? tier < o.tier : slab < o.slab;
+    }
+};
+
+struct Mapping {
+    char *dbase = nullptr;
+    char *hbase = nullptr;
+    uint64_t bytes = 0;
+    uint8_t handle[kHandleBytes] = {};
+    int refs = 0;
+    bool dedicated = false;
+    bool registered = false;
+};
+
+struct State {
+    std::recursive_mutex mu;
+    bool inited = false;
+    pid_t pid = 0;
+    std::string ns, daemon_mbox;
+    Channel chan;
+    NodeConfig daemon{};
+    int daemon_rank = 0;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint64_t seq = 0;
+    std::map<SlabKey, Mapping> imports;
+    std::set<lib_alloc *> allocs;
+    XferTuning tuning;
+    bool host_engine_kernel = false;
+    uint64_t host_kernel_max = 0;  // measured: SDMA beats the kernel on registered host slabs
+    int sync_mode = 0;             // 0 stream sync, 1 spin on an event, 2 blocking event sync
+    OpCounters ctr;
+    // persistent copy service (small blocking one-sided ops)
+    ServiceSlot *svc = nullptr;
+    hipStream_t svc_stream = nullptr;
+    bool svc_running = false;
+    unsigned long long svc_seq = 0;
+    uint64_t svc_max = 128ull << 10;  // measured: launches win above ~128 KiB
+    unsigned long long svc_idle_ticks = 200000ull;  // 2 ms at 100 MHz: live only during bursts of small ops
+    // network tier
+    std::map<std::string, int> net_conns;  // "ip:port" -> connected socket
+    void *net_stage = nullptr;             // pinned staging buffer (device-side local halves)
+    // Local GPU halves: stream-ordered pool (no device-wide sync in free, freed
+    // blocks reused without a new VA mapping). Reference K8: cudaMalloc/cudaFree.
+    hipMemPool_t pool = nullptr;
+    // Async one-sided ops run on lane streams, one lane per allocation (round
+    // robin), so ops on different allocations (different peers / links) overlap.
+    std::vector<hipStream_t> lanes;
+    int n_lanes = 4, next_lane = 0;
+    bool pool_tried = false;
+    uint64_t pool_keep = 8ull << 30;       // bytes kept reserved across frees
+    hipEvent_t done = nullptr;
+    int rpc_timeout_ms = 60000;
+};
+
+State &S();
+int env_int(const char *k, int dflt);
+long now_ms();
+Msg new_msg(uint32_t type);
+// Send a request and wait for the reply carrying the same seq.
+int rpc(Msg &req, Msg *reply, int timeout_ms);
+int recv_seq(Msg *m, uint64_t seq, uint32_t type, int timeout_ms);
+bool is_pair(enum ocm_kind k);
+
+struct DeviceGuard {
+    int prev = -1;
+    bool active = false;
+    explicit DeviceGuard(int dev) {
+        if (dev < 0) return;
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
+            (void)hipSetDevice(dev);
+            active = true;
+        }
+    }
+    ~DeviceGuard() {
+        if (active) (void)hipSetDevice(prev);
+    }
+};
+
+inline int log2_exact(uint64_t v) {
+    if (v == 0 || (v & (v - 1))) return -1;
+    return __builtin_ctzll(v);
+}
+
+// ---- import cache (runtime.cpp)
+int import_extent(Extent &e);
+void release_extent(const Extent &e, bool force);
+
+// ---- local halves (runtime.cpp)
+Loc pointer_loc(const void *p);
+hipMemPool_t local_pool();
+int free_local_half(lib_alloc *a);
+int alloc_local_half(lib_alloc *a, size_t bytes, Loc want);
+
+// ---- copy engine (transfer.cpp)
+struct Seg {
+    int ext;
+    uint64_t ext_off;
+    uint64_t lin_off;
+    uint64_t len;
+};
+void segments(const lib_alloc *a, uint64_t rem_off, uint64_t len, std::vector<Seg> &out);
+int wait_event(hipEvent_t ev);
+int honor_dep(lib_alloc *a, hipStream_t st, bool host_wait);
+int wait_alloc(lib_alloc *a);
+hipStream_t lane_stream(lib_alloc *a);
+int sync_stream();
+int service_start(unsigned long long first_seq);
+void service_park();
+void service_stop();
+int service_xfer(XferArgs x);
+int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async);
+int copy_local(void *dst, Loc dl, const void *src, Loc sl, size_t n);
+
+// ---- network tier (net.cpp)
+int net_conn(const std::string &ep, uint64_t token);
+void net_drop(const std::string &ep);
+int net_piece(const Extent &e, bool put, char *lin, Loc lloc, uint64_t ext_off, uint64_t len);
+
+#pragma GCC visibility pop
+}  // namespace ocmlib

@@ -13,853 +13,10 @@
 // Reference defects deliberately not reproduced: inverted ocm_is_remote
 // (src/lib.c:461), NULL deref before check in ocm_free (:357-359), stub
 // copy_in/out (:491-499), swapped GPU->RMA offsets (:654).
-#include <fcntl.h>
-#include <hip/hip_runtime_api.h>
-#include <sys/mman.h>
-#include <time.h>
-#include <unistd.h>
-
-#include <algorithm>
-#include <cerrno>
-#include <cstdlib>
-#include <cstring>
-#include <map>
-#include <mutex>
-#include <set>
-#include <string>
-#include <vector>
-
-#include "oncillamem.h"
-#include "ocm/log.h"
-#include "ocm/msg.h"
-#include "ocm/netdata.h"
-#include "ocm/pmsg.h"
-#include "ocm/sock.h"
-#include "ocm/trace.h"
-#include "ocm/xfer.h"
+#include "internal.h"
 
 using namespace ocm;
-
-namespace {
-
-enum Loc { LOC_HOST = 0, LOC_PINNED = 1, LOC_DEVICE = 2 };
-
-struct Extent {
-    Region r;
-    char *dptr = nullptr;  // device-usable address of the extent start (nullptr: none)
-    char *hptr = nullptr;  // host address (host tier only)
-    bool dev_ok = false;   // a kernel on this process's GPU can access dptr
-    bool net = false;      // owner on another node: streamed through its data server
-    std::string ep;        // "ip:port" of that data server
-    uint64_t net_token = 0;  // presented first on each connection to it
-};
-
-}  // namespace
-
-struct lib_alloc {
-    enum ocm_kind kind;
-    uint64_t alloc_id = 0;
-    void *local = nullptr;
-    size_t local_bytes = 0;
-    Loc loc = LOC_HOST;
-    bool remote = false;
-    size_t remote_bytes = 0;
-    uint64_t stripe_unit = 0;
-    std::vector<Extent> ext;
-    bool all_gpu = false;
-    bool any_gpu = false;
-    bool all_dev_ok = false;  // every extent reachable by a kernel on this GPU
-    bool any_net = false;     // some extent lives on another node
-    bool async_pending = false;
-    bool pooled = false;      // local half from the stream-ordered pool
-    int lane = -1;            // async ops: index into State::lanes (per-allocation ordering)
-    hipEvent_t ev = nullptr;  // completion of the last async op (ocm_wait)
-    void *batch_dev = nullptr;  // device copy of large batch descriptor lists
-    void *batch_host = nullptr; // pinned staging for their upload
-    size_t batch_cap = 0;
-    hipEvent_t batch_up = nullptr;  // the last upload out of batch_host finished
-    hipEvent_t dep_ev = nullptr;    // ocm_stream_wait: external work the next op depends on
-    bool dep_pending = false;
-    int plans = 0;                  // ocm_plan stages that reference this allocation
-};
-
-struct ocm_plan {
-    struct Stage {
-        lib_alloc *a = nullptr;
-        ocm::XferBatchArgs args;
-        void *dev = nullptr;  // descriptors + wave table (large lists)
-    };
-    std::vector<Stage> stages;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-    uint64_t bytes = 0, n_ops = 0;
-};
-
-namespace {
-
-struct SlabKey {
-    int owner;
-    uint32_t tier;
-    uint32_t slab;
-    bool operator<(const SlabKey &o) const {
-        return owner != o.owner ? owner < o.owner : tier != o.tier ? tier < o.tier : slab < o.slab;
-    }
-};
-
-struct Mapping {
-    char *dbase = nullptr;
-    char *hbase = nullptr;
-    uint64_t bytes = 0;
-    uint8_t handle[kHandleBytes] = {};
-    int refs = 0;
-    bool dedicated = false;
-    bool registered = false;
-};
-
-struct State {
-    std::recursive_mutex mu;
-    bool inited = false;
-    pid_t pid = 0;
-    std::string ns, daemon_mbox;
-    Channel chan;
-    NodeConfig daemon{};
-    int daemon_rank = 0;
-    int device = -1;
-    hipStream_t stream = nullptr;
-    uint64_t seq = 0;
-    std::map<SlabKey, Mapping> imports;
-    std::set<lib_alloc *> allocs;
-    XferTuning tuning;
-    bool host_engine_kernel = false;
-    uint64_t host_kernel_max = 0;  // measured: SDMA beats the kernel on registered host slabs
-    int sync_mode = 0;             // 0 stream sync, 1 spin on an event, 2 blocking event sync
-    OpCounters ctr;
-    // persistent copy service (small blocking one-sided ops)
-    ServiceSlot *svc = nullptr;
-    hipStream_t svc_stream = nullptr;
-    bool svc_running = false;
-    unsigned long long svc_seq = 0;
-    uint64_t svc_max = 128ull << 10;  // measured: launches win above ~128 KiB
-    unsigned long long svc_idle_ticks = 200000ull;  // 2 ms at 100 MHz: live only during bursts of small ops
-    // network tier
-    std::map<std::string, int> net_conns;  // "ip:port" -> connected socket
-    void *net_stage = nullptr;             // pinned staging buffer (device-side local halves)
-    // Local GPU halves: stream-ordered pool (no device-wide sync in free, freed
-    // blocks reused without a new VA mapping). Reference K8: cudaMalloc/cudaFree.
-    hipMemPool_t pool = nullptr;
-    // Async one-sided ops run on lane streams, one lane per allocation (round
-    // robin), so ops on different allocations (different peers / links) overlap.
-    std::vector<hipStream_t> lanes;
-    int n_lanes = 4, next_lane = 0;
-    bool pool_tried = false;
-    uint64_t pool_keep = 8ull << 30;       // bytes kept reserved across frees
-    hipEvent_t done = nullptr;
-    int rpc_timeout_ms = 60000;
-};
-
-State &S() {
-    static State *s = new State();  // never destroyed: safe at process exit
-    return *s;
-}
-
-int env_int(const char *k, int dflt) {
-    const char *v = std::getenv(k);
-    return (v && *v) ? std::atoi(v) : dflt;
-}
-
-struct DeviceGuard {
-    int prev = -1;
-    bool active = false;
-    explicit DeviceGuard(int dev) {
-        if (dev < 0) return;
-        if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
-            (void)hipSetDevice(dev);
-            active = true;
-        }
-    }
-    ~DeviceGuard() {
-        if (active) (void)hipSetDevice(prev);
-    }
-};
-
-long now_ms() {
-    struct timespec ts;
-    clock_gettime(CLOCK_MONOTONIC, &ts);
-    return ts.tv_sec * 1000L + ts.tv_nsec / 1000000L;
-}
-
-Msg new_msg(uint32_t type) {
-    Msg m;
-    std::memset(&m, 0, sizeof(m));
-    m.type = type;
-    m.status = MSG_REQUEST;
-    m.pid = S().pid;
-    m.rank = S().daemon_rank;
-    m.src_rank = -1;
-    return m;
-}
-
-// Send a request and wait for the reply carrying the same seq.
-int rpc(Msg &req, Msg *reply, int timeout_ms) {
-    State &s = S();
-    req.seq = ++s.seq;
-    if (s.chan.send(&req, kMsgBytes, timeout_ms) != 1) OCM_FAIL(-1, "mailbox send to daemon failed");
-    const long deadline = now_ms() + timeout_ms;
-    for (;;) {
-        long left = deadline - now_ms();
-        if (left <= 0) OCM_FAIL(-1, "daemon did not answer %s within %d ms", msg_type_str(req.type), timeout_ms);
-        int rc = s.chan.recv(reply, kMsgBytes, (int)std::min<long>(left, 1000));
-        if (rc < 0) return -1;
-        if (rc == 0) continue;
-        if (reply->seq == req.seq && reply->type != MSG_EXTENT) return 0;
-        OCM_LOG("dropping stale reply %s seq %llu", msg_type_str(reply->type), (unsigned long long)reply->seq);
-    }
-}
-
-int recv_seq(Msg *m, uint64_t seq, uint32_t type, int timeout_ms) {
-    const long deadline = now_ms() + timeout_ms;
-    for (;;) {
-        long left = deadline - now_ms();
-        if (left <= 0) OCM_FAIL(-1, "timed out waiting for %s", msg_type_str(type));
-        int rc = S().chan.recv(m, kMsgBytes, (int)std::min<long>(left, 1000));
-        if (rc < 0) return -1;
-        if (rc == 1 && m->seq == seq && m->type == type) return 0;
-    }
-}
-
-bool is_pair(enum ocm_kind k) { return k == OCM_REMOTE_GPU || k == OCM_REMOTE_RDMA || k == OCM_REMOTE_RMA; }
-
-// ---------------------------------------------------------------- import cache
-
-int import_extent(Extent &e) {
-    State &s = S();
-    const Region &r = e.r;
-    if (r.flags & REGION_NET) {
-        char buf[65] = {0};
-        std::memcpy(buf, r.handle, 64);
-        char host[64] = {0};
-        int port = 0;
-        unsigned long long tok = 0;
-        if (std::sscanf(buf, "net:%63[^:]:%d:%llx", host, &port, &tok) != 3 || port <= 0)
-            OCM_FAIL(-1, "bad network-tier handle");
-        e.net = true;
-        e.dev_ok = false;
-        e.ep = std::string(host) + ":" + std::to_string(port);
-        e.net_token = tok;
-        return 0;
-    }
-    SlabKey key{r.owner_rank, r.tier, r.slab_id};
-    auto it = s.imports.find(key);
-    if (it != s.imports.end() && std::memcmp(it->second.handle, r.handle, kHandleBytes) != 0) {
-        // Same id, different export: the owner restarted. Drop the stale mapping.
-        Mapping &m = it->second;
-        if (r.tier == TIER_GPU && m.dbase) (void)hipIpcCloseMemHandle(m.dbase);
-        if (m.registered) (void)hipHostUnregister(m.hbase);
-        if (m.hbase) munmap(m.hbase, m.bytes);
-        s.imports.erase(it);
-        it = s.imports.end();
-    }
-    if (it == s.imports.end()) {
-        Mapping m;
-        m.bytes = r.slab_bytes;
-        m.dedicated = (r.flags & REGION_DEDICATED) != 0;
-        std::memcpy(m.handle, r.handle, kHandleBytes);
-        if (r.tier == TIER_GPU) {
-            if (s.device < 0) OCM_FAIL(-1, "remote HBM extent but this process has no GPU");
-            DeviceGuard g(s.device);
-            hipIpcMemHandle_t h;
-            std::memcpy(&h, r.handle, sizeof(h));
-            void *p = nullptr;
-            hipError_t err = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-            if (err != hipSuccess) OCM_FAIL(-1, "hipIpcOpenMemHandle(owner %d slab %u): %s", r.owner_rank, r.slab_id, hipGetErrorString(err));
-            m.dbase = static_cast<char *>(p);
-        } else {
-            char path[kHandleBytes + 1];
-            std::memcpy(path, r.handle, kHandleBytes);
-            path[kHandleBytes] = 0;
-            int fd = open(path, O_RDWR | O_CLOEXEC);
-            if (fd < 0) OCM_FAIL(-1, "open host-tier slab %s: %s", path, strerror(errno));
-            void *p = mmap(nullptr, r.slab_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-            close(fd);
-            if (p == MAP_FAILED) OCM_FAIL(-1, "mmap host-tier slab: %s", strerror(errno));
-            m.hbase = static_cast<char *>(p);
-            m.dbase = m.hbase;
-            if (s.device >= 0) {
-                DeviceGuard g(s.device);
-                hipError_t err = hipHostRegister(p, r.slab_bytes, hipHostRegisterMapped | hipHostRegisterPortable);
-                if (err == hipSuccess) {
-                    void *dp = nullptr;
-                    if (hipHostGetDevicePointer(&dp, p, 0) == hipSuccess) m.dbase = static_cast<char *>(dp);
-                    m.registered = true;
-                } else {
-                    (void)hipGetLastError();
-                    OCM_WARN("hipHostRegister of host-tier slab failed: %s (DMA from pageable memory)", hipGetErrorString(err));
-                }
-            }
-        }
-        it = s.imports.emplace(key, m).first;
-    }
-    it->second.refs++;
-    e.dev_ok = r.tier == TIER_GPU || it->second.registered;
-    e.dptr = it->second.dbase + r.offset;
-    e.hptr = it->second.hbase ? it->second.hbase + r.offset : nullptr;
-    return 0;
-}
-
-void release_extent(const Extent &e, bool force) {
-    State &s = S();
-    if (e.net) return;
-    SlabKey key{e.r.owner_rank, e.r.tier, e.r.slab_id};
-    auto it = s.imports.find(key);
-    if (it == s.imports.end()) return;
-    Mapping &m = it->second;
-    if (--m.refs > 0 && !force) return;
-    if (!m.dedicated && !force) return;  // shared slabs stay mapped for reuse
-    DeviceGuard g(s.device);
-    if (e.r.tier == TIER_GPU && m.dbase) (void)hipIpcCloseMemHandle(m.dbase);
-    if (m.registered) (void)hipHostUnregister(m.hbase);
-    if (m.hbase) munmap(m.hbase, m.bytes);
-    s.imports.erase(it);
-}
-
-// ---------------------------------------------------------------- copy engine
-
-struct Seg {
-    int ext;
-    uint64_t ext_off;
-    uint64_t lin_off;
-    uint64_t len;
-};
-
-// Split [rem_off, rem_off+len) of a striped buffer into contiguous pieces.
-void segments(const lib_alloc *a, uint64_t rem_off, uint64_t len, std::vector<Seg> &out) {
-    out.clear();
-    const int n = (int)a->ext.size();
-    if (n == 1 || a->stripe_unit == 0) {
-        out.push_back({0, rem_off, 0, len});
-        return;
-    }
-    const uint64_t unit = a->stripe_unit;
-    uint64_t pos = rem_off, done = 0;
-    while (done < len) {
-        const uint64_t u = pos / unit, within = pos % unit;
-        const uint64_t take = std::min(unit - within, len - done);
-        out.push_back({(int)(u % n), (u / n) * unit + within, done, take});
-        pos += take;
-        done += take;
-    }
-}
-
-int log2_exact(uint64_t v) {
-    if (v == 0 || (v & (v - 1))) return -1;
-    return __builtin_ctzll(v);
-}
-
-int wait_event(hipEvent_t ev) {
-    State &s = S();
-    hipError_t e = hipSuccess;
-    if (s.sync_mode == 1) {
-        while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
-        }
-    } else {
-        e = hipEventSynchronize(ev);
-    }
-    if (e != hipSuccess) OCM_FAIL(-1, "event wait: %s", hipGetErrorString(e));
-    return 0;
-}
-
-// ocm_stream_wait dependency: order it before work on `st` (nullptr: the
-// copy service, which has no stream, so wait on the host).
-int honor_dep(lib_alloc *a, hipStream_t st, bool host_wait) {
-    if (!a->dep_pending) return 0;
-    a->dep_pending = false;
-    hipError_t e = host_wait ? hipEventSynchronize(a->dep_ev) : hipStreamWaitEvent(st, a->dep_ev, 0);
-    if (e != hipSuccess) OCM_FAIL(-1, "stream dependency: %s", hipGetErrorString(e));
-    return 0;
-}
-
-// Completion of `a`'s queued async ops (its lane up to the recorded event).
-int wait_alloc(lib_alloc *a) {
-    State &s = S();
-    if (!a || !a->async_pending) return 0;
-    a->async_pending = false;
-    if (!a->ev) return 0;
-    DeviceGuard g(s.device);
-    return wait_event(a->ev);
-}
-
-hipStream_t lane_stream(lib_alloc *a) {
-    State &s = S();
-    if (a->lane < 0) {
-        if (s.lanes.empty()) {
-            DeviceGuard g(s.device);
-            for (int i = 0; i < std::max(1, s.n_lanes); i++) {
-                hipStream_t st = nullptr;
-                if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
-                    (void)hipGetLastError();
-                    break;
-                }
-                s.lanes.push_back(st);
-            }
-        }
-        if (s.lanes.empty()) return s.stream;
-        a->lane = s.next_lane++ % (int)s.lanes.size();
-    }
-    if (!a->ev) {
-        DeviceGuard g(s.device);
-        if (hipEventCreateWithFlags(&a->ev, hipEventDisableTiming) != hipSuccess) {
-            (void)hipGetLastError();
-            a->ev = nullptr;
-            return s.stream;
-        }
-    }
-    return s.lanes[a->lane];
-}
-
-int sync_stream() {
-    State &s = S();
-    if (!s.stream) return 0;
-    DeviceGuard g(s.device);
-    hipError_t e = hipSuccess;
-    if (s.sync_mode == 0 || !s.done) {
-        e = hipStreamSynchronize(s.stream);
-    } else {
-        e = hipEventRecord(s.done, s.stream);
-        if (e == hipSuccess && s.sync_mode == 1) {
-            // Spin: lowest completion latency for small one-sided ops.
-            while ((e = hipEventQuery(s.done)) == hipErrorNotReady) {
-            }
-        } else if (e == hipSuccess) {
-            e = hipEventSynchronize(s.done);
-        }
-    }
-    if (e != hipSuccess) OCM_FAIL(-1, "stream sync: %s", hipGetErrorString(e));
-    return 0;
-}
-
-// ---- persistent copy service ----
-
-int service_start(unsigned long long first_seq) {
-    State &s = S();
-    DeviceGuard g(s.device);
-    if (!s.svc) {
-        if (hipHostMalloc(reinterpret_cast<void **>(&s.svc), sizeof(ServiceSlot),
-                          hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
-            (void)hipGetLastError();
-            s.svc = nullptr;
-            s.svc_max = 0;
-            OCM_FAIL(-1, "copy service: no coherent host memory");
-        }
-        std::memset(s.svc, 0, sizeof(ServiceSlot));
-        if (hipStreamCreateWithFlags(&s.svc_stream, hipStreamNonBlocking) != hipSuccess) {
-            (void)hipGetLastError();
-            s.svc_max = 0;
-            OCM_FAIL(-1, "copy service: no stream");
-        }
-    }
-    __atomic_store_n(&s.svc->exited, 0ull, __ATOMIC_RELEASE);
-    __atomic_store_n(&s.svc->seq, 0ull, __ATOMIC_RELEASE);  // clear a STOP left by a parked instance
-    if (service_launch(s.svc, first_seq, s.svc_idle_ticks, s.svc_stream) != hipSuccess) {
-        (void)hipGetLastError();
-        s.svc_max = 0;
-        OCM_FAIL(-1, "copy service launch failed");
-    }
-    s.svc_running = true;
-    return 0;
-}
-
-// Park the resident kernel: its doorbell polls cross PCIe and slow down
-// large DMA-engine transfers (measured: 53 -> 34 GiB/s on host-tier sweeps).
-void service_park() {
-    State &s = S();
-    if (!s.svc || !s.svc_running) return;
-    DeviceGuard g(s.device);
-    __atomic_store_n(&s.svc->seq, kServiceStop, __ATOMIC_RELEASE);
-    (void)hipStreamSynchronize(s.svc_stream);
-    s.svc_running = false;
-}
-
-void service_stop() {
-    State &s = S();
-    if (!s.svc) return;
-    DeviceGuard g(s.device);
-    if (s.svc_running) {
-        __atomic_store_n(&s.svc->seq, kServiceStop, __ATOMIC_RELEASE);
-        (void)hipStreamSynchronize(s.svc_stream);
-        s.svc_running = false;
-    }
-    (void)hipStreamDestroy(s.svc_stream);
-    (void)hipHostFree(s.svc);
-    s.svc = nullptr;
-    s.svc_stream = nullptr;
-}
-
-// Run one normalized transfer through the resident kernel and wait for it.
-int service_xfer(XferArgs x) {
-    State &s = S();
-    if (xfer_normalize(x) != hipSuccess) OCM_FAIL(-1, "invalid transfer");
-    const unsigned long long seq = ++s.svc_seq;
-    if (!s.svc_running && service_start(seq) != 0) return -1;
-    std::memcpy(&s.svc->args, &x, sizeof(x));
-    __atomic_store_n(&s.svc->seq, seq, __ATOMIC_RELEASE);
-    const uint64_t t0 = now_ns();
-    for (unsigned spins = 1;; spins++) {
-        if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
-        if ((spins & 1023) == 0) {
-            // The kernel leaves after idle_ticks without work; if it left before
-            // taking this request, start a new one at this seq.
-            const unsigned long long ex = __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE);
-            if (ex && ex <= seq) {
-                DeviceGuard g(s.device);
-                (void)hipStreamSynchronize(s.svc_stream);
-                s.svc_running = false;
-                if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
-                if (service_start(seq) != 0) return -1;
-                __atomic_store_n(&s.svc->seq, seq, __ATOMIC_RELEASE);  // start cleared the doorbell: re-post
-            }
-            if (now_ns() - t0 > 10ull * 1000000000ull) OCM_FAIL(-1, "copy service did not complete a transfer in 10 s");
-        }
-    }
-}
-
-// ---- network tier client ----
-
-int net_conn(const std::string &ep, uint64_t token) {
-    State &s = S();
-    auto it = s.net_conns.find(ep);
-    if (it != s.net_conns.end()) return it->second;
-    const size_t colon = ep.rfind(':');
-    int fd = tcp_connect(ep.substr(0, colon), std::atoi(ep.c_str() + colon + 1), 10000);
-    if (fd < 0) OCM_FAIL(-1, "cannot reach data server %s", ep.c_str());
-    if (send_all(fd, &token, sizeof(token)) != 1) {
-        close(fd);
-        OCM_FAIL(-1, "data server %s refused the connection", ep.c_str());
-    }
-    s.net_conns[ep] = fd;
-    return fd;
-}
-
-void net_drop(const std::string &ep) {
-    State &s = S();
-    auto it = s.net_conns.find(ep);
-    if (it == s.net_conns.end()) return;
-    close(it->second);
-    s.net_conns.erase(it);
-}
-
-// Blocking one-sided PUT/GET of one contiguous piece over TCP. Device-side
-// local memory is staged through a pinned buffer, kNetChunk at a time.
-int net_piece(const Extent &e, bool put, char *lin, Loc lloc, uint64_t ext_off, uint64_t len) {
-    State &s = S();
-    int fd = net_conn(e.ep, e.net_token);
-    if (fd < 0) return -1;
-    NetReq q{kNetMagic, put ? (uint32_t)NET_PUT : (uint32_t)NET_GET, e.r.slab_id, e.r.tier, e.r.offset + ext_off, len};
-    const bool dev = lloc == LOC_DEVICE;
-    if (dev && !s.net_stage) {
-        DeviceGuard g(s.device);
-        if (hipHostMalloc(&s.net_stage, kNetChunk, hipHostMallocDefault) != hipSuccess) {
-            (void)hipGetLastError();
-            s.net_stage = nullptr;
-            OCM_FAIL(-1, "no pinned staging buffer for the network tier");
-        }
-    }
-    auto fail = [&](const char *what) {
-        net_drop(e.ep);
-        set_last_error("network tier %s with %s failed", what, e.ep.c_str());
-        return -1;
-    };
-    if (send_all(fd, &q, sizeof(q)) != 1) return fail("request");
-    NetResp r;
-    if (put) {
-        for (uint64_t done = 0; done < len;) {
-            const size_t n = (size_t)std::min<uint64_t>(kNetChunk, len - done);
-            const char *src = lin + done;
-            if (dev) {
-                DeviceGuard g(s.device);
-                if (hipMemcpy(s.net_stage, lin + done, n, hipMemcpyDeviceToHost) != hipSuccess) return fail("staging");
-                src = static_cast<const char *>(s.net_stage);
-            }
-            if (send_all(fd, src, n) != 1) return fail("payload");
-            done += n;
-        }
-        if (recv_all(fd, &r, sizeof(r)) != 1 || r.magic != kNetMagic) return fail("response");
-        if (r.err) OCM_FAIL(-1, "remote PUT refused: %s", strerror(r.err));
-        return 0;
-    }
-    if (recv_all(fd, &r, sizeof(r)) != 1 || r.magic != kNetMagic) return fail("response");
-    if (r.err) OCM_FAIL(-1, "remote GET refused: %s", strerror(r.err));
-    for (uint64_t done = 0; done < len;) {
-        const size_t n = (size_t)std::min<uint64_t>(kNetChunk, len - done);
-        char *dst = dev ? static_cast<char *>(s.net_stage) : lin + done;
-        if (recv_all(fd, dst, n) != 1) return fail("payload");
-        if (dev) {
-            DeviceGuard g(s.device);
-            if (hipMemcpy(lin + done, s.net_stage, n, hipMemcpyHostToDevice) != hipSuccess) return fail("staging");
-        }
-        done += n;
-    }
-    return 0;
-}
-
-// One-sided transfer between the linear buffer `lin` (location `lloc`) and the
-// remote half of `a` at striped offset `rem_off`.
-int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async) {
-    State &s = S();
-    if (len == 0) return 0;
-    if (a->any_net) {
-        // Another node: stream every piece through its owner's data server (blocking).
-        std::vector<Seg> segs;
-        segments(a, rem_off, len, segs);
-        if (wait_alloc(a) != 0) return -1;
-        if (honor_dep(a, nullptr, true) != 0) return -1;
-        for (auto &g : segs) {
-            const Extent &e = a->ext[g.ext];
-            if (e.net) {
-                if (net_piece(e, put, lin + g.lin_off, lloc, g.ext_off, g.len) != 0) return -1;
-                continue;
-            }
-            // mixed placement: this piece is on this node
-            char *r = (lloc == LOC_DEVICE || e.r.tier == TIER_GPU) ? e.dptr : e.hptr;
-            r += g.ext_off;
-            if (s.device < 0 || (lloc != LOC_DEVICE && e.r.tier != TIER_GPU)) {
-                std::memcpy(put ? r : lin + g.lin_off, put ? lin + g.lin_off : r, g.len);
-            } else {
-                DeviceGuard dg(s.device);
-                if ((put ? hipMemcpyAsync(r, lin + g.lin_off, g.len, hipMemcpyDefault, s.stream)
-                         : hipMemcpyAsync(lin + g.lin_off, r, g.len, hipMemcpyDefault, s.stream)) != hipSuccess)
-                    OCM_FAIL(-1, "transfer launch failed");
-                if (sync_stream() != 0) return -1;
-            }
-        }
-        return 0;
-    }
-    std::vector<Seg> segs;
-    if (s.device < 0) {
-        segments(a, rem_off, len, segs);
-        for (auto &g : segs) {
-            char *r = a->ext[g.ext].hptr + g.ext_off;
-            if (put)
-                std::memcpy(r, lin + g.lin_off, g.len);
-            else
-                std::memcpy(lin + g.lin_off, r, g.len);
-        }
-        return 0;
-    }
-    DeviceGuard guard(s.device);
-    const bool lin_dev = lloc == LOC_DEVICE;
-    // HBM extents: always the kernel. Host-tier extents: the kernel below
-    // host_kernel_max (lower latency), the DMA engines above (higher peak).
-    const bool use_kernel = lin_dev && (a->any_gpu || s.host_engine_kernel || len <= s.host_kernel_max);
-    hipError_t err = hipSuccess;
-    // Small blocking ops go to the resident copy service (no launch, no stream sync).
-    if (lin_dev && a->all_dev_ok && !async && len <= s.svc_max) {
-        XferArgs x;
-        std::memset(&x, 0, sizeof(x));
-        x.lin = lin;
-        for (size_t i = 0; i < a->ext.size(); i++) x.ext[i] = a->ext[i].dptr;
-        x.n_ext = (uint32_t)a->ext.size();
-        x.rem_off = rem_off;
-        x.len = len;
-        x.put = put ? 1 : 0;
-        if (x.n_ext > 1) x.unit_shift = (uint32_t)log2_exact(a->stripe_unit);
-        if (wait_alloc(a) != 0) return -1;  // keep program order with queued async ops
-        if (honor_dep(a, nullptr, true) != 0) return -1;
-        if (service_xfer(x) == 0) return 0;
-        OCM_WARN("copy service failed (%s); falling back to launches", last_error());
-        s.svc_max = 0;
-    }
-    // Async ops queue on the allocation's lane; blocking ops on the library stream
-    // after the allocation's queued async work.
-    if (!async && wait_alloc(a) != 0) return -1;
-    hipStream_t st = async ? lane_stream(a) : s.stream;
-    if (honor_dep(a, st, false) != 0) return -1;
-    if (use_kernel) {
-        XferArgs x;
-        std::memset(&x, 0, sizeof(x));
-        x.lin = lin;
-        for (size_t i = 0; i < a->ext.size(); i++) x.ext[i] = a->ext[i].dptr;
-        x.n_ext = (uint32_t)a->ext.size();
-        x.rem_off = rem_off;
-        x.len = len;
-        x.put = put ? 1 : 0;
-        if (x.n_ext > 1) {
-            int sh = log2_exact(a->stripe_unit);
-            if (sh < 0) OCM_FAIL(-1, "stripe unit %llu is not a power of two", (unsigned long long)a->stripe_unit);
-            x.unit_shift = (uint32_t)sh;
-        }
-        XferTuning t = s.tuning;
-        if (t.variant == XFER_AUTO) {
-            // Measured (profiles/ksweep_r01.json): LDS-DMA staging wins HBM->HBM
-            // copies up to ~256 MiB on the same GPU; everything else (peer HBM
-            // over xGMI, host-mapped memory, huge copies) uses the register path.
-            bool same_gpu = lloc == LOC_DEVICE;
-            for (auto &e : a->ext) same_gpu &= e.r.tier == TIER_GPU && e.r.owner_gpu == s.device;
-            t.variant = (same_gpu && len <= (256ull << 20)) ? XFER_LDS : XFER_REG;
-        }
-        err = xfer_launch(x, t, st);
-    } else {
-        service_park();
-        segments(a, rem_off, len, segs);
-        for (auto &g : segs) {
-            const Extent &e = a->ext[g.ext];
-            char *r = (lloc == LOC_DEVICE || e.r.tier == TIER_GPU) ? e.dptr : e.hptr;
-            r += g.ext_off;
-            if (lloc != LOC_DEVICE && e.r.tier != TIER_GPU) {
-                // host <-> host tier: the CPU is the fastest engine.
-                if (put)
-                    std::memcpy(r, lin + g.lin_off, g.len);
-                else
-                    std::memcpy(lin + g.lin_off, r, g.len);
-                continue;
-            }
-            err = put ? hipMemcpyAsync(r, lin + g.lin_off, g.len, hipMemcpyDefault, st)
-                      : hipMemcpyAsync(lin + g.lin_off, r, g.len, hipMemcpyDefault, st);
-            if (err != hipSuccess) break;
-        }
-    }
-    if (err != hipSuccess) OCM_FAIL(-1, "transfer launch failed: %s", hipGetErrorString(err));
-    if (async) {
-        if (st != s.stream && a->ev) {
-            err = hipEventRecord(a->ev, st);
-            if (err != hipSuccess) OCM_FAIL(-1, "event record failed: %s", hipGetErrorString(err));
-        } else if (a->ev == nullptr && sync_stream() != 0) {
-            return -1;  // no lane available: complete it now
-        }
-        a->async_pending = a->ev != nullptr;
-        return 0;
-    }
-    return sync_stream();
-}
-
-// Copy between two process-local buffers.
-int copy_local(void *dst, Loc dl, const void *src, Loc sl, size_t n) {
-    State &s = S();
-    if (n == 0) return 0;
-    if (dl != LOC_DEVICE && sl != LOC_DEVICE) {
-        std::memcpy(dst, src, n);
-        return 0;
-    }
-    DeviceGuard g(s.device);
-    hipError_t e;
-    if (dl == LOC_DEVICE && sl == LOC_DEVICE) {
-        XferTuning t = s.tuning;
-        if (t.variant == XFER_AUTO) t.variant = n <= (256ull << 20) ? XFER_LDS : XFER_REG;
-        e = xfer_copy(dst, src, n, t, s.stream);
-    } else
-    {
-        e = hipMemcpyAsync(dst, src, n, hipMemcpyDefault, s.stream);
-    }
-    if (e != hipSuccess) OCM_FAIL(-1, "local copy failed: %s", hipGetErrorString(e));
-    return sync_stream();
-}
-
-Loc pointer_loc(const void *p) {
-    State &s = S();
-    if (s.device < 0 || !p) return LOC_HOST;
-    hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return LOC_HOST;
-    }
-    if (at.type == hipMemoryTypeDevice) return LOC_DEVICE;
-    if (at.type == hipMemoryTypeHost) return LOC_PINNED;
-    return LOC_HOST;
-}
-
-hipMemPool_t local_pool() {
-    State &s = S();
-    if (s.pool_tried) return s.pool;
-    s.pool_tried = true;
-    if (s.device < 0 || !env_int("OCM_LOCAL_POOL", 1)) return nullptr;
-    DeviceGuard g(s.device);
-    hipMemPoolProps props;
-    std::memset(&props, 0, sizeof(props));
-    props.allocType = hipMemAllocationTypePinned;
-    props.handleTypes = hipMemHandleTypeNone;
-    props.location.type = hipMemLocationTypeDevice;
-    props.location.id = s.device;
-    if (hipMemPoolCreate(&s.pool, &props) != hipSuccess) {
-        (void)hipGetLastError();
-        OCM_WARN("hipMemPoolCreate on device %d failed; local halves use hipMalloc", s.device);
-        s.pool = nullptr;
-        return nullptr;
-    }
-    if (const char *k = std::getenv("OCM_LOCAL_POOL_KEEP")) s.pool_keep = std::strtoull(k, nullptr, 0);
-    uint64_t keep = s.pool_keep;
-    (void)hipMemPoolSetAttribute(s.pool, hipMemPoolAttrReleaseThreshold, &keep);
-    // Peers read/write the local half too (SDMA from peer engines, torch on another GPU).
-    int ndev = 0;
-    (void)hipGetDeviceCount(&ndev);
-    for (int p = 0; p < ndev; p++) {
-        int can = 0;
-        if (p == s.device || hipDeviceCanAccessPeer(&can, p, s.device) != hipSuccess || !can) continue;
-        hipMemAccessDesc d;
-        d.location.type = hipMemLocationTypeDevice;
-        d.location.id = p;
-        d.flags = hipMemAccessFlagsProtReadWrite;
-        if (hipMemPoolSetAccess(s.pool, &d, 1) != hipSuccess) (void)hipGetLastError();
-    }
-    return s.pool;
-}
-
-int free_local_half(lib_alloc *a) {
-    State &s = S();
-    if (!a->local) return 0;
-    if (a->pooled) {
-        DeviceGuard g(s.device);
-        // Ordered after every transfer queued on s.stream; the block returns to the pool.
-        if (hipFreeAsync(a->local, s.stream) != hipSuccess) (void)hipGetLastError();
-        a->pooled = false;
-    } else if (a->loc == LOC_DEVICE) {
-        DeviceGuard g(s.device);
-        (void)hipFree(a->local);
-    } else if (a->loc == LOC_PINNED) {
-        DeviceGuard g(s.device);
-        (void)hipHostFree(a->local);
-    } else {
-        std::free(a->local);
-    }
-    a->local = nullptr;
-    return 0;
-}
-
-int alloc_local_half(lib_alloc *a, size_t bytes, Loc want) {
-    State &s = S();
-    a->local_bytes = bytes;
-    if (bytes == 0) return 0;
-    if (want != LOC_HOST && s.device < 0) want = LOC_HOST;
-    if (want == LOC_DEVICE && local_pool()) {
-        DeviceGuard g(s.device);
-        hipError_t e = hipMallocFromPoolAsync(&a->local, bytes, s.pool, s.stream);
-        // The app may touch the buffer from any stream as soon as ocm_alloc returns.
-        if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            OCM_FAIL(-1, "pool allocation of %zu bytes for local half: %s", bytes, hipGetErrorString(e));
-        }
-        a->pooled = true;
-    } else if (want == LOC_DEVICE) {
-        DeviceGuard g(s.device);
-        hipError_t e = hipMalloc(&a->local, bytes);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            OCM_FAIL(-1, "hipMalloc(%zu) for local half: %s", bytes, hipGetErrorString(e));
-        }
-    } else if (want == LOC_PINNED) {
-        DeviceGuard g(s.device);
-        hipError_t e = hipHostMalloc(&a->local, bytes, hipHostMallocDefault);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            OCM_FAIL(-1, "hipHostMalloc(%zu) for local half: %s", bytes, hipGetErrorString(e));
-        }
-    } else {
-        if (posix_memalign(&a->local, 4096, bytes) != 0) OCM_FAIL(-1, "host allocation of %zu bytes failed", bytes);
-    }
-    a->loc = want;
-    return 0;
-}
-
-}  // namespace
+using namespace ocmlib;
 
 // ================================================================ C API
 
@@ -1223,296 +380,6 @@ static int onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
                  (unsigned long long)p->bytes, a->remote_bytes);
     return xfer(a, p->op_flag != 0, static_cast<char *>(a->local) + p->src_offset, a->loc, p->dest_offset, p->bytes,
                 async);
-}
-
-static int batch_impl(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, int flags, uint64_t *moved);
-
-// Batch launch arguments for `ops` on `a` (descriptors in `v`; inline ones copied into args).
-static void build_batch_args(lib_alloc *a, const struct ocm_params *ops, int n_ops, XferBatchArgs *args,
-                             std::vector<XferBatchOp> *v) {
-    std::memset(args, 0, sizeof(*args));
-    args->lin = static_cast<char *>(a->local);
-    for (size_t i = 0; i < a->ext.size(); i++) args->ext[i] = a->ext[i].dptr;
-    args->n_ext = (uint32_t)a->ext.size();
-    args->unit_shift = args->n_ext > 1 ? (uint32_t)log2_exact(a->stripe_unit) : 0;
-    args->tile_shift = xfer_batch_tile_shift(args->n_ext, args->unit_shift);
-    args->n_ops = (uint32_t)n_ops;
-    v->assign((size_t)n_ops, XferBatchOp{});
-    for (int i = 0; i < n_ops; i++) {
-        (*v)[i].lin_off = ops[i].src_offset;
-        (*v)[i].rem_off = ops[i].dest_offset;
-        (*v)[i].len = ops[i].bytes;
-        (*v)[i].put = ops[i].op_flag != 0;
-    }
-    args->total_tiles = xfer_batch_plan(v->data(), (uint32_t)n_ops, args->tile_shift);
-    args->grid = args->total_tiles ? xfer_batch_grid(args->total_tiles) : 0;
-    if (n_ops <= kXferInlineOps) std::memcpy(args->inline_ops, v->data(), v->size() * sizeof(XferBatchOp));
-}
-
-// Bounds of every op against the pair (as ocm_copy_onesided). Adds the bytes to *moved.
-static int check_batch_ops(lib_alloc *a, const struct ocm_params *ops, int n_ops, uint64_t *moved) {
-    for (int i = 0; i < n_ops; i++) {
-        const ocm_params &p = ops[i];
-        if (p.src_offset > a->local_bytes || p.bytes > a->local_bytes - p.src_offset)
-            OCM_FAIL(-1, "batch op %d: local range [%llu,+%llu) exceeds %zu bytes", i,
-                     (unsigned long long)p.src_offset, (unsigned long long)p.bytes, a->local_bytes);
-        if (p.dest_offset > a->remote_bytes || p.bytes > a->remote_bytes - p.dest_offset)
-            OCM_FAIL(-1, "batch op %d: remote range [%llu,+%llu) exceeds %zu bytes", i,
-                     (unsigned long long)p.dest_offset, (unsigned long long)p.bytes, a->remote_bytes);
-        *moved += p.bytes;
-    }
-    return 0;
-}
-
-// One kernel can serve this pair: device local half, every extent device-accessible.
-static bool batch_device_path(const lib_alloc *a) {
-    const State &s = S();
-    return s.device >= 0 && a->loc == LOC_DEVICE && a->all_dev_ok && !a->any_net &&
-           (a->ext.size() == 1 || log2_exact(a->stripe_unit) >= 4);
-}
-
-int ocm_copy_onesided_batch(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, int flags) {
-    TraceRange tr("ocm_batch");
-    const uint64_t t0 = now_ns();
-    uint64_t moved = 0;
-    int rc = batch_impl(a, ops, n_ops, flags, &moved);
-    const uint64_t t1 = now_ns();
-    if (rc == 0) {
-        OpCounters &c = S().ctr;
-        c.n_batch++;
-        c.n_batch_ops += (uint64_t)n_ops;
-        c.bytes_batch += moved;
-        c.ns_batch += t1 - t0;
-    }
-    trace_op("batch", moved, t0, t1, rc);
-    return rc;
-}
-
-static int batch_impl(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, int flags, uint64_t *moved) {
-    State &s = S();
-    std::lock_guard<std::recursive_mutex> lk(s.mu);
-    if (!a || (!ops && n_ops)) OCM_FAIL(-1, "ocm_copy_onesided_batch: NULL argument");
-    if (!s.allocs.count(a)) OCM_FAIL(-1, "ocm_copy_onesided_batch: unknown allocation");
-    if (!a->remote) OCM_FAIL(-1, "batched one-sided copies need a remote pair (kind %d)", (int)a->kind);
-    if (n_ops < 0) OCM_FAIL(-1, "ocm_copy_onesided_batch: n_ops < 0");
-    const bool async = (flags & OCM_BATCH_ASYNC) != 0;
-    if (check_batch_ops(a, ops, n_ops, moved) != 0) return -1;
-    if (n_ops == 0) return 0;
-    if (!batch_device_path(a)) {
-        // No device-side path (CPU app, network tier, host local half): op by op, in order.
-        for (int i = 0; i < n_ops; i++)
-            if (xfer(a, ops[i].op_flag != 0, static_cast<char *>(a->local) + ops[i].src_offset, a->loc,
-                     ops[i].dest_offset, ops[i].bytes, async) != 0)
-                return -1;
-        return 0;
-    }
-    DeviceGuard guard(s.device);
-    XferBatchArgs args;
-    std::vector<XferBatchOp> v;
-    build_batch_args(a, ops, n_ops, &args, &v);
-    if (args.total_tiles == 0) return 0;  // only empty ops
-    if (!async && wait_alloc(a) != 0) return -1;
-    hipStream_t st = async ? lane_stream(a) : s.stream;
-    if (honor_dep(a, st, false) != 0) return -1;
-    hipError_t err = hipSuccess;
-    if (n_ops > kXferInlineOps) {
-        // descriptors, then the per-wave starting ops, in one upload
-        const size_t dbytes = v.size() * sizeof(XferBatchOp);
-        const size_t need = dbytes + (size_t)args.grid * 4 * sizeof(uint32_t);
-        if (a->batch_up && hipEventSynchronize(a->batch_up) != hipSuccess)  // staging free again
-            OCM_FAIL(-1, "batch staging wait failed");
-        if (a->batch_cap < need) {
-            if (a->batch_dev) (void)hipFreeAsync(a->batch_dev, st);
-            if (a->batch_host) (void)hipHostFree(a->batch_host);
-            a->batch_dev = a->batch_host = nullptr;
-            a->batch_cap = 0;
-            const size_t cap = std::max<size_t>(need, 64 << 10);
-            err = local_pool() ? hipMallocFromPoolAsync(&a->batch_dev, cap, s.pool, st) : hipMallocAsync(&a->batch_dev, cap, st);
-            if (err == hipSuccess) err = hipHostMalloc(&a->batch_host, cap, hipHostMallocDefault);
-            if (err == hipSuccess && !a->batch_up) err = hipEventCreateWithFlags(&a->batch_up, hipEventDisableTiming);
-            if (err != hipSuccess) {
-                (void)hipGetLastError();
-                OCM_FAIL(-1, "batch descriptors: %s", hipGetErrorString(err));
-            }
-            a->batch_cap = cap;
-        }
-        char *up = static_cast<char *>(a->batch_host);
-        std::memcpy(up, v.data(), dbytes);
-        xfer_batch_wave_ops(v.data(), (uint32_t)n_ops, args.total_tiles, args.grid, reinterpret_cast<uint32_t *>(up + dbytes));
-        // Pinned source: a real async DMA; batch_up tells the next batch when `up` is free.
-        err = hipMemcpyAsync(a->batch_dev, up, need, hipMemcpyHostToDevice, st);
-        if (err == hipSuccess) err = hipEventRecord(a->batch_up, st);
-        if (err != hipSuccess) OCM_FAIL(-1, "batch descriptor upload: %s", hipGetErrorString(err));
-        args.ops = static_cast<const XferBatchOp *>(a->batch_dev);
-        args.wave_op = reinterpret_cast<const uint32_t *>(static_cast<char *>(a->batch_dev) + dbytes);
-    }
-    err = xfer_batch_launch(args, s.tuning, st);
-    if (err != hipSuccess) OCM_FAIL(-1, "batch launch failed: %s", hipGetErrorString(err));
-    if (async) {
-        if (st != s.stream && a->ev) {
-            err = hipEventRecord(a->ev, st);
-            if (err != hipSuccess) OCM_FAIL(-1, "event record failed: %s", hipGetErrorString(err));
-            a->async_pending = true;
-            return 0;
-        }
-    }
-    return sync_stream();
-}
-
-int ocm_stream_wait(ocm_alloc_t a, void *stream) {
-    State &s = S();
-    std::lock_guard<std::recursive_mutex> lk(s.mu);
-    if (!a || !s.allocs.count(a)) OCM_FAIL(-1, "ocm_stream_wait: unknown allocation");
-    if (s.device < 0) return 0;  // CPU app: every op is synchronous already
-    DeviceGuard g(s.device);
-    if (!a->dep_ev && hipEventCreateWithFlags(&a->dep_ev, hipEventDisableTiming) != hipSuccess) {
-        (void)hipGetLastError();
-        a->dep_ev = nullptr;
-        OCM_FAIL(-1, "ocm_stream_wait: no event");
-    }
-    hipError_t e = hipEventRecord(a->dep_ev, static_cast<hipStream_t>(stream));
-    if (e != hipSuccess) OCM_FAIL(-1, "ocm_stream_wait: %s", hipGetErrorString(e));
-    a->dep_pending = true;
-    return 0;
-}
-
-int ocm_stream_signal(ocm_alloc_t a, void *stream) {
-    State &s = S();
-    std::lock_guard<std::recursive_mutex> lk(s.mu);
-    if (!a || !s.allocs.count(a)) OCM_FAIL(-1, "ocm_stream_signal: unknown allocation");
-    if (s.device < 0 || !a->async_pending || !a->ev) return 0;  // nothing queued: already complete
-    DeviceGuard g(s.device);
-    hipError_t e = hipStreamWaitEvent(static_cast<hipStream_t>(stream), a->ev, 0);
-    if (e != hipSuccess) OCM_FAIL(-1, "ocm_stream_signal: %s", hipGetErrorString(e));
-    return 0;
-}
-
-// ---------------- transfer plans (hipGraph replay of fixed batch schedules) ----------------
-
-ocm_plan_t ocm_plan_create(void) {
-    State &s = S();
-    std::lock_guard<std::recursive_mutex> lk(s.mu);
-    if (!s.inited) {
-        set_last_error("ocm_plan_create: ocm_init first");
-        return nullptr;
-    }
-    if (s.device < 0) {
-        set_last_error("ocm_plan_create: plans replay on a GPU; this process has none");
-        return nullptr;
-    }
-    return new ocm_plan();
-}
-
-static void plan_drop_graph(ocm_plan *p) {
-    if (p->exec) (void)hipGraphExecDestroy(p->exec);
-    if (p->graph) (void)hipGraphDestroy(p->graph);
-    p->exec = nullptr;
-    p->graph = nullptr;
-}
-
-int ocm_plan_add(ocm_plan_t p, ocm_alloc_t a, const struct ocm_params *ops, int n_ops) {
-    State &s = S();
-    std::lock_guard<std::recursive_mutex> lk(s.mu);
-    if (!p || !a || (!ops && n_ops) || n_ops < 0) OCM_FAIL(-1, "ocm_plan_add: bad argument");
-    if (!s.allocs.count(a) || !a->remote) OCM_FAIL(-1, "ocm_plan_add: not a live remote pair");
-    if (!batch_device_path(a)) OCM_FAIL(-1, "ocm_plan_add: this pair has no device-side path (plans need one)");
-    uint64_t moved = 0;
-    if (check_batch_ops(a, ops, n_ops, &moved) != 0) return -1;
-    if (n_ops == 0) return 0;
-    DeviceGuard g(s.device);
-    ocm_plan::Stage st;
-    st.a = a;
-    std::vector<XferBatchOp> v;
-    build_batch_args(a, ops, n_ops, &st.args, &v);
-    if (st.args.total_tiles == 0) return 0;
-    if (n_ops > kXferInlineOps) {
-        const size_t dbytes = v.size() * sizeof(XferBatchOp);
-        const size_t need = dbytes + (size_t)st.args.grid * 4 * sizeof(uint32_t);
-        std::vector<char> up(need);
-        std::memcpy(up.data(), v.data(), dbytes);
-        xfer_batch_wave_ops(v.data(), (uint32_t)n_ops, st.args.total_tiles, st.args.grid,
-                            reinterpret_cast<uint32_t *>(up.data() + dbytes));
-        hipError_t e = hipMalloc(&st.dev, need);
-        if (e == hipSuccess) e = hipMemcpy(st.dev, up.data(), need, hipMemcpyHostToDevice);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            if (st.dev) (void)hipFree(st.dev);
-            OCM_FAIL(-1, "ocm_plan_add: descriptor upload: %s", hipGetErrorString(e));
-        }
-        st.args.ops = static_cast<const XferBatchOp *>(st.dev);
-        st.args.wave_op = reinterpret_cast<const uint32_t *>(static_cast<char *>(st.dev) + dbytes);
-    }
-    p->stages.push_back(st);
-    p->bytes += moved;
-    p->n_ops += (uint64_t)n_ops;
-    a->plans++;
-    plan_drop_graph(p);  // re-captured at the next launch
-    return 0;
-}
-
-int ocm_plan_launch(ocm_plan_t p, void *stream) {
-    State &s = S();
-    std::lock_guard<std::recursive_mutex> lk(s.mu);
-    TraceRange tr("ocm_plan_launch");
-    const uint64_t t0 = now_ns();
-    if (!p) OCM_FAIL(-1, "ocm_plan_launch: NULL plan");
-    if (p->stages.empty()) return 0;
-    DeviceGuard g(s.device);
-    hipError_t e = hipSuccess;
-    if (!p->exec) {
-        // Capture the stage chain once; every later launch is one hipGraphLaunch.
-        hipStream_t cs = nullptr;
-        e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
-        for (size_t i = 0; e == hipSuccess && i < p->stages.size(); i++)
-            e = xfer_batch_launch(p->stages[i].args, s.tuning, cs);
-        hipGraph_t graph = nullptr;
-        hipError_t e2 = cs ? hipStreamEndCapture(cs, &graph) : hipErrorInvalidValue;
-        if (e == hipSuccess) e = e2;
-        if (e == hipSuccess) e = hipGraphInstantiate(&p->exec, graph, nullptr, nullptr, 0);
-        if (cs) (void)hipStreamDestroy(cs);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            if (graph) (void)hipGraphDestroy(graph);
-            p->exec = nullptr;
-            OCM_FAIL(-1, "ocm_plan_launch: graph capture: %s", hipGetErrorString(e));
-        }
-        p->graph = graph;
-    }
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s.stream;
-    // Order after the allocations' own queued work and ocm_stream_wait dependencies.
-    for (auto &sg : p->stages) {
-        lib_alloc *a = sg.a;
-        if (a->async_pending && a->ev) (void)hipStreamWaitEvent(st, a->ev, 0);
-        if (honor_dep(a, st, false) != 0) return -1;
-    }
-    e = hipGraphLaunch(p->exec, st);
-    if (e != hipSuccess) OCM_FAIL(-1, "ocm_plan_launch: %s", hipGetErrorString(e));
-    int rc = stream ? 0 : sync_stream();
-    const uint64_t t1 = now_ns();
-    if (rc == 0) {
-        OpCounters &c = s.ctr;
-        c.n_batch++;
-        c.n_batch_ops += p->n_ops;
-        c.bytes_batch += p->bytes;
-        c.ns_batch += t1 - t0;
-    }
-    trace_op("plan", p->bytes, t0, t1, rc);
-    return rc;
-}
-
-int ocm_plan_destroy(ocm_plan_t p) {
-    State &s = S();
-    std::lock_guard<std::recursive_mutex> lk(s.mu);
-    if (!p) return -1;
-    DeviceGuard g(s.device);
-    plan_drop_graph(p);
-    for (auto &st : p->stages) {
-        if (st.dev) (void)hipFree(st.dev);  // synchronizing free: replays have finished
-        if (s.allocs.count(st.a) && st.a->plans > 0) st.a->plans--;
-    }
-    delete p;
-    return 0;
 }
 
 int ocm_copy_onesided(ocm_alloc_t a, ocm_param_t p) { return ocm_copy_onesided_impl(a, p, false); }

@@ -1,0 +1,266 @@
+// libocm process state, mailbox RPC to the local ocmd, the import cache of
+// remote extents (hipIpcOpenMemHandle / memfd + hipHostRegister), and the
+// local halves of allocations (stream-ordered pool, pinned host, malloc).
+#include "internal.h"
+
+namespace ocmlib {
+
+State &S() {
+    static State *s = new State();  // never destroyed: safe at process exit
+    return *s;
+}
+
+int env_int(const char *k, int dflt) {
+    const char *v = std::getenv(k);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
+
+long now_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1000L + ts.tv_nsec / 1000000L;
+}
+
+Msg new_msg(uint32_t type) {
+    Msg m;
+    std::memset(&m, 0, sizeof(m));
+    m.type = type;
+    m.status = MSG_REQUEST;
+    m.pid = S().pid;
+    m.rank = S().daemon_rank;
+    m.src_rank = -1;
+    return m;
+}
+
+// Send a request and wait for the reply carrying the same seq.
+int rpc(Msg &req, Msg *reply, int timeout_ms) {
+    State &s = S();
+    req.seq = ++s.seq;
+    if (s.chan.send(&req, kMsgBytes, timeout_ms) != 1) OCM_FAIL(-1, "mailbox send to daemon failed");
+    const long deadline = now_ms() + timeout_ms;
+    for (;;) {
+        long left = deadline - now_ms();
+        if (left <= 0) OCM_FAIL(-1, "daemon did not answer %s within %d ms", msg_type_str(req.type), timeout_ms);
+        int rc = s.chan.recv(reply, kMsgBytes, (int)std::min<long>(left, 1000));
+        if (rc < 0) return -1;
+        if (rc == 0) continue;
+        if (reply->seq == req.seq && reply->type != MSG_EXTENT) return 0;
+        OCM_LOG("dropping stale reply %s seq %llu", msg_type_str(reply->type), (unsigned long long)reply->seq);
+    }
+}
+
+int recv_seq(Msg *m, uint64_t seq, uint32_t type, int timeout_ms) {
+    const long deadline = now_ms() + timeout_ms;
+    for (;;) {
+        long left = deadline - now_ms();
+        if (left <= 0) OCM_FAIL(-1, "timed out waiting for %s", msg_type_str(type));
+        int rc = S().chan.recv(m, kMsgBytes, (int)std::min<long>(left, 1000));
+        if (rc < 0) return -1;
+        if (rc == 1 && m->seq == seq && m->type == type) return 0;
+    }
+}
+
+bool is_pair(enum ocm_kind k) { return k == OCM_REMOTE_GPU || k == OCM_REMOTE_RDMA || k == OCM_REMOTE_RMA; }
+
+// ---------------------------------------------------------------- import cache
+
+int import_extent(Extent &e) {
+    State &s = S();
+    const Region &r = e.r;
+    if (r.flags & REGION_NET) {
+        char buf[65] = {0};
+        std::memcpy(buf, r.handle, 64);
+        char host[64] = {0};
+        int port = 0;
+        unsigned long long tok = 0;
+        if (std::sscanf(buf, "net:%63[^:]:%d:%llx", host, &port, &tok) != 3 || port <= 0)
+            OCM_FAIL(-1, "bad network-tier handle");
+        e.net = true;
+        e.dev_ok = false;
+        e.ep = std::string(host) + ":" + std::to_string(port);
+        e.net_token = tok;
+        return 0;
+    }
+    SlabKey key{r.owner_rank, r.tier, r.slab_id};
+    auto it = s.imports.find(key);
+    if (it != s.imports.end() && std::memcmp(it->second.handle, r.handle, kHandleBytes) != 0) {
+        // Same id, different export: the owner restarted. Drop the stale mapping.
+        Mapping &m = it->second;
+        if (r.tier == TIER_GPU && m.dbase) (void)hipIpcCloseMemHandle(m.dbase);
+        if (m.registered) (void)hipHostUnregister(m.hbase);
+        if (m.hbase) munmap(m.hbase, m.bytes);
+        s.imports.erase(it);
+        it = s.imports.end();
+    }
+    if (it == s.imports.end()) {
+        Mapping m;
+        m.bytes = r.slab_bytes;
+        m.dedicated = (r.flags & REGION_DEDICATED) != 0;
+        std::memcpy(m.handle, r.handle, kHandleBytes);
+        if (r.tier == TIER_GPU) {
+            if (s.device < 0) OCM_FAIL(-1, "remote HBM extent but this process has no GPU");
+            DeviceGuard g(s.device);
+            hipIpcMemHandle_t h;
+            std::memcpy(&h, r.handle, sizeof(h));
+            void *p = nullptr;
+            hipError_t err = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+            if (err != hipSuccess) OCM_FAIL(-1, "hipIpcOpenMemHandle(owner %d slab %u): %s", r.owner_rank, r.slab_id, hipGetErrorString(err));
+            m.dbase = static_cast<char *>(p);
+        } else {
+            char path[kHandleBytes + 1];
+            std::memcpy(path, r.handle, kHandleBytes);
+            path[kHandleBytes] = 0;
+            int fd = open(path, O_RDWR | O_CLOEXEC);
+            if (fd < 0) OCM_FAIL(-1, "open host-tier slab %s: %s", path, strerror(errno));
+            void *p = mmap(nullptr, r.slab_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            close(fd);
+            if (p == MAP_FAILED) OCM_FAIL(-1, "mmap host-tier slab: %s", strerror(errno));
+            m.hbase = static_cast<char *>(p);
+            m.dbase = m.hbase;
+            if (s.device >= 0) {
+                DeviceGuard g(s.device);
+                hipError_t err = hipHostRegister(p, r.slab_bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+                if (err == hipSuccess) {
+                    void *dp = nullptr;
+                    if (hipHostGetDevicePointer(&dp, p, 0) == hipSuccess) m.dbase = static_cast<char *>(dp);
+                    m.registered = true;
+                } else {
+                    (void)hipGetLastError();
+                    OCM_WARN("hipHostRegister of host-tier slab failed: %s (DMA from pageable memory)", hipGetErrorString(err));
+                }
+            }
+        }
+        it = s.imports.emplace(key, m).first;
+    }
+    it->second.refs++;
+    e.dev_ok = r.tier == TIER_GPU || it->second.registered;
+    e.dptr = it->second.dbase + r.offset;
+    e.hptr = it->second.hbase ? it->second.hbase + r.offset : nullptr;
+    return 0;
+}
+
+void release_extent(const Extent &e, bool force) {
+    State &s = S();
+    if (e.net) return;
+    SlabKey key{e.r.owner_rank, e.r.tier, e.r.slab_id};
+    auto it = s.imports.find(key);
+    if (it == s.imports.end()) return;
+    Mapping &m = it->second;
+    if (--m.refs > 0 && !force) return;
+    if (!m.dedicated && !force) return;  // shared slabs stay mapped for reuse
+    DeviceGuard g(s.device);
+    if (e.r.tier == TIER_GPU && m.dbase) (void)hipIpcCloseMemHandle(m.dbase);
+    if (m.registered) (void)hipHostUnregister(m.hbase);
+    if (m.hbase) munmap(m.hbase, m.bytes);
+    s.imports.erase(it);
+}
+
+Loc pointer_loc(const void *p) {
+    State &s = S();
+    if (s.device < 0 || !p) return LOC_HOST;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return LOC_HOST;
+    }
+    if (at.type == hipMemoryTypeDevice) return LOC_DEVICE;
+    if (at.type == hipMemoryTypeHost) return LOC_PINNED;
+    return LOC_HOST;
+}
+
+hipMemPool_t local_pool() {
+    State &s = S();
+    if (s.pool_tried) return s.pool;
+    s.pool_tried = true;
+    if (s.device < 0 || !env_int("OCM_LOCAL_POOL", 1)) return nullptr;
+    DeviceGuard g(s.device);
+    hipMemPoolProps props;
+    std::memset(&props, 0, sizeof(props));
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = s.device;
+    if (hipMemPoolCreate(&s.pool, &props) != hipSuccess) {
+        (void)hipGetLastError();
+        OCM_WARN("hipMemPoolCreate on device %d failed; local halves use hipMalloc", s.device);
+        s.pool = nullptr;
+        return nullptr;
+    }
+    if (const char *k = std::getenv("OCM_LOCAL_POOL_KEEP")) s.pool_keep = std::strtoull(k, nullptr, 0);
+    uint64_t keep = s.pool_keep;
+    (void)hipMemPoolSetAttribute(s.pool, hipMemPoolAttrReleaseThreshold, &keep);
+    // Peers read/write the local half too (SDMA from peer engines, torch on another GPU).
+    int ndev = 0;
+    (void)hipGetDeviceCount(&ndev);
+    for (int p = 0; p < ndev; p++) {
+        int can = 0;
+        if (p == s.device || hipDeviceCanAccessPeer(&can, p, s.device) != hipSuccess || !can) continue;
+        hipMemAccessDesc d;
+        d.location.type = hipMemLocationTypeDevice;
+        d.location.id = p;
+        d.flags = hipMemAccessFlagsProtReadWrite;
+        if (hipMemPoolSetAccess(s.pool, &d, 1) != hipSuccess) (void)hipGetLastError();
+    }
+    return s.pool;
+}
+
+int free_local_half(lib_alloc *a) {
+    State &s = S();
+    if (!a->local) return 0;
+    if (a->pooled) {
+        DeviceGuard g(s.device);
+        // Ordered after every transfer queued on s.stream; the block returns to the pool.
+        if (hipFreeAsync(a->local, s.stream) != hipSuccess) (void)hipGetLastError();
+        a->pooled = false;
+    } else if (a->loc == LOC_DEVICE) {
+        DeviceGuard g(s.device);
+        (void)hipFree(a->local);
+    } else if (a->loc == LOC_PINNED) {
+        DeviceGuard g(s.device);
+        (void)hipHostFree(a->local);
+    } else {
+        std::free(a->local);
+    }
+    a->local = nullptr;
+    return 0;
+}
+
+int alloc_local_half(lib_alloc *a, size_t bytes, Loc want) {
+    State &s = S();
+    a->local_bytes = bytes;
+    if (bytes == 0) return 0;
+    if (want != LOC_HOST && s.device < 0) want = LOC_HOST;
+    if (want == LOC_DEVICE && local_pool()) {
+        DeviceGuard g(s.device);
+        hipError_t e = hipMallocFromPoolAsync(&a->local, bytes, s.pool, s.stream);
+        // The app may touch the buffer from any stream as soon as ocm_alloc returns.
+        if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            OCM_FAIL(-1, "pool allocation of %zu bytes for local half: %s", bytes, hipGetErrorString(e));
+        }
+        a->pooled = true;
+    } else if (want == LOC_DEVICE) {
+        DeviceGuard g(s.device);
+        hipError_t e = hipMalloc(&a->local, bytes);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            OCM_FAIL(-1, "hipMalloc(%zu) for local half: %s", bytes, hipGetErrorString(e));
+        }
+    } else if (want == LOC_PINNED) {
+        DeviceGuard g(s.device);
+        hipError_t e = hipHostMalloc(&a->local, bytes, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            OCM_FAIL(-1, "hipHostMalloc(%zu) for local half: %s", bytes, hipGetErrorString(e));
+        }
+    } else {
+        if (posix_memalign(&a->local, 4096, bytes) != 0) OCM_FAIL(-1, "host allocation of %zu bytes failed", bytes);
+    }
+    a->loc = want;
+    return 0;
+}
+
+
+}  // namespace ocmlib

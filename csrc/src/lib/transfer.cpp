@@ -1,0 +1,351 @@
+// libocm copy engine: striped segments, per-allocation lanes and events, the
+// resident copy service, one-sided transfers (gfx950 kernels / DMA / CPU)
+// and process-local copies.
+#include "internal.h"
+
+namespace ocmlib {
+
+// ---------------------------------------------------------------- copy engine
+
+
+// Split [rem_off, rem_off+len) of a striped buffer into contiguous pieces.
+void segments(const lib_alloc *a, uint64_t rem_off, uint64_t len, std::vector<Seg> &out) {
+    out.clear();
+    const int n = (int)a->ext.size();
+    if (n == 1 || a->stripe_unit == 0) {
+        out.push_back({0, rem_off, 0, len});
+        return;
+    }
+    const uint64_t unit = a->stripe_unit;
+    uint64_t pos = rem_off, done = 0;
+    while (done < len) {
+        const uint64_t u = pos / unit, within = pos % unit;
+        const uint64_t take = std::min(unit - within, len - done);
+        out.push_back({(int)(u % n), (u / n) * unit + within, done, take});
+        pos += take;
+        done += take;
+    }
+}
+
+
+int wait_event(hipEvent_t ev) {
+    State &s = S();
+    hipError_t e = hipSuccess;
+    if (s.sync_mode == 1) {
+        while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
+        }
+    } else {
+        e = hipEventSynchronize(ev);
+    }
+    if (e != hipSuccess) OCM_FAIL(-1, "event wait: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// ocm_stream_wait dependency: order it before work on `st` (nullptr: the
+// copy service, which has no stream, so wait on the host).
+int honor_dep(lib_alloc *a, hipStream_t st, bool host_wait) {
+    if (!a->dep_pending) return 0;
+    a->dep_pending = false;
+    hipError_t e = host_wait ? hipEventSynchronize(a->dep_ev) : hipStreamWaitEvent(st, a->dep_ev, 0);
+    if (e != hipSuccess) OCM_FAIL(-1, "stream dependency: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// Completion of `a`'s queued async ops (its lane up to the recorded event).
+int wait_alloc(lib_alloc *a) {
+    State &s = S();
+    if (!a || !a->async_pending) return 0;
+    a->async_pending = false;
+    if (!a->ev) return 0;
+    DeviceGuard g(s.device);
+    return wait_event(a->ev);
+}
+
+hipStream_t lane_stream(lib_alloc *a) {
+    State &s = S();
+    if (a->lane < 0) {
+        if (s.lanes.empty()) {
+            DeviceGuard g(s.device);
+            for (int i = 0; i < std::max(1, s.n_lanes); i++) {
+                hipStream_t st = nullptr;
+                if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+                    (void)hipGetLastError();
+                    break;
+                }
+                s.lanes.push_back(st);
+            }
+        }
+        if (s.lanes.empty()) return s.stream;
+        a->lane = s.next_lane++ % (int)s.lanes.size();
+    }
+    if (!a->ev) {
+        DeviceGuard g(s.device);
+        if (hipEventCreateWithFlags(&a->ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            a->ev = nullptr;
+            return s.stream;
+        }
+    }
+    return s.lanes[a->lane];
+}
+
+int sync_stream() {
+    State &s = S();
+    if (!s.stream) return 0;
+    DeviceGuard g(s.device);
+    hipError_t e = hipSuccess;
+    if (s.sync_mode == 0 || !s.done) {
+        e = hipStreamSynchronize(s.stream);
+    } else {
+        e = hipEventRecord(s.done, s.stream);
+        if (e == hipSuccess && s.sync_mode == 1) {
+            // Spin: lowest completion latency for small one-sided ops.
+            while ((e = hipEventQuery(s.done)) == hipErrorNotReady) {
+            }
+        } else if (e == hipSuccess) {
+            e = hipEventSynchronize(s.done);
+        }
+    }
+    if (e != hipSuccess) OCM_FAIL(-1, "stream sync: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// ---- persistent copy service ----
+
+int service_start(unsigned long long first_seq) {
+    State &s = S();
+    DeviceGuard g(s.device);
+    if (!s.svc) {
+        if (hipHostMalloc(reinterpret_cast<void **>(&s.svc), sizeof(ServiceSlot),
+                          hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+            (void)hipGetLastError();
+            s.svc = nullptr;
+            s.svc_max = 0;
+            OCM_FAIL(-1, "copy service: no coherent host memory");
+        }
+        std::memset(s.svc, 0, sizeof(ServiceSlot));
+        if (hipStreamCreateWithFlags(&s.svc_stream, hipStreamNonBlocking) != hipSuccess) {
+            (void)hipGetLastError();
+            s.svc_max = 0;
+            OCM_FAIL(-1, "copy service: no stream");
+        }
+    }
+    __atomic_store_n(&s.svc->exited, 0ull, __ATOMIC_RELEASE);
+    __atomic_store_n(&s.svc->seq, 0ull, __ATOMIC_RELEASE);  // clear a STOP left by a parked instance
+    if (service_launch(s.svc, first_seq, s.svc_idle_ticks, s.svc_stream) != hipSuccess) {
+        (void)hipGetLastError();
+        s.svc_max = 0;
+        OCM_FAIL(-1, "copy service launch failed");
+    }
+    s.svc_running = true;
+    return 0;
+}
+
+// Park the resident kernel: its doorbell polls cross PCIe and slow down
+// large DMA-engine transfers (measured: 53 -> 34 GiB/s on host-tier sweeps).
+void service_park() {
+    State &s = S();
+    if (!s.svc || !s.svc_running) return;
+    DeviceGuard g(s.device);
+    __atomic_store_n(&s.svc->seq, kServiceStop, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(s.svc_stream);
+    s.svc_running = false;
+}
+
+void service_stop() {
+    State &s = S();
+    if (!s.svc) return;
+    DeviceGuard g(s.device);
+    if (s.svc_running) {
+        __atomic_store_n(&s.svc->seq, kServiceStop, __ATOMIC_RELEASE);
+        (void)hipStreamSynchronize(s.svc_stream);
+        s.svc_running = false;
+    }
+    (void)hipStreamDestroy(s.svc_stream);
+    (void)hipHostFree(s.svc);
+    s.svc = nullptr;
+    s.svc_stream = nullptr;
+}
+
+// Run one normalized transfer through the resident kernel and wait for it.
+int service_xfer(XferArgs x) {
+    State &s = S();
+    if (xfer_normalize(x) != hipSuccess) OCM_FAIL(-1, "invalid transfer");
+    const unsigned long long seq = ++s.svc_seq;
+    if (!s.svc_running && service_start(seq) != 0) return -1;
+    std::memcpy(&s.svc->args, &x, sizeof(x));
+    __atomic_store_n(&s.svc->seq, seq, __ATOMIC_RELEASE);
+    const uint64_t t0 = now_ns();
+    for (unsigned spins = 1;; spins++) {
+        if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
+        if ((spins & 1023) == 0) {
+            // The kernel leaves after idle_ticks without work; if it left before
+            // taking this request, start a new one at this seq.
+            const unsigned long long ex = __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE);
+            if (ex && ex <= seq) {
+                DeviceGuard g(s.device);
+                (void)hipStreamSynchronize(s.svc_stream);
+                s.svc_running = false;
+                if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
+                if (service_start(seq) != 0) return -1;
+                __atomic_store_n(&s.svc->seq, seq, __ATOMIC_RELEASE);  // start cleared the doorbell: re-post
+            }
+            if (now_ns() - t0 > 10ull * 1000000000ull) OCM_FAIL(-1, "copy service did not complete a transfer in 10 s");
+        }
+    }
+}
+
+// One-sided transfer between the linear buffer `lin` (location `lloc`) and the
+// remote half of `a` at striped offset `rem_off`.
+int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async) {
+    State &s = S();
+    if (len == 0) return 0;
+    if (a->any_net) {
+        // Another node: stream every piece through its owner's data server (blocking).
+        std::vector<Seg> segs;
+        segments(a, rem_off, len, segs);
+        if (wait_alloc(a) != 0) return -1;
+        if (honor_dep(a, nullptr, true) != 0) return -1;
+        for (auto &g : segs) {
+            const Extent &e = a->ext[g.ext];
+            if (e.net) {
+                if (net_piece(e, put, lin + g.lin_off, lloc, g.ext_off, g.len) != 0) return -1;
+                continue;
+            }
+            // mixed placement: this piece is on this node
+            char *r = (lloc == LOC_DEVICE || e.r.tier == TIER_GPU) ? e.dptr : e.hptr;
+            r += g.ext_off;
+            if (s.device < 0 || (lloc != LOC_DEVICE && e.r.tier != TIER_GPU)) {
+                std::memcpy(put ? r : lin + g.lin_off, put ? lin + g.lin_off : r, g.len);
+            } else {
+                DeviceGuard dg(s.device);
+                if ((put ? hipMemcpyAsync(r, lin + g.lin_off, g.len, hipMemcpyDefault, s.stream)
+                         : hipMemcpyAsync(lin + g.lin_off, r, g.len, hipMemcpyDefault, s.stream)) != hipSuccess)
+                    OCM_FAIL(-1, "transfer launch failed");
+                if (sync_stream() != 0) return -1;
+            }
+        }
+        return 0;
+    }
+    std::vector<Seg> segs;
+    if (s.device < 0) {
+        segments(a, rem_off, len, segs);
+        for (auto &g : segs) {
+            char *r = a->ext[g.ext].hptr + g.ext_off;
+            if (put)
+                std::memcpy(r, lin + g.lin_off, g.len);
+            else
+                std::memcpy(lin + g.lin_off, r, g.len);
+        }
+        return 0;
+    }
+    DeviceGuard guard(s.device);
+    const bool lin_dev = lloc == LOC_DEVICE;
+    // HBM extents: always the kernel. Host-tier extents: the kernel below
+    // host_kernel_max (lower latency), the DMA engines above (higher peak).
+    const bool use_kernel = lin_dev && (a->any_gpu || s.host_engine_kernel || len <= s.host_kernel_max);
+    hipError_t err = hipSuccess;
+    // Small blocking ops go to the resident copy service (no launch, no stream sync).
+    if (lin_dev && a->all_dev_ok && !async && len <= s.svc_max) {
+        XferArgs x;
+        std::memset(&x, 0, sizeof(x));
+        x.lin = lin;
+        for (size_t i = 0; i < a->ext.size(); i++) x.ext[i] = a->ext[i].dptr;
+        x.n_ext = (uint32_t)a->ext.size();
+        x.rem_off = rem_off;
+        x.len = len;
+        x.put = put ? 1 : 0;
+        if (x.n_ext > 1) x.unit_shift = (uint32_t)log2_exact(a->stripe_unit);
+        if (wait_alloc(a) != 0) return -1;  // keep program order with queued async ops
+        if (honor_dep(a, nullptr, true) != 0) return -1;
+        if (service_xfer(x) == 0) return 0;
+        OCM_WARN("copy service failed (%s); falling back to launches", last_error());
+        s.svc_max = 0;
+    }
+    // Async ops queue on the allocation's lane; blocking ops on the library stream
+    // after the allocation's queued async work.
+    if (!async && wait_alloc(a) != 0) return -1;
+    hipStream_t st = async ? lane_stream(a) : s.stream;
+    if (honor_dep(a, st, false) != 0) return -1;
+    if (use_kernel) {
+        XferArgs x;
+        std::memset(&x, 0, sizeof(x));
+        x.lin = lin;
+        for (size_t i = 0; i < a->ext.size(); i++) x.ext[i] = a->ext[i].dptr;
+        x.n_ext = (uint32_t)a->ext.size();
+        x.rem_off = rem_off;
+        x.len = len;
+        x.put = put ? 1 : 0;
+        if (x.n_ext > 1) {
+            int sh = log2_exact(a->stripe_unit);
+            if (sh < 0) OCM_FAIL(-1, "stripe unit %llu is not a power of two", (unsigned long long)a->stripe_unit);
+            x.unit_shift = (uint32_t)sh;
+        }
+        XferTuning t = s.tuning;
+        if (t.variant == XFER_AUTO) {
+            // Measured (profiles/ksweep_r01.json): LDS-DMA staging wins HBM->HBM
+            // copies up to ~256 MiB on the same GPU; everything else (peer HBM
+            // over xGMI, host-mapped memory, huge copies) uses the register path.
+            bool same_gpu = lloc == LOC_DEVICE;
+            for (auto &e : a->ext) same_gpu &= e.r.tier == TIER_GPU && e.r.owner_gpu == s.device;
+            t.variant = (same_gpu && len <= (256ull << 20)) ? XFER_LDS : XFER_REG;
+        }
+        err = xfer_launch(x, t, st);
+    } else {
+        service_park();
+        segments(a, rem_off, len, segs);
+        for (auto &g : segs) {
+            const Extent &e = a->ext[g.ext];
+            char *r = (lloc == LOC_DEVICE || e.r.tier == TIER_GPU) ? e.dptr : e.hptr;
+            r += g.ext_off;
+            if (lloc != LOC_DEVICE && e.r.tier != TIER_GPU) {
+                // host <-> host tier: the CPU is the fastest engine.
+                if (put)
+                    std::memcpy(r, lin + g.lin_off, g.len);
+                else
+                    std::memcpy(lin + g.lin_off, r, g.len);
+                continue;
+            }
+            err = put ? hipMemcpyAsync(r, lin + g.lin_off, g.len, hipMemcpyDefault, st)
+                      : hipMemcpyAsync(lin + g.lin_off, r, g.len, hipMemcpyDefault, st);
+            if (err != hipSuccess) break;
+        }
+    }
+    if (err != hipSuccess) OCM_FAIL(-1, "transfer launch failed: %s", hipGetErrorString(err));
+    if (async) {
+        if (st != s.stream && a->ev) {
+            err = hipEventRecord(a->ev, st);
+            if (err != hipSuccess) OCM_FAIL(-1, "event record failed: %s", hipGetErrorString(err));
+        } else if (a->ev == nullptr && sync_stream() != 0) {
+            return -1;  // no lane available: complete it now
+        }
+        a->async_pending = a->ev != nullptr;
+        return 0;
+    }
+    return sync_stream();
+}
+
+// Copy between two process-local buffers.
+int copy_local(void *dst, Loc dl, const void *src, Loc sl, size_t n) {
+    State &s = S();
+    if (n == 0) return 0;
+    if (dl != LOC_DEVICE && sl != LOC_DEVICE) {
+        std::memcpy(dst, src, n);
+        return 0;
+    }
+    DeviceGuard g(s.device);
+    hipError_t e;
+    if (dl == LOC_DEVICE && sl == LOC_DEVICE) {
+        XferTuning t = s.tuning;
+        if (t.variant == XFER_AUTO) t.variant = n <= (256ull << 20) ? XFER_LDS : XFER_REG;
+        e = xfer_copy(dst, src, n, t, s.stream);
+    } else
+    {
+        e = hipMemcpyAsync(dst, src, n, hipMemcpyDefault, s.stream);
+    }
+    if (e != hipSuccess) OCM_FAIL(-1, "local copy failed: %s", hipGetErrorString(e));
+    return sync_stream();
+}
+
+
+}  // namespace ocmlib
