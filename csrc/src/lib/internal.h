@@ -27,6 +27,7 @@
 #include "ocm/msg.h"
 #include "ocm/netdata.h"
 #include "ocm/pmsg.h"
+#include "ocm/range_alloc.h"
 #include "ocm/sock.h"
 #include "ocm/trace.h"
 #include "ocm/xfer.h"
@@ -152,6 +153,8 @@ struct State {
     uint64_t pool_keep = 8ull << 30;       // bytes kept reserved across frees
     hipEvent_t done = nullptr;
     int rpc_timeout_ms = 60000;
+    uint64_t pinned_keep = 2ull << 30;     // idle pinned chunks kept for reuse
+    class PinnedArena *pinned = nullptr;   // created on first use
 };
 
 State &S();
@@ -186,6 +189,31 @@ inline int log2_exact(uint64_t v) {
 // ---- import cache (runtime.cpp)
 int import_extent(Extent &e);
 void release_extent(const Extent &e, bool force);
+
+// ---- pinned host arena for local halves (runtime.cpp)
+// hipHostMalloc pins pages (64 MiB ~ 10 ms) and hipHostFree synchronizes the
+// device (~230 us even for 4 KiB), so pinned local halves come from chunks
+// pinned once: small requests are best-fit ranges of shared 64 MiB chunks,
+// large ones get a dedicated chunk that is cached for reuse after free. Idle
+// chunks beyond OCM_PINNED_KEEP bytes (default 2 GiB) are unpinned.
+class PinnedArena {
+public:
+    void *alloc(size_t bytes);
+    bool free(void *p);  // false: not from this arena
+    void release_all();
+    uint64_t pinned() const { return pinned_; }
+
+private:
+    struct Chunk {
+        char *base = nullptr;
+        uint64_t bytes = 0;
+        bool dedicated = false;
+        RangeAllocator ra;
+    };
+    void trim();
+    std::map<uintptr_t, Chunk> chunks_;  // base -> chunk
+    uint64_t pinned_ = 0;
+};
 
 // ---- local halves (runtime.cpp)
 Loc pointer_loc(const void *p);

@@ -86,6 +86,7 @@ int ocm_init(void) {
     }
     s.sync_mode = env_int("OCM_SYNC_MODE", 1);
     s.n_lanes = env_int("OCM_ASYNC_LANES", 4);
+    if (const char *k = std::getenv("OCM_PINNED_KEEP")) s.pinned_keep = std::strtoull(k, nullptr, 0);
     if (const char *sm = std::getenv("OCM_SERVICE_MAX")) s.svc_max = std::strtoull(sm, nullptr, 0);
     s.tuning = xfer_tuning_from_env();
     const char *he = std::getenv("OCM_HOST_ENGINE");
@@ -141,6 +142,7 @@ int ocm_tini(void) {
         s.pool = nullptr;
     }
     s.pool_tried = false;
+    if (s.pinned) s.pinned->release_all();
     s.chan.close();
     s.inited = false;
     trace_flush("app");

@@ -205,6 +205,100 @@ hipMemPool_t local_pool() {
     return s.pool;
 }
 
+// ---------------------------------------------------------------- pinned arena
+
+namespace {
+constexpr uint64_t kPinnedChunk = 64ull << 20;
+constexpr uint64_t kPinnedAlign = 2ull << 20;
+PinnedArena &pinned_arena() {
+    State &s = S();
+    if (!s.pinned) s.pinned = new PinnedArena();
+    return *s.pinned;
+}
+}  // namespace
+
+void *PinnedArena::alloc(size_t bytes) {
+    State &s = S();
+    if (bytes == 0) return nullptr;
+    const bool big = bytes >= kPinnedChunk / 2;
+    if (!big) {
+        for (auto &kv : chunks_) {
+            Chunk &c = kv.second;
+            uint64_t off = 0;
+            if (!c.dedicated && c.ra.alloc(bytes, 4096, &off)) return c.base + off;
+        }
+    } else {
+        // A cached dedicated chunk of about this size (up to 2x) is reused as a whole.
+        Chunk *best = nullptr;
+        for (auto &kv : chunks_) {
+            Chunk &c = kv.second;
+            if (c.dedicated && c.ra.empty() && c.bytes >= bytes && c.bytes <= 2 * bytes &&
+                (!best || c.bytes < best->bytes))
+                best = &c;
+        }
+        uint64_t off = 0;
+        if (best && best->ra.alloc(bytes, 4096, &off)) return best->base + off;
+    }
+    const uint64_t size = big ? (bytes + kPinnedAlign - 1) & ~(kPinnedAlign - 1) : kPinnedChunk;
+    void *p = nullptr;
+    DeviceGuard g(s.device);
+    if (hipHostMalloc(&p, size, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        trim();  // give idle chunks back and try once more
+        if (hipHostMalloc(&p, size, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+    }
+    Chunk &c = chunks_[reinterpret_cast<uintptr_t>(p)];
+    c.base = static_cast<char *>(p);
+    c.bytes = size;
+    c.dedicated = big;
+    c.ra.reset(size);
+    pinned_ += size;
+    uint64_t off = 0;
+    c.ra.alloc(bytes, 4096, &off);
+    return c.base + off;
+}
+
+bool PinnedArena::free(void *ptr) {
+    const uintptr_t v = reinterpret_cast<uintptr_t>(ptr);
+    auto it = chunks_.upper_bound(v);
+    if (it == chunks_.begin()) return false;
+    --it;
+    Chunk &c = it->second;
+    if (v >= it->first + c.bytes) return false;
+    if (!c.ra.free(v - it->first)) return false;
+    if (c.ra.empty()) trim();
+    return true;
+}
+
+void PinnedArena::trim() {
+    State &s = S();
+    // Unpin idle chunks beyond the keep budget (largest first).
+    uint64_t idle = 0;
+    for (auto &kv : chunks_) idle += kv.second.ra.empty() ? kv.second.bytes : 0;
+    while (idle > s.pinned_keep) {
+        auto victim = chunks_.end();
+        for (auto it = chunks_.begin(); it != chunks_.end(); ++it)
+            if (it->second.ra.empty() && (victim == chunks_.end() || it->second.bytes > victim->second.bytes)) victim = it;
+        if (victim == chunks_.end()) break;
+        DeviceGuard g(s.device);
+        (void)hipHostFree(victim->second.base);
+        idle -= victim->second.bytes;
+        pinned_ -= victim->second.bytes;
+        chunks_.erase(victim);
+    }
+}
+
+void PinnedArena::release_all() {
+    State &s = S();
+    DeviceGuard g(s.device);
+    for (auto &kv : chunks_) (void)hipHostFree(kv.second.base);
+    chunks_.clear();
+    pinned_ = 0;
+}
+
 int free_local_half(lib_alloc *a) {
     State &s = S();
     if (!a->local) return 0;
@@ -217,8 +311,10 @@ int free_local_half(lib_alloc *a) {
         DeviceGuard g(s.device);
         (void)hipFree(a->local);
     } else if (a->loc == LOC_PINNED) {
-        DeviceGuard g(s.device);
-        (void)hipHostFree(a->local);
+        if (!pinned_arena().free(a->local)) {
+            DeviceGuard g(s.device);
+            (void)hipHostFree(a->local);
+        }
     } else {
         std::free(a->local);
     }
@@ -249,12 +345,8 @@ int alloc_local_half(lib_alloc *a, size_t bytes, Loc want) {
             OCM_FAIL(-1, "hipMalloc(%zu) for local half: %s", bytes, hipGetErrorString(e));
         }
     } else if (want == LOC_PINNED) {
-        DeviceGuard g(s.device);
-        hipError_t e = hipHostMalloc(&a->local, bytes, hipHostMallocDefault);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            OCM_FAIL(-1, "hipHostMalloc(%zu) for local half: %s", bytes, hipGetErrorString(e));
-        }
+        a->local = pinned_arena().alloc(bytes);
+        if (!a->local) OCM_FAIL(-1, "pinned host memory for a %zu-byte local half", bytes);
     } else {
         if (posix_memalign(&a->local, 4096, bytes) != 0) OCM_FAIL(-1, "host allocation of %zu bytes failed", bytes);
     }

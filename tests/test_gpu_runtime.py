@@ -5,6 +5,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import pytest
 import torch
@@ -228,3 +229,37 @@ def test_async_lanes_per_allocation(mesh_factory):
         assert c.lib.ocm_wait(None) == 0
         for a in allocs:
             a.free()
+
+
+def test_pinned_local_halves_are_pooled(mesh_factory):
+    # RDMA/RMA kinds keep their local half in pinned host memory; it comes from a
+    # per-process arena (shared 64 MiB chunks + cached dedicated chunks), so
+    # allocations must never overlap and freed ranges must be reused.
+    import random
+
+    m = mesh_factory(2, gpus=[0, 0])
+    rng = random.Random(5)
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        live = {}
+        seed = 100
+        for rnd in range(4):
+            for _ in range(12):
+                n = rng.choice([4096, 100_000, 1 << 20, 5 << 20, 40 << 20])
+                a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=n, remote_bytes=n)
+                seed += 1
+                a.fill(seed=seed)
+                live[seed] = (a, n)
+            for s, (a, n) in live.items():  # nothing overwrote anything
+                assert a.check(seed=s) == 0, (rnd, s, n)
+            for s in rng.sample(sorted(live), len(live) // 2):
+                live.pop(s)[0].free()
+        for s, (a, n) in list(live.items()):
+            a.put(0, 0, n)
+            a.fill(seed=0)
+            a.get(0, 0, n)
+            assert a.check(seed=s) == 0
+            a.free()
+        t0 = time.perf_counter()
+        for _ in range(20):  # a cached dedicated chunk: no re-pinning
+            c.alloc(api.OCM_REMOTE_RDMA, local_bytes=64 << 20, remote_bytes=1 << 20).free()
+        assert (time.perf_counter() - t0) / 20 < 2e-3

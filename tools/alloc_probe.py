@@ -24,9 +24,11 @@ def child(ns: str, samples: int) -> None:
 
     out = {}
     with api.Client(daemon_rank=0, gpu=0, ns=ns) as c:
-        for kind, name in ((api.OCM_LOCAL_GPU, "local_gpu"), (api.OCM_REMOTE_GPU, "remote_gpu")):
+        for kind, name in ((api.OCM_LOCAL_GPU, "local_gpu"), (api.OCM_REMOTE_GPU, "remote_gpu"),
+                           (api.OCM_REMOTE_RDMA, "remote_rdma_pinned_local")):
             for s in SIZES:
-                r = wl.alloc_latency(c, kind, samples, local_bytes=s, remote_bytes=s if kind == api.OCM_REMOTE_GPU else 0)
+                remote = s if kind != api.OCM_LOCAL_GPU else 0
+                r = wl.alloc_latency(c, kind, samples, local_bytes=s, remote_bytes=remote)
                 out[f"{name}_{s}"] = {k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()}
     print(json.dumps(out))
 
