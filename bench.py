@@ -33,6 +33,9 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+# (variant 1 register / 2 LDS-DMA, grid cap 0 = default, nontemporal stores)
+TUNING_GRID = {"reg_default": (1, 0, 1), "reg_b256": (1, 256, 1), "reg_b1024": (1, 1024, 1), "reg_b2048": (1, 2048, 1),
+               "reg_nt0": (1, 0, 0), "lds_default": (2, 0, 1), "lds_b512": (2, 512, 1)}
 METRIC = "remote put/get GiB/s + p50 ocm_alloc latency, 4 KiB-1 GiB, 1/2/4/8 MI355X"
 GiB = float(1 << 30)
 
@@ -50,6 +53,7 @@ def parse():
                     help="auto: governor placement; loopback: the rank's own daemon HBM (IPC); host: pinned host tier")
     ap.add_argument("--alloc-samples", type=int, default=200)
     ap.add_argument("--no-characterize", action="store_true")
+    ap.add_argument("--no-tuning-sweep", action="store_true", help="skip the N>1 xGMI tuning extras")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -193,6 +197,23 @@ def main() -> int:
                 p = max(c[s]["put_s"] for c in chs)
                 sweep[str(s)] = {"get_GiBps": round(world * s / g / GiB, 3), "put_GiBps": round(world * s / p / GiB, 3),
                                  "get_us": round(g * 1e6, 2), "put_us": round(p * 1e6, 2)}
+        # ---- xGMI tuning data (N > 1 only, after the timed region): every rank runs
+        # each variant at once, so the numbers are all-to-all under full load ----
+        tuning = {}
+        if use_gpu and world > 1 and not args.no_tuning_sweep:
+            n_t = min(256 << 20, max_bytes)
+            for name, (variant, blocks, nt) in TUNING_GRID.items():
+                api.set_tuning(variant, blocks, bool(nt))
+                if dist is not None:
+                    dist.barrier()
+                tp = pair.time_onesided(1, n_t, 3)
+                if dist is not None:
+                    dist.barrier()
+                tg = pair.time_onesided(0, n_t, 3)
+                res = gather_obj(dist, {"put": tp, "get": tg}, world)
+                tuning[name] = {"put_GiBps": round(world * n_t / max(r["put"] for r in res) / GiB, 2),
+                                "get_GiBps": round(world * n_t / max(r["get"] for r in res) / GiB, 2)}
+            api.set_tuning()
         pair.free()
         if dist is not None:
             dist.barrier()  # every rank is done with every owner before daemons stop
@@ -231,6 +252,8 @@ def main() -> int:
             "local_alloc_p50_us": round(max(s["lat_local"]["alloc_p50_us"] for s in stats), 2),
             "sweep": sweep,
         }
+        if tuning:
+            result["xgmi_tuning_256MiB"] = tuning
     finally:
         if client is not None:
             client.close()

@@ -572,6 +572,16 @@ void ocm_x_counters(uint64_t out[16]) {
     std::memcpy(out, v, sizeof(v));
 }
 
+// Transfer tuning at runtime (benchmarks): variant 0 auto / 1 reg / 2 lds,
+// blocks 0 = per-path default, nt = nontemporal destination stores.
+void ocm_x_set_tuning(int variant, int blocks, int nt) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    s.tuning.variant = variant;
+    s.tuning.max_blocks = blocks;
+    s.tuning.nontemporal = nt != 0;
+}
+
 void ocm_x_layout(uint64_t out[8]) {
     out[0] = sizeof(Msg);
     out[1] = sizeof(struct ocm_params);

@@ -171,6 +171,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_time_onesided": (ctypes.c_double, [vp, ctypes.POINTER(OcmParams), i32]),
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
+            "ocm_x_set_tuning": (None, [i32, i32, i32]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(lib, name)
@@ -260,6 +261,11 @@ def batch_ops(ops) -> BatchOps:
     for i, (flag, loff, roff, n) in enumerate(ops):
         arr[i] = OcmParams(loff, roff, 0, 0, n, flag)
     return BatchOps(arr, len(ops))
+
+
+def set_tuning(variant: int = 0, blocks: int = 0, nontemporal: bool = True) -> None:
+    """Transfer-kernel tuning for this process (0 auto / 1 register / 2 LDS-DMA; grid cap; nt stores)."""
+    load().ocm_x_set_tuning(variant, blocks, 1 if nontemporal else 0)
 
 
 def counters() -> dict:
