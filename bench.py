@@ -77,6 +77,81 @@ def gather_obj(dist, obj, world):
     return out
 
 
+
+def _local(fn):
+    """Run a rank-local measurement; (value, None) or (None, error string)."""
+    try:
+        return fn(), None
+    except Exception as e:  # noqa: BLE001 - recorded, never fatal
+        return None, repr(e)[:200]
+
+
+def xgmi_tuning_extras(pair, dist, world: int, max_bytes: int) -> dict:
+    """put/get GiB/s of each kernel configuration, all ranks at once (all-to-all load)."""
+    from oncilla_amd import api
+
+    n_t = min(256 << 20, max_bytes)
+    out = {}
+    for name, (variant, blocks, nt) in TUNING_GRID.items():
+        _, et = _local(lambda: api.set_tuning(variant, blocks, bool(nt)))
+        if dist is not None:
+            dist.barrier()
+        tp, ep = _local(lambda: pair.time_onesided(1, n_t, 3))
+        if dist is not None:
+            dist.barrier()
+        tg, eg = _local(lambda: pair.time_onesided(0, n_t, 3))
+        res = gather_obj(dist, {"put": tp, "get": tg, "err": et or ep or eg}, world)
+        errs = [r["err"] for r in res if r["err"]]
+        if errs:
+            out[name] = {"error": errs[0]}
+        else:
+            out[name] = {"put_GiBps": round(world * n_t / max(r["put"] for r in res) / GiB, 2),
+                         "get_GiBps": round(world * n_t / max(r["get"] for r in res) / GiB, 2)}
+    _local(lambda: api.set_tuning())
+    return out
+
+
+def hw_baseline_extras(dist, world: int, rank: int, local_rank: int) -> dict:
+    """The runtime's own peer copy (ring r -> r+1, all ranks at once) and rank 0's link table."""
+    import torch
+
+    from oncilla_amd import api
+
+    out = {}
+    peer = (local_rank + 1) % world
+    n_b = 256 << 20
+    visible = bool(_local(lambda: torch.cuda.device_count() >= world)[0])
+    bufs, err = _local(lambda: (torch.empty(n_b, dtype=torch.uint8, device=f"cuda:{local_rank}"),
+                                torch.empty(n_b, dtype=torch.uint8, device=f"cuda:{peer}")) if visible else None)
+
+    def run(reps):
+        src, dst = bufs
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(src)
+        torch.cuda.synchronize(local_rank)
+        torch.cuda.synchronize(peer)
+        return (time.perf_counter() - t0) / reps
+
+    if bufs:
+        _, err = _local(lambda: run(1))
+    if dist is not None:
+        dist.barrier()
+    tb = None
+    if bufs and not err:
+        tb, err = _local(lambda: run(3))
+    res = gather_obj(dist, {"t": tb, "err": err, "visible": visible}, world)
+    if all(r["visible"] for r in res):
+        errs = [r["err"] for r in res if r["err"]]
+        out["torch_peer_copy_ring_256MiB_GiBps"] = (
+            {"error": errs[0]} if errs else round(world * n_b / max(r["t"] for r in res) / GiB, 2))
+    if rank == 0:
+        links, _ = _local(lambda: {str(p): api.link_info(local_rank, p) for p in range(world) if p != local_rank})
+        if links:
+            out["links_from_rank0"] = links
+    del bufs
+    return out
+
 def main() -> int:
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -197,23 +272,13 @@ def main() -> int:
                 p = max(c[s]["put_s"] for c in chs)
                 sweep[str(s)] = {"get_GiBps": round(world * s / g / GiB, 3), "put_GiBps": round(world * s / p / GiB, 3),
                                  "get_us": round(g * 1e6, 2), "put_us": round(p * 1e6, 2)}
-        # ---- xGMI tuning data (N > 1 only, after the timed region): every rank runs
-        # each variant at once, so the numbers are all-to-all under full load ----
-        tuning = {}
+        # ---- extras for N > 1, after the timed region (never affect the metric) ----
+        # Every rank reaches every collective below even when its local part
+        # fails, so a failure is recorded instead of deadlocking the job.
+        tuning, baseline = {}, {}
         if use_gpu and world > 1 and not args.no_tuning_sweep:
-            n_t = min(256 << 20, max_bytes)
-            for name, (variant, blocks, nt) in TUNING_GRID.items():
-                api.set_tuning(variant, blocks, bool(nt))
-                if dist is not None:
-                    dist.barrier()
-                tp = pair.time_onesided(1, n_t, 3)
-                if dist is not None:
-                    dist.barrier()
-                tg = pair.time_onesided(0, n_t, 3)
-                res = gather_obj(dist, {"put": tp, "get": tg}, world)
-                tuning[name] = {"put_GiBps": round(world * n_t / max(r["put"] for r in res) / GiB, 2),
-                                "get_GiBps": round(world * n_t / max(r["get"] for r in res) / GiB, 2)}
-            api.set_tuning()
+            tuning = xgmi_tuning_extras(pair, dist, world, max_bytes)
+            baseline = hw_baseline_extras(dist, world, rank, local_rank)
         pair.free()
         if dist is not None:
             dist.barrier()  # every rank is done with every owner before daemons stop
@@ -254,6 +319,8 @@ def main() -> int:
         }
         if tuning:
             result["xgmi_tuning_256MiB"] = tuning
+        if baseline:
+            result["hw_baseline"] = baseline
     finally:
         if client is not None:
             client.close()

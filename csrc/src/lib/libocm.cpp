@@ -582,6 +582,15 @@ void ocm_x_set_tuning(int variant, int blocks, int nt) {
     s.tuning.nontemporal = nt != 0;
 }
 
+// Link type (hipExtLinkType) and hop count between two devices; -1 on error.
+int ocm_x_link_info(int dev, int peer, uint32_t *type, uint32_t *hops) {
+    if (hipExtGetLinkTypeAndHopCount(dev, peer, type, hops) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return 0;
+}
+
 void ocm_x_layout(uint64_t out[8]) {
     out[0] = sizeof(Msg);
     out[1] = sizeof(struct ocm_params);

@@ -172,6 +172,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
             "ocm_x_set_tuning": (None, [i32, i32, i32]),
+            "ocm_x_link_info": (i32, [i32, i32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(lib, name)
@@ -266,6 +267,14 @@ def batch_ops(ops) -> BatchOps:
 def set_tuning(variant: int = 0, blocks: int = 0, nontemporal: bool = True) -> None:
     """Transfer-kernel tuning for this process (0 auto / 1 register / 2 LDS-DMA; grid cap; nt stores)."""
     load().ocm_x_set_tuning(variant, blocks, 1 if nontemporal else 0)
+
+
+def link_info(dev: int, peer: int) -> Optional[dict]:
+    """xGMI/PCIe link type and hop count between two visible devices (hipExtGetLinkTypeAndHopCount)."""
+    t, h = ctypes.c_uint32(), ctypes.c_uint32()
+    if load().ocm_x_link_info(dev, peer, ctypes.byref(t), ctypes.byref(h)) != 0:
+        return None
+    return {"type": int(t.value), "hops": int(h.value)}
 
 
 def counters() -> dict:
