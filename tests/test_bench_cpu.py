@@ -38,3 +38,21 @@ def test_bench_multi_rank(native, n):
     res = _last_json(r.stdout)
     assert res["n_gpus"] == n and res["value"] > 0 and res["config"]["parallelism"] == f"stripe{n}"
     assert res["config"]["extents_per_pair"] == n - 1  # 8 MiB+1 pair = 9 stripe units: every peer gets one
+
+
+def test_bench_extras_helpers_run(native):
+    # The N>1 extras only run on multi-GPU nodes (the driver's scaling run):
+    # exercise their code here so a Python error cannot hide until then.
+    sys.path.insert(0, REPO)
+    import bench
+
+    class FakePair:
+        def time_onesided(self, op, n, iters):
+            return 1e-3
+
+    t = bench.xgmi_tuning_extras(FakePair(), None, 2, 1 << 20)
+    assert set(t) == set(bench.TUNING_GRID)
+    assert all("put_GiBps" in v and "error" not in v for v in t.values()), t
+    b = bench.hw_baseline_extras(None, 2, 0, 0)
+    assert isinstance(b, dict)
+    assert bench._local(lambda: 1 / 0)[1].startswith("ZeroDivisionError")
