@@ -1,0 +1,39 @@
+"""The examples/ programs run as documented (C example against a CPU mesh,
+Python quickstart on CPU and GPU, KV offload on GPU)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env=None, timeout=300):
+    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout, cwd="/tmp", env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def test_c_example_against_cpu_mesh(mesh_factory, native):
+    m = mesh_factory(2)
+    out = _run([f"{native}/ocm_example_hello", "4"], env=dict(m.client_env(0), OCM_NO_GPU="1"))
+    assert "round trip through rank 1" in out and "0 bad words" in out
+
+
+def test_quickstart_cpu(native):
+    out = _run([sys.executable, os.path.join(REPO, "examples", "quickstart.py")], env=dict(os.environ, OCM_NO_GPU="1"))
+    assert "round trip, striped over ranks [1, 2]" in out
+
+
+@pytest.mark.gpu
+def test_quickstart_gpu(native):
+    env = {k: v for k, v in os.environ.items() if k != "OCM_NO_GPU"}
+    out = _run([sys.executable, os.path.join(REPO, "examples", "quickstart.py"), "--gpu", "0"], env=env)
+    assert "round trip" in out
+
+
+@pytest.mark.gpu
+def test_kv_offload_example(native):
+    out = _run([sys.executable, os.path.join(REPO, "examples", "kv_offload.py")])
+    assert "64 KV blocks swapped out and back" in out
