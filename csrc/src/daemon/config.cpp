@@ -25,6 +25,27 @@
 namespace ocm {
 using namespace dm;
 
+static const char *kUsage =
+    "usage: ocmd <nodefile> [options]            (one daemon per GPU; rank 0 is the master)\n"
+    "  --rank R                 this daemon's nodefile line (default: OCM_RANK / LOCAL_RANK / hostname)\n"
+    "  --gpu G|none             device ordinal (default: gpu= column, else rank % visible GPUs)\n"
+    "  --ns NS                  mailbox namespace, several meshes per host      [OCM_NS]\n"
+    "  --policy P               ring | least_loaded | stripe | loopback        [OCM_PLACEMENT]\n"
+    "  --stripe-unit B          default stripe unit (power of two)             [OCM_STRIPE_UNIT]\n"
+    "  --slab-bytes B           HBM slab size (default 4G)                       [OCM_SLAB_BYTES]\n"
+    "  --gpu-capacity B         HBM this daemon may hand out (default 75% free) [OCM_GPU_CAPACITY]\n"
+    "  --host-capacity B        host-tier bytes (default 25% MemAvailable)      [OCM_HOST_CAPACITY]\n"
+    "  --ctrl tcp|rccl|socket   daemon<->daemon record transport               [OCM_CTRL]\n"
+    "  --lease-bytes B          capacity lease chunk (0 = off, default 1G)      [OCM_LEASE_BYTES]\n"
+    "  --state-file PATH        rank0 directory checkpoint (resume)            [OCM_STATE_FILE]\n"
+    "  --host-alias NAME        node name to report (emulate several nodes)    [OCM_HOST_ALIAS]\n"
+    "  --bind IP                listen address (default 0.0.0.0)\n"
+    "  --join-timeout-ms MS     how long to wait for rank0\n"
+    "  --ready-file PATH        written once the mesh is complete\n"
+    "  --watch-pid PID          exit when this process exits\n"
+    "  --zero                   zero memory on allocation                      [OCM_ZERO_ON_ALLOC]\n"
+    "sizes accept K/M/G/T suffixes; OCM_MESH_KEY sets the mesh authentication secret";
+
 int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err) {
     auto env = [](const char *k) -> const char * {
         const char *v = std::getenv(k);
@@ -51,6 +72,10 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
     if (const char *v = env("OCM_STATE_INTERVAL_MS")) cfg->state_interval_ms = std::atoi(v);
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
+        if (a == "-h" || a == "--help") {
+            *err = kUsage;
+            return 1;
+        }
         auto val = [&](std::string *out) {
             if (i + 1 >= argc) {
                 *err = "missing value for " + a;
@@ -116,7 +141,7 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
         }
     }
     if (cfg->nodefile.empty()) {
-        *err = "usage: ocmd <nodefile> [--rank R] [--gpu G|none] [--ns NS] [--policy ring|least_loaded|stripe|loopback]";
+        *err = kUsage;
         return -1;
     }
     if (cfg->ns.empty()) cfg->ns = pmsg_namespace();

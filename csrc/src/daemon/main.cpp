@@ -10,7 +10,12 @@
 int main(int argc, char **argv) {
     ocm::DaemonConfig cfg;
     std::string err;
-    if (ocm::parse_daemon_args(argc, argv, &cfg, &err) != 0) {
+    const int rc = ocm::parse_daemon_args(argc, argv, &cfg, &err);
+    if (rc > 0) {  // --help
+        std::printf("%s\n", err.c_str());
+        return 0;
+    }
+    if (rc != 0) {
         std::fprintf(stderr, "%s\n", err.c_str());
         return 2;
     }
