@@ -14,6 +14,7 @@ struct OpCounters {
     uint64_t n_alloc = 0, n_free = 0, n_copy = 0, bytes_copy = 0;
     uint64_t ns_put = 0, ns_get = 0, ns_alloc = 0, ns_free = 0;
     uint64_t n_batch = 0, n_batch_ops = 0, bytes_batch = 0, ns_batch = 0;
+    uint64_t n_batch_launches = 0;  // batch kernels launched outside plans (batches, remote->remote copies)
 };
 
 bool trace_enabled();  // OCM_TRACE=0 disables the roctx ranges

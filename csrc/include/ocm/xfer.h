@@ -82,7 +82,7 @@ struct XferBatchArgs {
     uint32_t n_ops;
     uint64_t total_tiles;
     uint32_t grid;                        // workgroups (4 waves each)
-    uint32_t pad;
+    uint32_t abs_lin;                     // 1: op.lin_off is an absolute device address (lin unused)
     const XferBatchOp *ops;               // device copy when n_ops > kXferInlineOps
     const uint32_t *wave_op;              // device: first op of each wave (n_ops > kXferInlineOps)
     XferBatchOp inline_ops[kXferInlineOps];

@@ -327,8 +327,9 @@ __global__ __launch_bounds__(kThreads) void xfer_batch_kernel(XferBatchArgs a) {
     for (; t < t1; t++) {
         while (i + 1 < a.n_ops && ops[i + 1].first_tile <= t) i++;
         const XferBatchOp &op = ops[i];
-        TileSpan sp = tile_span_of(a, a.n_ext, a.unit_shift, a.tile_shift, a.lin + op.lin_off, op.rem_off, op.len,
-                                   op.put, t - op.first_tile, op.rem_off & ~tile_mask);
+        char *lin = a.abs_lin ? reinterpret_cast<char *>(static_cast<uintptr_t>(op.lin_off)) : a.lin + op.lin_off;
+        TileSpan sp = tile_span_of(a, a.n_ext, a.unit_shift, a.tile_shift, lin, op.rem_off, op.len, op.put,
+                                   t - op.first_tile, op.rem_off & ~tile_mask);
         wave_copy<NT>(sp.dst, sp.src, sp.n, lane);
     }
 }

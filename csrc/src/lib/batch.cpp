@@ -6,20 +6,24 @@
 using namespace ocm;
 using namespace ocmlib;
 
-extern "C" {
-
-static int batch_impl(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, int flags, uint64_t *moved);
-
-// Batch launch arguments for `ops` on `a` (descriptors in `v`; inline ones copied into args).
-static void build_batch_args(lib_alloc *a, const struct ocm_params *ops, int n_ops, XferBatchArgs *args,
-                             std::vector<XferBatchOp> *v) {
+// Launch geometry of a batch on `a` for the descriptors in `v` (first_tile filled in).
+static void plan_batch_args(lib_alloc *a, std::vector<XferBatchOp> &v, bool abs_lin, XferBatchArgs *args) {
     std::memset(args, 0, sizeof(*args));
-    args->lin = static_cast<char *>(a->local);
+    args->lin = abs_lin ? nullptr : static_cast<char *>(a->local);
+    args->abs_lin = abs_lin ? 1 : 0;
     for (size_t i = 0; i < a->ext.size(); i++) args->ext[i] = a->ext[i].dptr;
     args->n_ext = (uint32_t)a->ext.size();
     args->unit_shift = args->n_ext > 1 ? (uint32_t)log2_exact(a->stripe_unit) : 0;
     args->tile_shift = xfer_batch_tile_shift(args->n_ext, args->unit_shift);
-    args->n_ops = (uint32_t)n_ops;
+    args->n_ops = (uint32_t)v.size();
+    args->total_tiles = xfer_batch_plan(v.data(), (uint32_t)v.size(), args->tile_shift);
+    args->grid = args->total_tiles ? xfer_batch_grid(args->total_tiles) : 0;
+    if (v.size() <= (size_t)kXferInlineOps) std::memcpy(args->inline_ops, v.data(), v.size() * sizeof(XferBatchOp));
+}
+
+// Batch launch arguments for `ops` on `a` (descriptors in `v`; inline ones copied into args).
+static void build_batch_args(lib_alloc *a, const struct ocm_params *ops, int n_ops, XferBatchArgs *args,
+                             std::vector<XferBatchOp> *v) {
     v->assign((size_t)n_ops, XferBatchOp{});
     for (int i = 0; i < n_ops; i++) {
         (*v)[i].lin_off = ops[i].src_offset;
@@ -27,9 +31,7 @@ static void build_batch_args(lib_alloc *a, const struct ocm_params *ops, int n_o
         (*v)[i].len = ops[i].bytes;
         (*v)[i].put = ops[i].op_flag != 0;
     }
-    args->total_tiles = xfer_batch_plan(v->data(), (uint32_t)n_ops, args->tile_shift);
-    args->grid = args->total_tiles ? xfer_batch_grid(args->total_tiles) : 0;
-    if (n_ops <= kXferInlineOps) std::memcpy(args->inline_ops, v->data(), v->size() * sizeof(XferBatchOp));
+    plan_batch_args(a, *v, false, args);
 }
 
 // Bounds of every op against the pair (as ocm_copy_onesided). Adds the bytes to *moved.
@@ -54,6 +56,79 @@ static bool batch_device_path(const lib_alloc *a) {
            (a->ext.size() == 1 || log2_exact(a->stripe_unit) >= 4);
 }
 
+namespace ocmlib {
+
+// Upload (large lists), launch and complete one batch on `a`. `args` from plan_batch_args.
+int run_batch(lib_alloc *a, XferBatchArgs &args, std::vector<XferBatchOp> &v, bool async) {
+    State &s = S();
+    DeviceGuard guard(s.device);
+    if (!async && wait_alloc(a) != 0) return -1;
+    hipStream_t st = async ? lane_stream(a) : s.stream;
+    if (honor_dep(a, st, false) != 0) return -1;
+    hipError_t err = hipSuccess;
+    const size_t n_ops = v.size();
+    if (n_ops > (size_t)kXferInlineOps) {
+        // descriptors, then the per-wave starting ops, in one upload
+        const size_t dbytes = v.size() * sizeof(XferBatchOp);
+        const size_t need = dbytes + (size_t)args.grid * 4 * sizeof(uint32_t);
+        if (a->batch_up && hipEventSynchronize(a->batch_up) != hipSuccess)  // staging free again
+            OCM_FAIL(-1, "batch staging wait failed");
+        if (a->batch_cap < need) {
+            if (a->batch_dev) (void)hipFreeAsync(a->batch_dev, st);
+            if (a->batch_host) (void)hipHostFree(a->batch_host);
+            a->batch_dev = a->batch_host = nullptr;
+            a->batch_cap = 0;
+            const size_t cap = std::max<size_t>(need, 64 << 10);
+            err = local_pool() ? hipMallocFromPoolAsync(&a->batch_dev, cap, s.pool, st) : hipMallocAsync(&a->batch_dev, cap, st);
+            if (err == hipSuccess) err = hipHostMalloc(&a->batch_host, cap, hipHostMallocDefault);
+            if (err == hipSuccess && !a->batch_up) err = hipEventCreateWithFlags(&a->batch_up, hipEventDisableTiming);
+            if (err != hipSuccess) {
+                (void)hipGetLastError();
+                OCM_FAIL(-1, "batch descriptors: %s", hipGetErrorString(err));
+            }
+            a->batch_cap = cap;
+        }
+        char *up = static_cast<char *>(a->batch_host);
+        std::memcpy(up, v.data(), dbytes);
+        xfer_batch_wave_ops(v.data(), (uint32_t)n_ops, args.total_tiles, args.grid, reinterpret_cast<uint32_t *>(up + dbytes));
+        // Pinned source: a real async DMA; batch_up tells the next batch when `up` is free.
+        err = hipMemcpyAsync(a->batch_dev, up, need, hipMemcpyHostToDevice, st);
+        if (err == hipSuccess) err = hipEventRecord(a->batch_up, st);
+        if (err != hipSuccess) OCM_FAIL(-1, "batch descriptor upload: %s", hipGetErrorString(err));
+        args.ops = static_cast<const XferBatchOp *>(a->batch_dev);
+        args.wave_op = reinterpret_cast<const uint32_t *>(static_cast<char *>(a->batch_dev) + dbytes);
+    }
+    err = xfer_batch_launch(args, s.tuning, st);
+    if (err != hipSuccess) OCM_FAIL(-1, "batch launch failed: %s", hipGetErrorString(err));
+    s.ctr.n_batch_launches++;
+    if (async) {
+        if (st != s.stream && a->ev) {
+            err = hipEventRecord(a->ev, st);
+            if (err != hipSuccess) OCM_FAIL(-1, "event record failed: %s", hipGetErrorString(err));
+            a->async_pending = true;
+            return 0;
+        }
+    }
+    return sync_stream();
+}
+
+// Remote -> remote copies: every op's linear side is an absolute device address
+// (a source extent), written into `dst`'s remote half by one launch.
+int batch_put_abs(lib_alloc *dst, std::vector<XferBatchOp> &v) {
+    if (v.empty()) return 0;
+    XferBatchArgs args;
+    plan_batch_args(dst, v, true, &args);
+    if (args.total_tiles == 0) return 0;
+    return run_batch(dst, args, v, false);
+}
+
+}  // namespace ocmlib
+
+extern "C" {
+
+static int batch_impl(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, int flags, uint64_t *moved);
+
+// Batch launch arguments for `ops` on `a` (descriptors in `v`; inline ones copied into args).
 int ocm_copy_onesided_batch(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, int flags) {
     TraceRange tr("ocm_batch");
     const uint64_t t0 = now_ns();
@@ -94,52 +169,7 @@ static int batch_impl(ocm_alloc_t a, const struct ocm_params *ops, int n_ops, in
     std::vector<XferBatchOp> v;
     build_batch_args(a, ops, n_ops, &args, &v);
     if (args.total_tiles == 0) return 0;  // only empty ops
-    if (!async && wait_alloc(a) != 0) return -1;
-    hipStream_t st = async ? lane_stream(a) : s.stream;
-    if (honor_dep(a, st, false) != 0) return -1;
-    hipError_t err = hipSuccess;
-    if (n_ops > kXferInlineOps) {
-        // descriptors, then the per-wave starting ops, in one upload
-        const size_t dbytes = v.size() * sizeof(XferBatchOp);
-        const size_t need = dbytes + (size_t)args.grid * 4 * sizeof(uint32_t);
-        if (a->batch_up && hipEventSynchronize(a->batch_up) != hipSuccess)  // staging free again
-            OCM_FAIL(-1, "batch staging wait failed");
-        if (a->batch_cap < need) {
-            if (a->batch_dev) (void)hipFreeAsync(a->batch_dev, st);
-            if (a->batch_host) (void)hipHostFree(a->batch_host);
-            a->batch_dev = a->batch_host = nullptr;
-            a->batch_cap = 0;
-            const size_t cap = std::max<size_t>(need, 64 << 10);
-            err = local_pool() ? hipMallocFromPoolAsync(&a->batch_dev, cap, s.pool, st) : hipMallocAsync(&a->batch_dev, cap, st);
-            if (err == hipSuccess) err = hipHostMalloc(&a->batch_host, cap, hipHostMallocDefault);
-            if (err == hipSuccess && !a->batch_up) err = hipEventCreateWithFlags(&a->batch_up, hipEventDisableTiming);
-            if (err != hipSuccess) {
-                (void)hipGetLastError();
-                OCM_FAIL(-1, "batch descriptors: %s", hipGetErrorString(err));
-            }
-            a->batch_cap = cap;
-        }
-        char *up = static_cast<char *>(a->batch_host);
-        std::memcpy(up, v.data(), dbytes);
-        xfer_batch_wave_ops(v.data(), (uint32_t)n_ops, args.total_tiles, args.grid, reinterpret_cast<uint32_t *>(up + dbytes));
-        // Pinned source: a real async DMA; batch_up tells the next batch when `up` is free.
-        err = hipMemcpyAsync(a->batch_dev, up, need, hipMemcpyHostToDevice, st);
-        if (err == hipSuccess) err = hipEventRecord(a->batch_up, st);
-        if (err != hipSuccess) OCM_FAIL(-1, "batch descriptor upload: %s", hipGetErrorString(err));
-        args.ops = static_cast<const XferBatchOp *>(a->batch_dev);
-        args.wave_op = reinterpret_cast<const uint32_t *>(static_cast<char *>(a->batch_dev) + dbytes);
-    }
-    err = xfer_batch_launch(args, s.tuning, st);
-    if (err != hipSuccess) OCM_FAIL(-1, "batch launch failed: %s", hipGetErrorString(err));
-    if (async) {
-        if (st != s.stream && a->ev) {
-            err = hipEventRecord(a->ev, st);
-            if (err != hipSuccess) OCM_FAIL(-1, "event record failed: %s", hipGetErrorString(err));
-            a->async_pending = true;
-            return 0;
-        }
-    }
-    return sync_stream();
+    return run_batch(a, args, v, async);
 }
 
 int ocm_stream_wait(ocm_alloc_t a, void *stream) {

@@ -241,6 +241,11 @@ int service_xfer(XferArgs x);
 int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async);
 int copy_local(void *dst, Loc dl, const void *src, Loc sl, size_t n);
 
+// ---- batches (batch.cpp)
+int run_batch(lib_alloc *a, XferBatchArgs &args, std::vector<XferBatchOp> &v, bool async);
+// Copy absolute device ranges (op.lin_off = address) into dst's remote half, one launch.
+int batch_put_abs(lib_alloc *dst, std::vector<XferBatchOp> &v);
+
 // ---- network tier (net.cpp)
 int net_conn(const std::string &ep, uint64_t token);
 void net_drop(const std::string &ep);

@@ -471,6 +471,20 @@ static int copy_impl(ocm_alloc_t dst, ocm_alloc_t src, ocm_param_t p) {
     }
     std::vector<Seg> ss;
     segments(src, q.src_offset, n, ss);
+    const bool one_launch = s.device >= 0 && src->all_dev_ok && dst->all_dev_ok &&
+                            (dst->ext.size() == 1 || log2_exact(dst->stripe_unit) >= 4);
+    if (one_launch) {
+        // Every source segment is a device address: one batched launch writes them all.
+        std::vector<XferBatchOp> v(ss.size());
+        for (size_t i = 0; i < ss.size(); i++) {
+            const Seg &g = ss[i];
+            v[i].lin_off = reinterpret_cast<uintptr_t>(src->ext[g.ext].dptr + g.ext_off);
+            v[i].rem_off = q.dest_offset + g.lin_off;
+            v[i].len = g.len;
+            v[i].put = 1;
+        }
+        return batch_put_abs(dst, v);
+    }
     for (auto &g : ss) {
         const Extent &e = src->ext[g.ext];
         char *sp = (s.device >= 0 ? e.dptr : e.hptr) + g.ext_off;
@@ -563,12 +577,12 @@ const char *ocm_last_error(void) { return last_error(); }
 
 // ---------------- internal hooks for tests and benchmarks (not part of the ABI) ----------------
 
-// Per-process operation counters (see ocm/trace.h): 16 x uint64.
-void ocm_x_counters(uint64_t out[16]) {
+// Per-process operation counters (see ocm/trace.h): 17 x uint64.
+void ocm_x_counters(uint64_t out[17]) {
     const OpCounters &c = S().ctr;
-    const uint64_t v[16] = {c.n_put,  c.n_get,    c.bytes_put, c.bytes_get,   c.n_alloc,     c.n_free,
+    const uint64_t v[17] = {c.n_put,  c.n_get,    c.bytes_put, c.bytes_get,   c.n_alloc,     c.n_free,
                             c.n_copy, c.bytes_copy, c.ns_put,  c.ns_get,      c.ns_alloc,    c.ns_free,
-                            c.n_batch, c.n_batch_ops, c.bytes_batch, c.ns_batch};
+                            c.n_batch, c.n_batch_ops, c.bytes_batch, c.ns_batch, c.n_batch_launches};
     std::memcpy(out, v, sizeof(v));
 }
 

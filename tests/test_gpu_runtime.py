@@ -263,3 +263,25 @@ def test_pinned_local_halves_are_pooled(mesh_factory):
         for _ in range(20):  # a cached dedicated chunk: no re-pinning
             c.alloc(api.OCM_REMOTE_RDMA, local_bytes=64 << 20, remote_bytes=1 << 20).free()
         assert (time.perf_counter() - t0) / 20 < 2e-3
+
+
+def test_remote_to_remote_copy_one_launch(mesh_factory):
+    # ocm_copy between two striped pairs with different stripe units and offsets:
+    # every source segment becomes one descriptor of a single batched launch.
+    m = mesh_factory(4, gpus=[0, 0, 0, 0], policy="stripe")
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 24 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, stripe_unit=64 << 10)
+        b = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, stripe_unit=256 << 10)
+        a.fill(seed=31)
+        a.put(0, 0, n)
+        before = api.counters()["n_batch_launches"]
+        k = (16 << 20) + 4096
+        api.copy(b, a, k, src_offset=12288, dest_offset=4096)  # b.remote[4096:] <- a.remote[12288:]
+        assert api.counters()["n_batch_launches"] == before + 1  # one launch, not one per 64 KiB segment
+        b.fill(seed=0)
+        b.get(4096, 4096, k)
+        # a.local held pattern words from offset 0; a.remote[12288 + i] == pattern word (12288 + i) / 4
+        assert b.check(seed=31, offset=4096, nbytes=k, first_word=12288 // 4) == 0
+        a.free()
+        b.free()
