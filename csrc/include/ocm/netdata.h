@@ -10,6 +10,7 @@
 // Extents reached this way carry REGION_NET and "net:<ip>:<port>:<token>" as handle.
 #pragma once
 #include <atomic>
+#include <memory>
 #include <cstdint>
 #include <mutex>
 #include <string>
@@ -59,9 +60,15 @@ private:
     int listen_fd_ = -1, port_ = 0;
     std::atomic<bool> stop_{false};
     std::thread acceptor_;
+    struct Worker {
+        std::thread th;
+        std::shared_ptr<std::atomic<bool>> done;
+    };
+    void reap();  // join workers whose connection ended (under mu_)
     std::mutex mu_;
-    std::vector<std::thread> workers_;
+    std::vector<Worker> workers_;
     std::vector<int> conns_;
+    static constexpr size_t kMaxConns = 1024;
 };
 
 // "net:<ip>:<port>:<token hex>"

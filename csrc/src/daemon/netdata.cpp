@@ -53,8 +53,9 @@ void DataServer::stop() {
         std::lock_guard<std::mutex> lk(mu_);
         for (int fd : conns_) shutdown(fd, SHUT_RDWR);
     }
-    for (auto &t : workers_)
-        if (t.joinable()) t.join();
+    for (auto &w : workers_)
+        if (w.th.joinable()) w.th.join();
+    workers_.clear();
     close(listen_fd_);
     listen_fd_ = -1;
 }
@@ -67,8 +68,30 @@ void DataServer::accept_loop() {
         int fd = tcp_accept(listen_fd_);
         if (fd < 0) continue;
         std::lock_guard<std::mutex> lk(mu_);
+        reap();
+        if (conns_.size() >= kMaxConns) {
+            OCM_WARN("data server: %zu connections open, refusing another", conns_.size());
+            close(fd);
+            continue;
+        }
         conns_.push_back(fd);
-        workers_.emplace_back([this, fd] { serve(fd); });
+        auto done = std::make_shared<std::atomic<bool>>(false);
+        workers_.push_back(Worker{std::thread([this, fd, done] {
+                                      serve(fd);
+                                      done->store(true);
+                                  }),
+                                  done});
+    }
+}
+
+void DataServer::reap() {
+    for (auto it = workers_.begin(); it != workers_.end();) {
+        if (it->done->load()) {
+            it->th.join();
+            it = workers_.erase(it);
+        } else {
+            ++it;
+        }
     }
 }
 

@@ -181,3 +181,26 @@ def test_data_server_requires_token(mesh_factory):
         a.get(0, 0, 1 << 20)
         assert a.check(seed=3) == 0
         a.free()
+
+
+def test_data_server_reaps_connections(mesh_factory):
+    # Short-lived connections (scanners, reconnecting apps) must not pile up threads.
+    m = mesh_factory(2, rank_env={0: {"OCM_HOST_ALIAS": "A"}, 1: {"OCM_HOST_ALIAS": "B"}})
+    port = m.ready_info()[1]["data_port"]
+    pid = m.daemons[1].proc.pid
+
+    def threads():
+        for line in open(f"/proc/{pid}/status"):
+            if line.startswith("Threads:"):
+                return int(line.split()[1])
+
+    base = threads()
+    for _ in range(300):
+        s = socket.create_connection(("127.0.0.1", port), timeout=5)
+        s.sendall(b"\0" * 8)  # wrong token: the server drops it
+        s.close()
+    s = socket.create_connection(("127.0.0.1", port), timeout=5)  # one more accept triggers the reaping
+    s.close()
+    time.sleep(0.3)
+    assert threads() <= base + 3, (base, threads())
+    assert m.daemons[1].alive()
