@@ -642,6 +642,57 @@ int ocm_x_xfer(int device, void *lin, void **ext, int n_ext, uint64_t unit, uint
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
+// Batched transfer between raw device pointers (kernel numerics tests / PMC
+// profiles without daemons). ops: n x {lin_off, rem_off, len, put} (u64 each).
+// Returns 0, or -1 on bad arguments; iters > 1 repeats the launch (profiling).
+int ocm_x_batch(int device, void *lin, void **ext, int n_ext, uint64_t unit, const uint64_t *ops, int n_ops, int iters) {
+    if (n_ext < 1 || n_ext > kXferMaxExtents || n_ops < 1 || !ops) return -1;
+    DeviceGuard g(device);
+    XferBatchArgs args;
+    std::memset(&args, 0, sizeof(args));
+    args.lin = static_cast<char *>(lin);
+    for (int i = 0; i < n_ext; i++) args.ext[i] = static_cast<char *>(ext[i]);
+    args.n_ext = (uint32_t)n_ext;
+    if (n_ext > 1) {
+        const int sh = log2_exact(unit);
+        if (sh < 4) return -1;
+        args.unit_shift = (uint32_t)sh;
+    }
+    args.tile_shift = xfer_batch_tile_shift(args.n_ext, args.unit_shift);
+    std::vector<XferBatchOp> v((size_t)n_ops);
+    for (int i = 0; i < n_ops; i++) {
+        v[i].lin_off = ops[4 * i];
+        v[i].rem_off = ops[4 * i + 1];
+        v[i].len = ops[4 * i + 2];
+        v[i].put = ops[4 * i + 3] != 0;
+    }
+    args.n_ops = (uint32_t)n_ops;
+    args.total_tiles = xfer_batch_plan(v.data(), (uint32_t)n_ops, args.tile_shift);
+    if (!args.total_tiles) return 0;
+    args.grid = xfer_batch_grid(args.total_tiles);
+    void *dev = nullptr;
+    if (n_ops <= kXferInlineOps) {
+        std::memcpy(args.inline_ops, v.data(), v.size() * sizeof(XferBatchOp));
+    } else {
+        const size_t dbytes = v.size() * sizeof(XferBatchOp), need = dbytes + (size_t)args.grid * 16;
+        std::vector<char> up(need);
+        std::memcpy(up.data(), v.data(), dbytes);
+        xfer_batch_wave_ops(v.data(), (uint32_t)n_ops, args.total_tiles, args.grid,
+                            reinterpret_cast<uint32_t *>(up.data() + dbytes));
+        if (hipMalloc(&dev, need) != hipSuccess || hipMemcpy(dev, up.data(), need, hipMemcpyHostToDevice) != hipSuccess)
+            return -1;
+        args.ops = static_cast<const XferBatchOp *>(dev);
+        args.wave_op = reinterpret_cast<const uint32_t *>(static_cast<char *>(dev) + dbytes);
+    }
+    XferTuning t = xfer_tuning_from_env();
+    int rc = 0;
+    for (int k = 0; k < std::max(1, iters) && rc == 0; k++)
+        rc = xfer_batch_launch(args, t, nullptr) == hipSuccess ? 0 : -1;
+    if (hipDeviceSynchronize() != hipSuccess) rc = -1;
+    if (dev) (void)hipFree(dev);
+    return rc;
+}
+
 // Time `iters` back-to-back device copies (seconds per copy, event-timed).
 double ocm_x_time_device_copy(int device, void *dst, const void *src, uint64_t bytes, int variant, int blocks,
                               int nt, int iters) {

@@ -172,6 +172,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
             "ocm_x_set_tuning": (None, [i32, i32, i32]),
+            "ocm_x_batch": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, ctypes.POINTER(u64), i32, i32]),
             "ocm_x_link_info": (i32, [i32, i32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
         }
         for name, (res, args) in sigs.items():

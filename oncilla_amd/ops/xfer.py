@@ -58,3 +58,18 @@ def device_copy_seconds(dst, src, nbytes: int, variant: int = XFER_REG, blocks: 
     lib = api.load()
     return lib.ocm_x_time_device_copy(dst.device.index or 0, ctypes.c_void_p(_ptr(dst)), ctypes.c_void_p(_ptr(src)),
                                       nbytes, variant, blocks, 1 if nontemporal else 0, iters)
+
+
+def batch(lin, exts: list, unit: int, ops, iters: int = 1) -> None:
+    """Batched one-sided ops between device tensors with the gfx950 batch kernel
+    (no daemons): ops = [(put, lin_off, rem_off, nbytes)], remote side striped
+    over `exts` in `unit`-byte units (the libocm layout)."""
+    lib = api.load()
+    n = len(exts)
+    arr = (ctypes.c_void_p * n)(*[_ptr(e) for e in exts])
+    flat = (ctypes.c_uint64 * (4 * max(1, len(ops))))()
+    for i, (put, lo, ro, nb) in enumerate(ops):
+        flat[4 * i:4 * i + 4] = [lo, ro, nb, 1 if put else 0]
+    rc = lib.ocm_x_batch(lin.device.index or 0, ctypes.c_void_p(_ptr(lin)), arr, n, unit, flat, len(ops), iters)
+    if rc != 0:
+        raise api.OcmError("ocm_x_batch failed")

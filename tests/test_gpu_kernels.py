@@ -65,3 +65,50 @@ def test_copy_bandwidth_sane():
     t = ops.device_copy_seconds(b, a, n, iters=5)
     gbps = 2 * n / t / 1e9  # read + write
     assert gbps > 1000, f"HBM copy only {gbps:.0f} GB/s"
+
+
+def _disjoint_ranges(rng, space, lens):
+    """Random disjoint placement of ranges with the given lengths inside [0, space)."""
+    n = len(lens)
+    slack = space - sum(lens)
+    assert slack >= 0
+    cuts = sorted(rng.randint(0, slack) for _ in range(n))
+    order = list(range(n))
+    rng.shuffle(order)
+    offs, pos, prev = [0] * n, 0, 0
+    for k, i in enumerate(order):
+        pos += cuts[k] - prev
+        prev = cuts[k]
+        offs[i] = pos
+        pos += lens[i]
+    return offs
+
+
+@pytest.mark.parametrize("n_ext,unit,n_ops,max_len", [(1, 0, 1, 100000), (1, 0, 48, 9000), (3, 4096, 49, 9000),
+                                                      (3, 65536, 700, 3000), (7, 1 << 20, 2000, 1500),
+                                                      (8, 32768, 64, 70000), (2, 16, 300, 100)])
+def test_batch_kernel_matches_reference(n_ext, unit, n_ops, max_len):
+    # Mixed puts/gets with unaligned sizes and offsets; local ranges disjoint and
+    # remote ranges disjoint, so every op reads initial data and order is irrelevant.
+    import random
+
+    rng = random.Random(n_ops * 31 + n_ext)
+    total = 8 << 20
+    ext_len = total if n_ext == 1 else ((total // unit) // n_ext + 2) * unit
+    exts = [_rand(ext_len, 500 + i) for i in range(n_ext)]
+    lin = _rand(total, 9)
+    lens = [rng.randint(1, max_len) for _ in range(n_ops)]
+    loffs, roffs = _disjoint_ranges(rng, total, lens), _disjoint_ranges(rng, total, lens)
+    ops_list = [(rng.random() < 0.5, loffs[i], roffs[i], lens[i]) for i in range(n_ops)]
+    lin0, exts0 = lin.clone(), [e.clone() for e in exts]
+    ref_lin, ref_exts = lin.clone(), [e.clone() for e in exts]
+    for put, lo, ro, nb in ops_list:
+        if put:
+            ops.striped_reference(lin0[lo:], ref_exts, unit, ro, nb, put=True)
+        else:
+            ops.striped_reference(ref_lin[lo:], exts0, unit, ro, nb, put=False)
+    ops.batch(lin, exts, unit, ops_list)
+    torch.cuda.synchronize()
+    assert torch.equal(lin, ref_lin)
+    for e, r in zip(exts, ref_exts):
+        assert torch.equal(e, r)
