@@ -1,0 +1,98 @@
+"""Command line: run a node's daemon mesh, inspect it, build the native tree.
+
+    python -m oncilla_amd mesh --gpus 8 [--policy stripe] [--state-file F]   # foreground, Ctrl-C stops
+    python -m oncilla_amd stats --ns NS [--rank 0]                           # every daemon's counters
+    python -m oncilla_amd build [--sanitize address|thread]
+
+`mesh` prints the environment apps need (OCM_NS; OCM_DAEMON_RANK is the
+daemon an app attaches to; LOCAL_RANK is used when unset).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import sys
+import time
+
+
+def _mesh(args) -> int:
+    from .parallel import Mesh
+
+    n = args.daemons or args.gpus or 1
+    gpus = [i % args.gpus for i in range(n)] if args.gpus else None
+    rank_env = {0: {"OCM_STATE_FILE": args.state_file}} if args.state_file else None
+    extra = []
+    if args.ctrl:
+        extra += ["--ctrl", args.ctrl]
+    m = Mesh(n, gpus=gpus, policy=args.policy, ns=args.ns, rank_env=rank_env, extra_args=extra, watch=True)
+    m.start(timeout=120)
+    print(f"mesh up: {n} daemons, namespace {m.ns}, nodefile {m.nodefile}", flush=True)
+    print(f"  export OCM_NS={m.ns}    # apps attach to OCM_DAEMON_RANK (default LOCAL_RANK)", flush=True)
+    stop = {"flag": False}
+
+    def _sig(*_):
+        stop["flag"] = True
+
+    signal.signal(signal.SIGINT, _sig)
+    signal.signal(signal.SIGTERM, _sig)
+    try:
+        while not stop["flag"]:
+            dead = [d.rank for d in m.daemons if not d.alive()]
+            if dead and not args.keep_going:
+                print(f"daemon(s) {dead} exited:\n{m.logs()[-3000:]}", file=sys.stderr)
+                return 1
+            time.sleep(0.5)
+    finally:
+        m.stop()
+    return 0
+
+
+def _stats(args) -> int:
+    from . import api
+
+    os.environ.setdefault("OCM_NO_GPU", "1")  # inspecting needs no GPU
+    with api.Client(daemon_rank=args.rank, ns=args.ns) as c:
+        n = c.lib.ocm_num_nodes()
+        keys = ["gpu", "num_apps", "gpu_used", "gpu_capacity", "host_used", "host_capacity", "n_alloc", "n_free",
+                "n_reclaimed", "n_spilled", "n_slabs", "n_leases", "lease_allocs", "ctrl_ticks"]
+        print("rank " + " ".join(f"{k:>13}" for k in keys))
+        for r in range(n):
+            try:
+                st = c.stats(r)
+            except api.OcmError as e:
+                print(f"{r:>4} unreachable: {e}")
+                continue
+            print(f"{r:>4} " + " ".join(f"{st[k]:>13}" for k in keys))
+    return 0
+
+
+def _build(args) -> int:
+    from .utils.build import build
+
+    print(build(sanitize=args.sanitize or False, verbose=True))
+    return 0
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m oncilla_amd", description=__doc__.splitlines()[0])
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    m = sub.add_parser("mesh", help="run one daemon per GPU (or CPU-only daemons) in the foreground")
+    m.add_argument("--gpus", type=int, default=0, help="GPUs on this node (0: CPU-only daemons)")
+    m.add_argument("--daemons", type=int, default=0, help="daemons (default: one per GPU)")
+    m.add_argument("--policy", default="stripe", choices=["ring", "least_loaded", "stripe", "loopback"])
+    m.add_argument("--ns", default=None)
+    m.add_argument("--ctrl", default=None, choices=["tcp", "rccl", "socket"])
+    m.add_argument("--state-file", default=None, help="rank0 directory checkpoint")
+    m.add_argument("--keep-going", action="store_true", help="keep running when a daemon exits")
+    s = sub.add_parser("stats", help="print every daemon's counters")
+    s.add_argument("--ns", required=True)
+    s.add_argument("--rank", type=int, default=0, help="daemon to attach to")
+    b = sub.add_parser("build", help="build the native tree (CMake + Ninja, gfx950)")
+    b.add_argument("--sanitize", default=None, choices=["address", "thread"])
+    args = ap.parse_args(argv)
+    return {"mesh": _mesh, "stats": _stats, "build": _build}[args.cmd](args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -37,3 +37,22 @@ def test_quickstart_gpu(native):
 def test_kv_offload_example(native):
     out = _run([sys.executable, os.path.join(REPO, "examples", "kv_offload.py")])
     assert "64 KV blocks swapped out and back" in out
+
+
+def test_cli_mesh_and_stats(native):
+    import signal
+    import time
+
+    p = subprocess.Popen([sys.executable, "-m", "oncilla_amd", "mesh", "--daemons", "3", "--ns", "clitest42"],
+                         cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         env=dict(os.environ, OCM_NO_GPU="1"))
+    try:
+        line = p.stdout.readline()
+        assert "mesh up: 3 daemons" in line, line + p.stderr.read()
+        out = _run([sys.executable, "-m", "oncilla_amd", "stats", "--ns", "clitest42"],
+                   env=dict(os.environ, OCM_NO_GPU="1", PYTHONPATH=REPO))
+        assert len([l for l in out.splitlines() if l.strip()[:1].isdigit()]) == 3, out
+    finally:
+        p.send_signal(signal.SIGINT)
+        p.wait(timeout=30)
+    assert p.returncode == 0
