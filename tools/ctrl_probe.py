@@ -1,0 +1,48 @@
+"""Control-plane transport cost: remote ocm_alloc p50 with the records on TCP
+(self queue) vs an RCCL ncclAllGather tick (1-rank communicator, OCM_TICK_SELF)
+vs the socket-ring collective, on one GPU. Leases off so every allocation
+takes the full REQ_ALLOC -> DO_ALLOC -> reply path.
+
+    python tools/ctrl_probe.py [--out gpurun_out/ctrl_probe.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from oncilla_amd import api  # noqa: E402
+from oncilla_amd.models import workloads as wl  # noqa: E402
+from oncilla_amd.parallel import Mesh  # noqa: E402
+
+
+def run(ctrl, tick_self):
+    env = {"OCM_LEASE_BYTES": "0"}
+    if tick_self:
+        env["OCM_TICK_SELF"] = "1"
+    with Mesh(1, gpus=[0], extra_args=["--ctrl", ctrl], env=env) as m:
+        with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+            deadline = time.time() + 30
+            while tick_self and c.stats(0)["ctrl_ticks"] == 0 and time.time() < deadline:
+                c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=1 << 20).free()
+                time.sleep(0.05)
+            r = wl.alloc_latency(c, api.OCM_REMOTE_GPU, 300, local_bytes=4096, remote_bytes=1 << 20)
+            r["ticks"] = c.stats(0)["ctrl_ticks"]
+            return {k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    out = {"tcp": run("tcp", False), "rccl_tick": run("rccl", True), "socket_tick": run("socket", True)}
+    print(json.dumps(out, indent=1))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
