@@ -369,19 +369,34 @@ static int ocm_copy_onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
 
 static int onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
     State &s = S();
-    std::lock_guard<std::recursive_mutex> lk(s.mu);
-    if (!a || !p) OCM_FAIL(-1, "ocm_copy_onesided: NULL argument");
-    if (!a->remote) OCM_FAIL(-1, "one-sided copy needs a remote pair (kind %d)", (int)a->kind);
-    // Bounds (reference src/rdma.c:55-59, src/lib.c:679): the local side is
-    // src_offset, the remote side dest_offset, for both directions.
-    if (p->bytes > a->local_bytes || p->src_offset + p->bytes > a->local_bytes)
-        OCM_FAIL(-1, "one-sided copy: local range [%llu,+%llu) exceeds %zu bytes", (unsigned long long)p->src_offset,
-                 (unsigned long long)p->bytes, a->local_bytes);
-    if (p->dest_offset + p->bytes > a->remote_bytes)
-        OCM_FAIL(-1, "one-sided copy: remote range [%llu,+%llu) exceeds %zu bytes", (unsigned long long)p->dest_offset,
-                 (unsigned long long)p->bytes, a->remote_bytes);
-    return xfer(a, p->op_flag != 0, static_cast<char *>(a->local) + p->src_offset, a->loc, p->dest_offset, p->bytes,
-                async);
+    hipEvent_t wait_ev = nullptr;
+    {
+        std::lock_guard<std::recursive_mutex> lk(s.mu);
+        if (!a || !p) OCM_FAIL(-1, "ocm_copy_onesided: NULL argument");
+        if (!s.allocs.count(a)) OCM_FAIL(-1, "ocm_copy_onesided: unknown allocation");
+        if (!a->remote) OCM_FAIL(-1, "one-sided copy needs a remote pair (kind %d)", (int)a->kind);
+        // Bounds (reference src/rdma.c:55-59, src/lib.c:679): the local side is
+        // src_offset, the remote side dest_offset, for both directions (overflow-safe).
+        if (p->src_offset > a->local_bytes || p->bytes > a->local_bytes - p->src_offset)
+            OCM_FAIL(-1, "one-sided copy: local range [%llu,+%llu) exceeds %zu bytes",
+                     (unsigned long long)p->src_offset, (unsigned long long)p->bytes, a->local_bytes);
+        if (p->dest_offset > a->remote_bytes || p->bytes > a->remote_bytes - p->dest_offset)
+            OCM_FAIL(-1, "one-sided copy: remote range [%llu,+%llu) exceeds %zu bytes",
+                     (unsigned long long)p->dest_offset, (unsigned long long)p->bytes, a->remote_bytes);
+        char *lin = static_cast<char *>(a->local) + p->src_offset;
+        const bool put = p->op_flag != 0;
+        // Large blocking ops: launch on the allocation's lane under the lock, wait
+        // outside it, so other threads' ops proceed meanwhile. Small ones keep the
+        // copy service (no launch) and the network tier its own blocking path.
+        const bool service = a->loc == LOC_DEVICE && a->all_dev_ok && p->bytes <= s.svc_max;
+        if (async || s.device < 0 || service || a->any_net)
+            return xfer(a, put, lin, a->loc, p->dest_offset, p->bytes, async);
+        if (xfer(a, put, lin, a->loc, p->dest_offset, p->bytes, true) != 0) return -1;
+        if (!a->async_pending || !a->ev) return 0;  // it completed inside xfer
+        wait_ev = a->ev;
+    }
+    DeviceGuard g(s.device);
+    return wait_event(wait_ev);
 }
 
 int ocm_copy_onesided(ocm_alloc_t a, ocm_param_t p) { return ocm_copy_onesided_impl(a, p, false); }

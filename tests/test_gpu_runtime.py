@@ -285,3 +285,38 @@ def test_remote_to_remote_copy_one_launch(mesh_factory):
         assert b.check(seed=31, offset=4096, nbytes=k, first_word=12288 // 4) == 0
         a.free()
         b.free()
+
+
+def test_threads_share_the_library(mesh_factory):
+    # Blocking transfers wait outside the library lock: threads on different
+    # allocations overlap, and every round trip stays exact.
+    import threading
+
+    m = mesh_factory(3, gpus=[0, 0, 0], policy="stripe")
+    errors = []
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 64 << 20
+        allocs = [c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n) for _ in range(4)]
+
+        def worker(i, a):
+            try:
+                for r in range(5):
+                    s = 1000 + 10 * i + r
+                    a.fill(seed=s)
+                    a.put(0, 0, n)
+                    a.fill(seed=0)
+                    a.get(0, 0, n)
+                    if a.check(seed=s) != 0:
+                        errors.append((i, r))
+                    a.batch([(0, 0, 4096, 8192), (1, 8192, 0, 4096)])  # batches interleave too
+            except Exception as e:  # noqa: BLE001
+                errors.append((i, repr(e)))
+
+        ts = [threading.Thread(target=worker, args=(i, a)) for i, a in enumerate(allocs)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        assert not errors, errors
+        for a in allocs:
+            a.free()
