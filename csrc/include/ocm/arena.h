@@ -28,7 +28,11 @@ struct ArenaConfig {
     uint64_t slab_bytes = 4ull << 30;  // HBM slab: requests < 2 GiB carve from resident slabs
     uint64_t align = 4096;           // sub-allocation alignment
     bool zero_on_alloc = false;
+    int numa_node = -1;              // host-tier pages preferred on this node (the GPU's socket); -1 = any
 };
+
+// NUMA node of a GPU's PCIe root (sysfs), -1 when unknown.
+int gpu_numa_node(int device);
 
 struct Slab {
     uint32_t id = 0;

@@ -2,10 +2,13 @@
 
 #include <hip/hip_runtime_api.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <cerrno>
+#include <string>
 #include <cstdio>
 #include <cstring>
 
@@ -14,6 +17,23 @@
 namespace ocm {
 
 static constexpr uint64_t kHugeAlign = 2ull << 20;
+
+int gpu_numa_node(int device) {
+    if (device < 0) return -1;
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    for (char *c = bus; *c; c++) *c = (char)std::tolower((unsigned char)*c);
+    std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+    FILE *f = std::fopen(path.c_str(), "r");
+    if (!f) return -1;
+    int node = -1;
+    if (std::fscanf(f, "%d", &node) != 1) node = -1;
+    std::fclose(f);
+    return node;
+}
 
 Arena::Arena(const ArenaConfig &cfg) : cfg_(cfg) {
     if (cfg_.align == 0 || (cfg_.align & (cfg_.align - 1))) cfg_.align = 4096;
@@ -97,6 +117,13 @@ Slab *Arena::new_slab(uint32_t tier, uint64_t bytes, bool dedicated, int *err) {
             return nullptr;
         }
         s->base = p;
+        if (cfg_.numa_node >= 0 && cfg_.numa_node < 64) {
+            // Shared policy on the memfd object: whichever process faults the pages in
+            // (importers pin them), they land on the GPU's socket, so DMA stays local.
+            unsigned long mask = 1ul << cfg_.numa_node;
+            if (syscall(SYS_mbind, p, s->bytes, 1 /* MPOL_PREFERRED */, &mask, 64ul, 0u) != 0)
+                OCM_WARN("mbind host slab to node %d: %s", cfg_.numa_node, strerror(errno));
+        }
         snprintf(reinterpret_cast<char *>(s->handle), kHandleBytes, "/proc/%d/fd/%d", (int)getpid(), s->memfd);
     }
     s->ra.reset(s->bytes);

@@ -114,6 +114,8 @@ int Daemon::init() {
     }
     ArenaConfig ac;
     ac.gpu = gpu_;
+    ac.numa_node = gpu_numa_node(gpu_);
+    if (const char *v = std::getenv("OCM_HOST_NUMA")) ac.numa_node = std::atoi(v);  // -1: no policy
     ac.slab_bytes = cfg_.slab_bytes;
     ac.zero_on_alloc = cfg_.zero_on_alloc;
     if (gpu_ >= 0) {
@@ -238,8 +240,8 @@ int Daemon::init() {
     }
     // Join: report our configuration to rank0 (reference notify_rank0, src/main.c:143-160).
     join_rank0();
-    OCM_INFO("ocmd rank %d/%d up: gpu %d (%d visible), hbm capacity %.1f GiB, host tier %.1f GiB, policy %s, ns %s",
-             rank_, n_, gpu_, num_gpu_, (double)arena_->capacity(TIER_GPU) / (1 << 30),
+    OCM_INFO("ocmd rank %d/%d up: gpu %d (%d visible, host tier on NUMA node %d), hbm capacity %.1f GiB, host tier %.1f GiB, policy %s, ns %s",
+             rank_, n_, gpu_, num_gpu_, arena_->config().numa_node, (double)arena_->capacity(TIER_GPU) / (1 << 30),
              (double)arena_->capacity(TIER_HOST) / (1 << 30), policy_name(cfg_.policy), ns_.c_str());
     return 0;
 }

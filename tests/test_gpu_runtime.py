@@ -320,3 +320,19 @@ def test_threads_share_the_library(mesh_factory):
         assert not errors, errors
         for a in allocs:
             a.free()
+
+
+def test_host_tier_prefers_the_gpus_numa_node(mesh_factory):
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=1 << 20, remote_bytes=1 << 20)  # N=1: host tier
+        assert a.remote_info()["extents"][0]["tier"] == api.OCM_TIER_HOST
+        import re
+
+        node = int(re.search(r"host tier on NUMA node (-?\d+)", m.logs()).group(1))
+        if node < 0:
+            pytest.skip("no NUMA information for this GPU")
+        maps = open(f"/proc/{m.daemons[0].proc.pid}/numa_maps").read()
+        slab = [l for l in maps.splitlines() if "ocm_host_slab" in l]
+        assert slab and all(f"prefer:{node}" in l for l in slab), slab
+        a.free()
