@@ -61,3 +61,33 @@ def test_threads_under_tsan(tsan_bin):
         m.stop()
     logs = m.logs()
     assert "WARNING: ThreadSanitizer" not in logs, logs
+
+
+def test_resume_net_tier_and_fuzz_under_asan(asan_bin, tmp_path):
+    # The newer daemon paths under ASan/UBSan: network tier (node split by host
+    # alias), rank0 checkpoint -> kill -> restart -> reconcile, and a mailbox storm.
+    import signal
+    import sys as _sys
+
+    _sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_fuzz_mailbox import _storm
+
+    state = str(tmp_path / "dir.ckpt")
+    hosts = {0: {"OCM_HOST_ALIAS": "A", "OCM_STATE_FILE": state}, 1: {"OCM_HOST_ALIAS": "A"},
+             2: {"OCM_HOST_ALIAS": "B"}}
+    m = Mesh(3, bin_dir=asan_bin, env=SAN_ENV, rank_env=hosts).start(timeout=120)
+    try:
+        env = dict(m.client_env(2), **SAN_ENV)  # rank 2 is alone on node B: network tier
+        for args in (["2", "4", "8"], ["3", "2", "4"]):
+            r = subprocess.run([f"{asan_bin}/ocm_test", *args], capture_output=True, text=True, timeout=300, env=env)
+            assert r.returncode == 0 and not any(b in r.stderr for b in BAD), f"{args}\n{r.stdout}\n{r.stderr}"
+        _storm(m.ns, seed=11, n=1500)
+        m.kill(0, signal.SIGKILL)
+        m.restart(0, timeout=120)
+        r = subprocess.run([f"{asan_bin}/ocm_test", "2", "4", "8"], capture_output=True, text=True, timeout=300,
+                           env=dict(m.client_env(1), **SAN_ENV))
+        assert r.returncode == 0 and not any(b in r.stderr for b in BAD), r.stdout + r.stderr
+    finally:
+        m.stop()
+    logs = m.logs()
+    assert not any(b in logs for b in BAD), logs[-6000:]
