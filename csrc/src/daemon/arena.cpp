@@ -152,7 +152,10 @@ int Arena::alloc(uint32_t tier, uint64_t bytes, Region *out) {
     if (tier != TIER_GPU && tier != TIER_HOST) return EINVAL;
     const uint64_t cap = capacity(tier), used = tier == TIER_GPU ? used_gpu_ : used_host_;
     if (bytes > cap || used > cap - bytes) return ENOMEM;  // overflow-safe
-    uint64_t slab_default = tier == TIER_GPU ? cfg_.slab_bytes : std::min<uint64_t>(cfg_.slab_bytes, 256ull << 20);
+    // Host slabs: 1 GiB. Importers mmap + hipHostRegister a slab once (pinning
+    // costs ~25 ms per 128 MiB), so requests below half a slab carve from one
+    // already registered instead of paying that per allocation.
+    uint64_t slab_default = tier == TIER_GPU ? cfg_.slab_bytes : std::min<uint64_t>(cfg_.slab_bytes, 1ull << 30);
     // Never map more than the tier may hand out (small capacities in tests / shared GPUs).
     slab_default = std::max(kHugeAlign, std::min(slab_default, (capacity(tier) + kHugeAlign - 1) & ~(kHugeAlign - 1)));
     Slab *slab = nullptr;
