@@ -104,6 +104,7 @@ int import_extent(Extent &e) {
             hipIpcMemHandle_t h;
             std::memcpy(&h, r.handle, sizeof(h));
             void *p = nullptr;
+            // (the lazy-peer-access flag is mandatory: 0 is rejected as an invalid argument)
             hipError_t err = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
             if (err != hipSuccess) OCM_FAIL(-1, "hipIpcOpenMemHandle(owner %d slab %u): %s", r.owner_rank, r.slab_id, hipGetErrorString(err));
             m.dbase = static_cast<char *>(p);
