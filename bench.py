@@ -190,8 +190,9 @@ def main() -> int:
         dist.barrier()
 
     # ---- daemon mesh: one ocmd per rank / GPU ----
-    my_port = free_ports(1)[0]
-    ports = gather_obj(dist, my_port, world)
+    # rank 0 picks every daemon port while holding them all bound, so no two
+    # ranks of this node can be handed the same ephemeral port
+    ports = gather_obj(dist, free_ports(world) if rank == 0 else None, world)[0]
     ns = f"bench{os.environ.get('MASTER_PORT', '0')}_{ports[0]}"
     workdir = os.path.join("/tmp", f"ocm_{ns}")
     os.makedirs(workdir, exist_ok=True)

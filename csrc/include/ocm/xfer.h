@@ -98,26 +98,49 @@ void xfer_batch_wave_ops(const XferBatchOp *ops, uint32_t n, uint64_t total_tile
 uint32_t xfer_batch_tile_shift(uint32_t n_ext, uint32_t unit_shift);
 hipError_t xfer_batch_launch(const XferBatchArgs &a, const XferTuning &t, hipStream_t stream);
 
-// ---- persistent copy service (low-latency small one-sided ops) ----
-// One resident workgroup polls a doorbell in host-pinned coherent memory. The
-// host writes the transfer arguments, then bumps `seq` (release); the kernel
-// copies, makes the bytes visible system-wide (acq_rel fence), and publishes
-// `done = seq`. Bounded: the kernel exits on kServiceStop or after `idle_ticks`
-// of s_memrealtime (100 MHz) without work; `exited` records that it left.
+// ---- persistent copy service (low-latency blocking one-sided ops) ----
+// A resident gang of `blocks` workgroups. Workgroup 0 polls a 128-byte request
+// record in host-pinned coherent memory: {seq, sum, args}. One wave reads the
+// whole record in a single pass; `sum` (a hash of seq and the args, written
+// before seq) proves the args it read belong to that seq, so a request costs
+// one PCIe read round trip, not two. Requests of at most `solo_tiles` tiles
+// are copied by workgroup 0 alone; larger ones are published to the rest of
+// the gang through a device-memory box (agent-scope release/acquire), every
+// workgroup copies its share of tiles, and the last one to finish (device
+// counter) makes the bytes visible system-wide and publishes `done = seq`.
+// Bounded: workgroup 0 exits on kServiceStop or after `idle_ticks` of
+// s_memrealtime (100 MHz) without work, and takes the gang with it; `exited`
+// records the first seq it did not serve.
 constexpr unsigned long long kServiceStop = ~0ull;
+constexpr int kServiceArgWords = (int)((sizeof(XferArgs) + 7) / 8);
+static_assert(kServiceArgWords <= 14, "service request record holds 14 argument words");
 
-struct alignas(64) ServiceSlot {
+struct alignas(128) ServiceSlot {
     unsigned long long seq;           // host -> device, written last
-    unsigned long long pad0[7];
-    XferArgs args;                    // host -> device
-    unsigned long long pad1[3];
+    unsigned long long sum;           // service_sum(seq, args)
+    unsigned long long args[14];      // XferArgs, host -> device
     unsigned long long done;          // device -> host (own cache line)
     unsigned long long exited;        // device -> host: first seq NOT served when it left
-    unsigned long long pad2[6];
+    unsigned long long pad[14];
+};
+static_assert(sizeof(ServiceSlot) == 256, "service slot layout");
+
+// Device-memory mailbox of the gang (zeroed before every launch).
+struct alignas(128) ServiceBox {
+    unsigned long long seq;           // last published gang request (kServiceStop: leave)
+    unsigned long long active;        // workgroups taking part in it (min(gang, tiles))
+    unsigned long long pad0[14];
+    unsigned long long cnt;           // workgroups finished with the current gang request
+    unsigned long long pad1[15];
+    unsigned long long args[14];
+    unsigned long long pad2[2];
 };
 
-hipError_t service_launch(ServiceSlot *slot, unsigned long long first_seq, unsigned long long idle_ticks,
-                          hipStream_t stream);
+// Post one request (args, then sum, then seq with release) for the service.
+void service_post(ServiceSlot *slot, const XferArgs &a, unsigned long long seq);
+
+hipError_t service_launch(ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
+                          unsigned long long idle_ticks, unsigned blocks, unsigned solo_tiles, hipStream_t stream);
 
 // Deterministic 32-bit word pattern (word i of a buffer) for data verification.
 hipError_t pattern_fill(void *p, uint64_t words, uint64_t first_word, uint32_t seed, hipStream_t stream);

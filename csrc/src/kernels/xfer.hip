@@ -384,66 +384,181 @@ hipError_t xfer_batch_launch(const XferBatchArgs &a, const XferTuning &t, hipStr
 
 namespace {
 
-constexpr int kArgWords = (sizeof(XferArgs) + 7) / 8;
-static_assert(kArgWords <= 64, "args must fit one wave's loads");
+__host__ __device__ __forceinline__ unsigned long long service_mix(unsigned long long h, unsigned long long w) {
+    h ^= w + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h *= 0xBF58476D1CE4E5B9ull;
+    return h ^ (h >> 31);
+}
 
-__global__ __launch_bounds__(kThreads) void service_kernel(ServiceSlot *slot, unsigned long long first_seq,
-                                                           unsigned long long idle_ticks) {
-    __shared__ __attribute__((aligned(16))) unsigned long long sh[kArgWords + 2];
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long w, int lane) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)w, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(w >> 32), lane);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t service_tiles(const XferArgs &a) {
+    const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
+    return (((a.rem_off + a.len + tile_mask) & ~tile_mask) - (a.rem_off & ~tile_mask)) >> a.tile_shift;
+}
+
+// Tiles first, first + stride, ... of the request in `sh` (args at sh + 2).
+__device__ __forceinline__ void service_copy(const unsigned long long *sh, uint64_t first, uint64_t stride) {
+    const XferArgs &a = *reinterpret_cast<const XferArgs *>(sh + 2);  // read in place (no scratch copy)
+    const uint64_t ntiles = service_tiles(a);
+    const uint64_t base = a.rem_off & ~((1ull << a.tile_shift) - 1);
+    for (uint64_t ti = first; ti < ntiles; ti += stride) {
+        TileSpan sp = tile_span(a, ti, base);
+        span_copy<false>(sp.dst, sp.src, sp.n);
+    }
+}
+
+// Release this workgroup's bytes system-wide with ONE cache writeback: every
+// wave drains its own stores into L2 (vmcnt), the barrier joins them, then a
+// single thread fences at system scope (guide: scoped release after a barrier).
+__device__ __forceinline__ void service_release() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __threadfence_system();
+}
+
+// Gang completion: each taking-part workgroup releases its bytes, then counts
+// itself in; the last of `active` publishes `done`.
+__device__ __forceinline__ void service_gang_done(ServiceSlot *slot, ServiceBox *box, unsigned long long s,
+                                                  unsigned long long active) {
+    service_release();
+    if (threadIdx.x == 0) {
+        const unsigned long long old =
+            __hip_atomic_fetch_add(&box->cnt, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == active - 1) __hip_atomic_store(&slot->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void service_kernel(ServiceSlot *slot, ServiceBox *box,
+                                                           unsigned long long first_seq,
+                                                           unsigned long long idle_ticks, unsigned solo_tiles) {
+    __shared__ __attribute__((aligned(16))) unsigned long long sh[16];
+    const int tid = threadIdx.x;
+    if (blockIdx.x != 0) {
+        // Gang member: wait for workgroup 0 to publish a large request in the box.
+        // Thread 0 takes a consistent snapshot {seq, active, args}: if seq moved
+        // while it read, that request completed without this workgroup (it was
+        // not taking part), so the newer one is taken instead.
+        unsigned long long last = 0;
+        for (;;) {
+            if (tid == 0) {
+                unsigned long long v = 0, act = 0;
+                for (;;) {
+                    v = __hip_atomic_load(&box->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (v == last || v == 0) {
+                        __builtin_amdgcn_s_sleep(4);
+                        continue;
+                    }
+                    if (v == kServiceStop) break;
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // box contents, and no stale cached data
+                    act = __hip_atomic_load(&box->active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (blockIdx.x < act)
+                        for (int i = 0; i < kServiceArgWords; i++)
+                            sh[2 + i] = __hip_atomic_load(&box->args[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the reads above before the re-check
+                    if (__hip_atomic_load(&box->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v) break;
+                }
+                sh[0] = v;
+                sh[1] = act;
+            }
+            __syncthreads();
+            const unsigned long long v = sh[0], active = sh[1];
+            if (v == kServiceStop) break;
+            if (blockIdx.x < active) {  // block-uniform: workgroups past `active` sit this one out
+                service_copy(sh, blockIdx.x, active);
+                service_gang_done(slot, box, v, active);
+            }
+            last = v;
+            __syncthreads();  // sh is rewritten by the next request
+        }
+        return;
+    }
     unsigned long long expect = first_seq;
     unsigned long long idle_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long *req = reinterpret_cast<unsigned long long *>(slot);
     for (;;) {
-        if (threadIdx.x == 0) {
-            unsigned long long s;
+        if (tid < 64) {
+            // One wave reads the whole request record per poll (lanes 0..15).
+            unsigned long long w = 0, s;
             for (;;) {
-                s = __hip_atomic_load(&slot->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (s == expect || s == kServiceStop) break;
+                if (tid < 16) w = __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                s = readlane64(w, 0);
+                if (s == kServiceStop) break;
+                if (s == expect) {
+                    unsigned long long h = service_mix(0, s);
+#pragma unroll
+                    for (int i = 0; i < kServiceArgWords; i++) h = service_mix(h, readlane64(w, 2 + i));
+                    if (h == readlane64(w, 1)) break;
+                    continue;  // seq landed before the args: read the record again
+                }
                 if (__builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks) {
                     s = kServiceStop;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(8);  // ~0.2 us between PCIe polls
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // order the argument loads after the doorbell
-            sh[kArgWords] = s;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // order the data loads after the doorbell
+            if (tid < 16) sh[tid] = w;
+            if (tid == 0) sh[0] = s;
         }
         __syncthreads();
-        const unsigned long long s = sh[kArgWords];
+        const unsigned long long s = sh[0];
         if (s == kServiceStop) break;
-        // The arguments live in host memory: fetch them with one wave, in parallel.
-        if (threadIdx.x < kArgWords)
-            sh[threadIdx.x] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(&slot->args) + threadIdx.x,
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __syncthreads();
-        const XferArgs &a = *reinterpret_cast<const XferArgs *>(sh);  // read in place (no scratch copy)
-        const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
-        const uint64_t first = a.rem_off & ~tile_mask;
-        const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;
-        for (uint64_t ti = 0; ti < ntiles; ti++) {
-            TileSpan sp = tile_span(a, ti, first);
-            span_copy<false>(sp.dst, sp.src, sp.n);
+        const uint64_t ntiles = service_tiles(*reinterpret_cast<const XferArgs *>(sh + 2));
+        if (gridDim.x > 1 && ntiles > solo_tiles) {
+            const unsigned long long active = ntiles < gridDim.x ? ntiles : gridDim.x;
+            if (tid < kServiceArgWords) box->args[tid] = sh[2 + tid];
+            if (tid == 0) {
+                __hip_atomic_store(&box->active, active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&box->cnt, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(&box->seq, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            service_copy(sh, 0, active);
+            service_gang_done(slot, box, s, active);
+        } else {
+            service_copy(sh, 0, 1);
+            // Make the bytes visible to the host, other kernels and DMA (system scope).
+            service_release();
+            if (tid == 0) __hip_atomic_store(&slot->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        // Make the bytes visible to the host, other kernels and DMA, and drop
-        // any cached copies before the next request (acq_rel, system scope).
-        __threadfence_system();
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __hip_atomic_store(&slot->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            idle_start = __builtin_amdgcn_s_memrealtime();
-        }
+        idle_start = __builtin_amdgcn_s_memrealtime();  // every lane: the idle test must stay wave-uniform
         expect++;
+        __syncthreads();  // sh is rewritten by the next poll
     }
-    if (threadIdx.x == 0) __hip_atomic_store(&slot->exited, expect, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0) {
+        __hip_atomic_store(&box->seq, kServiceStop, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&slot->exited, expect, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 }  // namespace
 
-hipError_t service_launch(ServiceSlot *slot, unsigned long long first_seq, unsigned long long idle_ticks,
-                          hipStream_t stream) {
-    hipLaunchKernelGGL(service_kernel, dim3(1), dim3(kThreads), 0, stream, slot, first_seq, idle_ticks);
-    return hipGetLastError();
+void service_post(ServiceSlot *slot, const XferArgs &a, unsigned long long seq) {
+    unsigned long long w[kServiceArgWords] = {};
+    std::memcpy(w, &a, sizeof(a));
+    unsigned long long h = service_mix(0, seq);
+    for (int i = 0; i < kServiceArgWords; i++) {
+        h = service_mix(h, w[i]);
+        __atomic_store_n(&slot->args[i], w[i], __ATOMIC_RELAXED);
+    }
+    __atomic_store_n(&slot->sum, h, __ATOMIC_RELAXED);
+    __atomic_store_n(&slot->seq, seq, __ATOMIC_RELEASE);
 }
 
+hipError_t service_launch(ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
+                          unsigned long long idle_ticks, unsigned blocks, unsigned solo_tiles, hipStream_t stream) {
+    if (!slot || !box || blocks == 0) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(box, 0, sizeof(ServiceBox), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(service_kernel, dim3(blocks), dim3(kThreads), 0, stream, slot, box, first_seq, idle_ticks,
+                       solo_tiles);
+    return hipGetLastError();
+}
 // ---- verification patterns (benchmarks and tests check data without a host round trip) ----
 
 __device__ __host__ __forceinline__ uint32_t pattern_word(uint64_t i, uint32_t seed) {

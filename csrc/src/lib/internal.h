@@ -40,6 +40,14 @@ using namespace ocm;
 
 enum Loc { LOC_HOST = 0, LOC_PINNED = 1, LOC_DEVICE = 2 };
 
+// Resident copy service defaults (OCM_SERVICE_MAX / _BLOCKS / _SOLO_TILES).
+// Measured (profiles/svc_probe_r01.json): a 32-workgroup gang beats a kernel
+// launch + sync (13.7-14.9 us) up to 4 MiB on HBM pairs: 8.8 us at 128 KiB-1 MiB,
+// 11.8 us at 4 MiB; requests of <= 2 tiles (64 KiB) stay on workgroup 0 (4.6 us at 4 KiB).
+constexpr uint64_t kServiceMaxDefault = 4ull << 20;
+constexpr int kServiceBlocksDefault = 32;
+constexpr int kServiceSoloTilesDefault = 2;
+
 struct Extent {
     Region r;
     char *dptr = nullptr;  // device-usable address of the extent start (nullptr: none)
@@ -134,10 +142,13 @@ struct State {
     OpCounters ctr;
     // persistent copy service (small blocking one-sided ops)
     ServiceSlot *svc = nullptr;
+    ServiceBox *svc_box = nullptr;   // device-memory mailbox of the gang
     hipStream_t svc_stream = nullptr;
+    unsigned svc_blocks = kServiceBlocksDefault;          // gang size (OCM_SERVICE_BLOCKS)
+    unsigned svc_solo_tiles = kServiceSoloTilesDefault;  // requests of <= this many tiles stay on workgroup 0
     bool svc_running = false;
     unsigned long long svc_seq = 0;
-    uint64_t svc_max = 128ull << 10;  // measured: launches win above ~128 KiB
+    uint64_t svc_max = kServiceMaxDefault;
     unsigned long long svc_idle_ticks = 200000ull;  // 2 ms at 100 MHz: live only during bursts of small ops
     // network tier
     std::map<std::string, int> net_conns;  // "ip:port" -> connected socket

@@ -87,7 +87,10 @@ int ocm_init(void) {
     s.sync_mode = env_int("OCM_SYNC_MODE", 1);
     s.n_lanes = env_int("OCM_ASYNC_LANES", 4);
     if (const char *k = std::getenv("OCM_PINNED_KEEP")) s.pinned_keep = std::strtoull(k, nullptr, 0);
-    if (const char *sm = std::getenv("OCM_SERVICE_MAX")) s.svc_max = std::strtoull(sm, nullptr, 0);
+    const char *sm = std::getenv("OCM_SERVICE_MAX");
+    s.svc_max = sm && *sm ? std::strtoull(sm, nullptr, 0) : kServiceMaxDefault;
+    s.svc_blocks = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_BLOCKS", kServiceBlocksDefault), 1024));
+    s.svc_solo_tiles = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES", kServiceSoloTilesDefault));
     s.tuning = xfer_tuning_from_env();
     const char *he = std::getenv("OCM_HOST_ENGINE");
     s.host_engine_kernel = he && !std::strcmp(he, "kernel");

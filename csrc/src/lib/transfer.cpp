@@ -124,6 +124,12 @@ int service_start(unsigned long long first_seq) {
             OCM_FAIL(-1, "copy service: no coherent host memory");
         }
         std::memset(s.svc, 0, sizeof(ServiceSlot));
+        if (hipMalloc(reinterpret_cast<void **>(&s.svc_box), sizeof(ServiceBox)) != hipSuccess) {
+            (void)hipGetLastError();
+            s.svc_box = nullptr;
+            s.svc_max = 0;
+            OCM_FAIL(-1, "copy service: no device mailbox");
+        }
         if (hipStreamCreateWithFlags(&s.svc_stream, hipStreamNonBlocking) != hipSuccess) {
             (void)hipGetLastError();
             s.svc_max = 0;
@@ -132,7 +138,8 @@ int service_start(unsigned long long first_seq) {
     }
     __atomic_store_n(&s.svc->exited, 0ull, __ATOMIC_RELEASE);
     __atomic_store_n(&s.svc->seq, 0ull, __ATOMIC_RELEASE);  // clear a STOP left by a parked instance
-    if (service_launch(s.svc, first_seq, s.svc_idle_ticks, s.svc_stream) != hipSuccess) {
+    if (service_launch(s.svc, s.svc_box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_solo_tiles, s.svc_stream) !=
+        hipSuccess) {
         (void)hipGetLastError();
         s.svc_max = 0;
         OCM_FAIL(-1, "copy service launch failed");
@@ -163,7 +170,9 @@ void service_stop() {
     }
     (void)hipStreamDestroy(s.svc_stream);
     (void)hipHostFree(s.svc);
+    if (s.svc_box) (void)hipFree(s.svc_box);
     s.svc = nullptr;
+    s.svc_box = nullptr;
     s.svc_stream = nullptr;
 }
 
@@ -173,8 +182,7 @@ int service_xfer(XferArgs x) {
     if (xfer_normalize(x) != hipSuccess) OCM_FAIL(-1, "invalid transfer");
     const unsigned long long seq = ++s.svc_seq;
     if (!s.svc_running && service_start(seq) != 0) return -1;
-    std::memcpy(&s.svc->args, &x, sizeof(x));
-    __atomic_store_n(&s.svc->seq, seq, __ATOMIC_RELEASE);
+    service_post(s.svc, x, seq);
     const uint64_t t0 = now_ns();
     for (unsigned spins = 1;; spins++) {
         if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
@@ -188,7 +196,7 @@ int service_xfer(XferArgs x) {
                 s.svc_running = false;
                 if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
                 if (service_start(seq) != 0) return -1;
-                __atomic_store_n(&s.svc->seq, seq, __ATOMIC_RELEASE);  // start cleared the doorbell: re-post
+                service_post(s.svc, x, seq);  // start cleared the doorbell: re-post
             }
             if (now_ns() - t0 > 10ull * 1000000000ull) OCM_FAIL(-1, "copy service did not complete a transfer in 10 s");
         }

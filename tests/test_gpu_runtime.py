@@ -150,6 +150,34 @@ def test_copy_service_small_ops(mesh_factory, policy):
         a.free()
 
 
+@pytest.mark.parametrize("blocks", ["1", "64"])
+def test_copy_service_gang(mesh_factory, monkeypatch, blocks):
+    """Mid-size blocking ops on the service gang (every workgroup takes a share
+    of the tiles, the last one publishes completion): odd sizes and offsets,
+    striped over three owners, interleaved with launch-path writes."""
+    monkeypatch.setenv("OCM_SERVICE_MAX", str(16 << 20))
+    monkeypatch.setenv("OCM_SERVICE_BLOCKS", blocks)
+    m = mesh_factory(4, gpus=[0, 0, 0, 0], policy="stripe")
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 24 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, stripe_unit=64 << 10)
+        assert len(a.remote_info()["extents"]) == 3
+        for i, (size, off) in enumerate([(96 << 10, 0), ((1 << 20) + 4, 4096), (3 << 20, 1 << 16),
+                                         ((16 << 20) - 4, 8), (5 << 20, (7 << 20) + 64)]):
+            seed = 300 + i
+            a.fill(seed=seed)
+            a.put(off, off, size)
+            a.fill(seed=0)
+            a.get(off, off, size)
+            assert a.check(seed=seed, offset=off, nbytes=size - size % 4, first_word=off // 4) == 0, (size, off)
+            a.fill(seed=seed + 50)
+            a.put(0, 0, n)                        # launch path (above the service limit)
+            a.fill(seed=0)
+            a.get(0, 0, 2 << 20)                  # service gang reads what the launch wrote
+            assert a.check(seed=seed + 50, nbytes=2 << 20) == 0
+        a.free()
+
+
 def test_tensor_views_on_peer_memory(mesh_factory):
     """Zero-copy torch views: compute directly on the remote half (another
     daemon's HBM via IPC) and move it with one-sided ops."""

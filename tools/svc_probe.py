@@ -1,0 +1,85 @@
+"""Resident copy service vs kernel launches: blocking put/get latency by size.
+
+Each configuration runs in its own process (the library reads OCM_SERVICE_*
+at ocm_init): the launch path only (OCM_SERVICE_MAX=0), and the service with
+a gang of 1..256 workgroups taking every op up to 64 MiB. Pairs: a loopback
+HBM pair (the daemon's HBM, IPC-imported) and a pinned host-tier pair (PCIe),
+data verified at every size before timing.
+
+    python tools/svc_probe.py [--out profiles/svc_probe_r01.json] [--tiers hbm,host] [--configs launch,svc_g32]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+SIZES = [4096 << i for i in range(15)]  # 4 KiB .. 64 MiB
+CONFIGS = {"launch": {"OCM_SERVICE_MAX": "0"}}
+for g in (1, 16, 32, 64, 128, 256):
+    CONFIGS[f"svc_g{g}"] = {"OCM_SERVICE_MAX": str(64 << 20), "OCM_SERVICE_BLOCKS": str(g)}
+
+
+def child(tier: str) -> None:
+    from oncilla_amd import api
+    from oncilla_amd.parallel.mesh import Mesh
+
+    out = {}
+    with Mesh(1, gpus=[0]) as m:
+        with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+            sizes = SIZES if tier == "hbm" else SIZES[:13]
+            n = sizes[-1] + 8192
+            flags = api.OCM_ALLOC_LOOPBACK if tier == "hbm" else api.OCM_ALLOC_HOST_TIER
+            a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=flags)
+            for s in sizes:
+                off = 4096 if s < (1 << 20) else 0
+                a.fill(seed=s & 0xFFFF)
+                a.put(off, off, s)
+                a.fill(seed=0)
+                a.get(off, off, s)
+                bad = a.check(seed=s & 0xFFFF, offset=off, nbytes=s, first_word=off // 4)
+                if bad:
+                    raise SystemExit(f"size {s}: {bad} words differ")
+                it = 200 if s <= (1 << 20) else 30
+                a.time_onesided(1, s, 5)
+                put = min(a.time_onesided(1, s, it) for _ in range(3))
+                get = min(a.time_onesided(0, s, it) for _ in range(3))
+                out[str(s)] = {"put_us": round(put * 1e6, 2), "get_us": round(get * 1e6, 2)}
+            a.free()
+    print(json.dumps(out))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--child", default=None, choices=["hbm", "host"])
+    ap.add_argument("--tiers", default="hbm,host")
+    ap.add_argument("--configs", default=",".join(CONFIGS))
+    args = ap.parse_args()
+    if args.child:
+        child(args.child)
+        return
+    res = {}
+    for tier in args.tiers.split(","):
+        for name in args.configs.split(","):
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", tier],
+                               env=dict(os.environ, **CONFIGS[name]), capture_output=True, text=True, timeout=300)
+            key = f"{tier}/{name}"
+            if r.returncode != 0:
+                res[key] = {"error": (r.stdout + r.stderr)[-800:]}
+                print(key, "FAILED", res[key]["error"], file=sys.stderr, flush=True)
+                break
+            res[key] = json.loads(r.stdout.strip().splitlines()[-1])
+            print(key, json.dumps(res[key]), flush=True)
+    line = json.dumps(res)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+    print(line)
+
+
+if __name__ == "__main__":
+    main()
