@@ -175,3 +175,19 @@ def test_daemons_exit_with_their_launcher(native, tmp_path):
                  open(f"/proc/{pid}/stat").read().split()[2] != "Z"]
         time.sleep(0.05)
     assert not alive, f"orphan daemons {alive}"
+
+
+def test_native_bench_json(four, tool, native):
+    """ocm_bench (C++, no Python in the loop): alloc latency distribution, the
+    reference R/W sweep on a verified pair, and a batch, as one JSON line."""
+    import json
+
+    rc, out = tool([f"{native}/ocm_bench", "--max", str(1 << 20), "--alloc-samples", "50", "--batch", "64",
+                    "--place", "stripe"], env=four.client_env(1))
+    assert rc == 0, out + four.logs()
+    res = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert res["nodes"] == 4 and res["extents"] == 3 and res["tiers"] == ["host"] * 3
+    assert 0 < res["alloc_us"]["p50"] <= res["alloc_us"]["p99"]
+    assert res["local_alloc_us"]["p50"] > 0 and res["batch"]["ops"] == 64
+    assert sorted(int(k) for k in res["sweep"]) == [4096 << i for i in range(9)]
+    assert all(v["get_GiBps"] > 0 and v["put_GiBps"] > 0 for v in res["sweep"].values())
