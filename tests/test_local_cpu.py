@@ -1,6 +1,8 @@
 """Config #1: one CPU-only daemon, loopback mailbox, malloc-backed local kinds.
 Runs the reference-equivalent ocm_test 1-4 (reference test/ocm_test.c) and the
 Python API against it."""
+import os
+
 import pytest
 
 from oncilla_amd import api
@@ -100,3 +102,36 @@ def test_tensor_views_cpu(one, monkeypatch):
         a.get(0, 0, 4096)
         assert int(loc[10]) == 15
         a.free()
+
+
+def test_reference_style_daemon_launch(tmp_path, native, tool):
+    """`oncillamem <nodefile>` exactly as the reference starts it (src/main.c:187-224):
+    a 5-column nodefile with no GPU column and no --rank; the rank is the line
+    whose dns column matches gethostname() (src/nodefile.c:92-103). Then the
+    reference's ocm_test 1 (host kind) runs against it."""
+    import socket
+    import subprocess
+    import time
+
+    from oncilla_amd.parallel.mesh import free_ports
+
+    port = free_ports(1)[0]
+    nf = tmp_path / "nodefile"
+    nf.write_text(f"#rank dns ethernet_ip ocm_port rdmacm_port\n0 {socket.gethostname()} 127.0.0.1 {port} 0\n")
+    ns = f"refstyle{port}"
+    env = dict(os.environ, OCM_NS=ns, OCM_NO_GPU="1")
+    env.pop("OCM_RANK", None)
+    env.pop("LOCAL_RANK", None)
+    ready = tmp_path / "ready.json"
+    d = subprocess.Popen([f"{native}/oncillamem", str(nf), "--gpu", "none", "--ready-file", str(ready),
+                          "--watch-pid", str(os.getpid())], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    try:
+        deadline = time.time() + 20
+        while not ready.exists() and time.time() < deadline and d.poll() is None:
+            time.sleep(0.05)
+        assert ready.exists(), d.stdout.read().decode() if d.poll() is not None else "daemon not ready"
+        rc, out = tool([f"{native}/ocm_test", "1", "1", "2", "3"], env=dict(env, OCM_DAEMON_RANK="0"))
+        assert rc == 0 and "completed successfully" in out, out
+    finally:
+        d.terminate()
+        d.wait(timeout=10)
