@@ -115,8 +115,31 @@ __device__ __forceinline__ TileSpan tile_span(const XferArgs &a, uint64_t ti, ui
     return tile_span_of(a, a.n_ext, a.unit_shift, a.tile_shift, a.lin, a.rem_off, a.len, a.put, ti, first_tile);
 }
 
+// Drain every wave's stores into L2, join the workgroup, then ONE system-scope
+// fence per workgroup writes them back and makes them visible to the host,
+// DMA engines and other kernels (guide: scoped release after a barrier).
+__device__ __forceinline__ void block_release_system() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __threadfence_system();
+}
+
+// Kernel-published completion (see XferDone): the last workgroup to count in
+// re-arms the counter and releases the host flag.
+__device__ __forceinline__ void xfer_publish(const XferDone &d) {
+    if (!d.flag) return;  // kernel argument: uniform
+    block_release_system();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(d.cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == gridDim.x - 1) {
+            __hip_atomic_store(d.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(d.flag, d.val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 template <bool NT>
-__global__ __launch_bounds__(kThreads) void xfer_reg_kernel(XferArgs a) {
+__global__ __launch_bounds__(kThreads) void xfer_reg_kernel(XferArgs a, XferDone d) {
     const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
     const uint64_t first = a.rem_off & ~tile_mask;
     const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;
@@ -124,6 +147,7 @@ __global__ __launch_bounds__(kThreads) void xfer_reg_kernel(XferArgs a) {
         TileSpan s = tile_span(a, ti, first);
         span_copy<NT>(s.dst, s.src, s.n);
     }
+    xfer_publish(d);
 }
 
 // ---- LDS-DMA variant ----
@@ -154,16 +178,10 @@ __device__ __forceinline__ void drain_tile(char *dst, const char *buf, int wave,
     for (int c = 0; c < kChunksPerWave; c++) store16<NT>(reinterpret_cast<u32x4 *>(g + c * 1024), v[c]);
 }
 
+// Body of the LDS-DMA kernel: this workgroup's tiles ti, ti + grid, ...
 template <bool NT>
-__global__ __launch_bounds__(kThreads) void xfer_lds_kernel(XferArgs a) {
-    // One LDS array (guide: a second __shared__ object can de-pipeline glds).
-    __shared__ __attribute__((aligned(16))) char lds[2 * (1 << kTileShift)];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
-    const uint64_t first = a.rem_off & ~tile_mask;
-    const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;
-    uint64_t ti = blockIdx.x;
-    if (ti >= ntiles) return;
+__device__ __forceinline__ void lds_stream(const XferArgs &a, char *lds, int wave, int lane, uint64_t ti,
+                                           uint64_t first, uint64_t ntiles) {
     TileSpan cur = tile_span(a, ti, first);
     bool cur_staged = full_aligned(cur);
     if (cur_staged) stage_tile(cur.src, lds, wave, lane);
@@ -193,6 +211,19 @@ __global__ __launch_bounds__(kThreads) void xfer_lds_kernel(XferArgs a) {
         cur_staged = nxt_staged;
         slot ^= 1;
     }
+}
+
+template <bool NT>
+__global__ __launch_bounds__(kThreads) void xfer_lds_kernel(XferArgs a, XferDone d) {
+    // One LDS array (guide: a second __shared__ object can de-pipeline glds).
+    __shared__ __attribute__((aligned(16))) char lds[2 * (1 << kTileShift)];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
+    const uint64_t first = a.rem_off & ~tile_mask;
+    const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;
+    uint64_t ti = blockIdx.x;
+    if (ti < ntiles) lds_stream<NT>(a, lds, wave, lane, ti, first, ntiles);  // grid <= ntiles: always true
+    xfer_publish(d);
 }
 
 int env_int(const char *k, int dflt) {
@@ -234,7 +265,7 @@ hipError_t xfer_normalize(XferArgs &a) {
     return hipSuccess;
 }
 
-hipError_t xfer_launch(const XferArgs &in, const XferTuning &t, hipStream_t stream) {
+hipError_t xfer_launch(const XferArgs &in, const XferTuning &t, hipStream_t stream, const XferDone *done) {
     if (in.len == 0) return hipSuccess;
     XferArgs a = in;
     if (xfer_normalize(a) != hipSuccess) return hipErrorInvalidValue;
@@ -248,16 +279,17 @@ hipError_t xfer_launch(const XferArgs &in, const XferTuning &t, hipStream_t stre
     // path at 2 per CU; never more blocks than tiles.
     int cap = t.max_blocks > 0 ? t.max_blocks : num_cus() * (variant == XFER_LDS ? 4 : 2);
     const unsigned grid = (unsigned)(ntiles < (uint64_t)cap ? ntiles : (uint64_t)cap);
+    const XferDone d = done ? *done : XferDone{};
     if (variant == XFER_LDS) {
         if (t.nontemporal)
-            hipLaunchKernelGGL(xfer_lds_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a);
+            hipLaunchKernelGGL(xfer_lds_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a, d);
         else
-            hipLaunchKernelGGL(xfer_lds_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a);
+            hipLaunchKernelGGL(xfer_lds_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a, d);
     } else {
         if (t.nontemporal)
-            hipLaunchKernelGGL(xfer_reg_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a);
+            hipLaunchKernelGGL(xfer_reg_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a, d);
         else
-            hipLaunchKernelGGL(xfer_reg_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a);
+            hipLaunchKernelGGL(xfer_reg_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a, d);
     }
     return hipGetLastError();
 }
@@ -412,20 +444,11 @@ __device__ __forceinline__ void service_copy(const unsigned long long *sh, uint6
     }
 }
 
-// Release this workgroup's bytes system-wide with ONE cache writeback: every
-// wave drains its own stores into L2 (vmcnt), the barrier joins them, then a
-// single thread fences at system scope (guide: scoped release after a barrier).
-__device__ __forceinline__ void service_release() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __threadfence_system();
-}
-
 // Gang completion: each taking-part workgroup releases its bytes, then counts
 // itself in; the last of `active` publishes `done`.
 __device__ __forceinline__ void service_gang_done(ServiceSlot *slot, ServiceBox *box, unsigned long long s,
                                                   unsigned long long active) {
-    service_release();
+    block_release_system();
     if (threadIdx.x == 0) {
         const unsigned long long old =
             __hip_atomic_fetch_add(&box->cnt, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -523,7 +546,7 @@ __global__ __launch_bounds__(kThreads) void service_kernel(ServiceSlot *slot, Se
         } else {
             service_copy(sh, 0, 1);
             // Make the bytes visible to the host, other kernels and DMA (system scope).
-            service_release();
+            block_release_system();
             if (tid == 0) __hip_atomic_store(&slot->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         idle_start = __builtin_amdgcn_s_memrealtime();  // every lane: the idle test must stay wave-uniform

@@ -47,6 +47,11 @@ enum Loc { LOC_HOST = 0, LOC_PINNED = 1, LOC_DEVICE = 2 };
 constexpr uint64_t kServiceMaxDefault = 4ull << 20;
 constexpr int kServiceBlocksDefault = 32;
 constexpr int kServiceSoloTilesDefault = 2;
+// Kernel-published completion of blocking launches (XferDone) up to this size.
+// Measured on HBM pairs (profiles/launch_flag_r01.json): 9.1-13.4 us against
+// 13.0-14.6 us with the runtime event up to 4 MiB; above that the per-workgroup
+// system-scope writeback costs more than it saves (16 MiB: 30.9 against 15.8 us).
+constexpr uint64_t kLaunchFlagMaxDefault = 4ull << 20;
 
 struct Extent {
     Region r;
@@ -160,6 +165,13 @@ struct State {
     // robin), so ops on different allocations (different peers / links) overlap.
     std::vector<hipStream_t> lanes;
     int n_lanes = 4, next_lane = 0;
+    // Kernel-published completion of blocking launch-path ops (XferDone), one
+    // slot per lane: a host-coherent flag line and a device counter line.
+    unsigned long long *lane_flags = nullptr;  // 16 words per lane
+    unsigned int *lane_cnt = nullptr;          // 32 words per lane
+    std::vector<unsigned long long> lane_flag_seq;
+    bool launch_flags = true;                  // OCM_LAUNCH_FLAG=0 waits on the runtime event instead
+    uint64_t launch_flag_max = kLaunchFlagMaxDefault;  // OCM_LAUNCH_FLAG_MAX
     bool pool_tried = false;
     uint64_t pool_keep = 8ull << 30;       // bytes kept reserved across frees
     hipEvent_t done = nullptr;
@@ -249,7 +261,12 @@ int service_start(unsigned long long first_seq);
 void service_park();
 void service_stop();
 int service_xfer(XferArgs x);
-int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async);
+// `done` (optional, async launches on a lane): receives the kernel-published
+// completion flag of the launch, or flag == nullptr when the op has none.
+int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async,
+         XferDone *done = nullptr);
+// Wait for a kernel-published flag (>= val), with the runtime event as the backstop.
+int wait_done(const XferDone &d, hipEvent_t ev);
 int copy_local(void *dst, Loc dl, const void *src, Loc sl, size_t n);
 
 // ---- batches (batch.cpp)

@@ -91,6 +91,9 @@ int ocm_init(void) {
     s.svc_max = sm && *sm ? std::strtoull(sm, nullptr, 0) : kServiceMaxDefault;
     s.svc_blocks = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_BLOCKS", kServiceBlocksDefault), 1024));
     s.svc_solo_tiles = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES", kServiceSoloTilesDefault));
+    s.launch_flags = env_int("OCM_LAUNCH_FLAG", 1) != 0;
+    const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");
+    s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
     s.tuning = xfer_tuning_from_env();
     const char *he = std::getenv("OCM_HOST_ENGINE");
     s.host_engine_kernel = he && !std::strcmp(he, "kernel");
@@ -133,6 +136,14 @@ int ocm_tini(void) {
     }
     s.lanes.clear();
     s.next_lane = 0;
+    if (s.lane_flags) {
+        DeviceGuard g(s.device);
+        (void)hipHostFree(s.lane_flags);
+        (void)hipFree(s.lane_cnt);
+        s.lane_flags = nullptr;
+        s.lane_cnt = nullptr;
+        s.lane_flag_seq.clear();
+    }
     if (s.stream) {
         DeviceGuard g(s.device);
         (void)hipStreamSynchronize(s.stream);
@@ -373,6 +384,7 @@ static int ocm_copy_onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
 static int onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
     State &s = S();
     hipEvent_t wait_ev = nullptr;
+    XferDone wait_done_flag;
     {
         std::lock_guard<std::recursive_mutex> lk(s.mu);
         if (!a || !p) OCM_FAIL(-1, "ocm_copy_onesided: NULL argument");
@@ -394,11 +406,13 @@ static int onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
         const bool service = a->loc == LOC_DEVICE && a->all_dev_ok && p->bytes <= s.svc_max;
         if (async || s.device < 0 || service || a->any_net)
             return xfer(a, put, lin, a->loc, p->dest_offset, p->bytes, async);
-        if (xfer(a, put, lin, a->loc, p->dest_offset, p->bytes, true) != 0) return -1;
+        if (xfer(a, put, lin, a->loc, p->dest_offset, p->bytes, true, &wait_done_flag) != 0) return -1;
         if (!a->async_pending || !a->ev) return 0;  // it completed inside xfer
         wait_ev = a->ev;
     }
     DeviceGuard g(s.device);
+    // The kernel publishes its own completion (~6 us before the runtime's event).
+    if (wait_done_flag.flag) return wait_done(wait_done_flag, wait_ev);
     return wait_event(wait_ev);
 }
 
@@ -762,6 +776,7 @@ long long ocm_x_pattern(void *p, uint64_t words, uint64_t first, uint32_t seed, 
         }
         return bad;
     }
+    std::lock_guard<std::recursive_mutex> lk(s.mu);  // the library stream and its event are shared
     DeviceGuard g(s.device);
     if (!check) {
         if (pattern_fill(p, words, first, seed, s.stream) != hipSuccess) return -1;

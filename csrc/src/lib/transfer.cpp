@@ -76,6 +76,20 @@ hipStream_t lane_stream(lib_alloc *a) {
             }
         }
         if (s.lanes.empty()) return s.stream;
+        if (!s.lane_flags && s.launch_flags) {
+            DeviceGuard g(s.device);
+            const size_t nl = s.lanes.size();
+            if (hipHostMalloc(reinterpret_cast<void **>(&s.lane_flags), nl * 128,
+                              hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&s.lane_cnt), nl * 128) != hipSuccess ||
+                hipMemset(s.lane_cnt, 0, nl * 128) != hipSuccess) {
+                (void)hipGetLastError();
+                s.launch_flags = false;  // events only
+            } else {
+                std::memset(s.lane_flags, 0, nl * 128);
+                s.lane_flag_seq.assign(nl, 0);
+            }
+        }
         a->lane = s.next_lane++ % (int)s.lanes.size();
     }
     if (!a->ev) {
@@ -205,8 +219,22 @@ int service_xfer(XferArgs x) {
 
 // One-sided transfer between the linear buffer `lin` (location `lloc`) and the
 // remote half of `a` at striped offset `rem_off`.
-int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async) {
+int wait_done(const XferDone &d, hipEvent_t ev) {
+    for (unsigned spins = 1;; spins++) {
+        if ((long long)(__atomic_load_n(d.flag, __ATOMIC_ACQUIRE) - d.val) >= 0) return 0;
+        if ((spins & 4095) == 0) {
+            // Backstop: the runtime saw the kernel end (the flag is then set, or
+            // the kernel had nothing to publish); errors surface here too.
+            const hipError_t e = hipEventQuery(ev);
+            if (e == hipSuccess) return 0;
+            if (e != hipErrorNotReady) OCM_FAIL(-1, "event wait: %s", hipGetErrorString(e));
+        }
+    }
+}
+
+int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async, XferDone *done) {
     State &s = S();
+    if (done) *done = XferDone{};
     if (len == 0) return 0;
     if (a->any_net) {
         // Another node: stream every piece through its owner's data server (blocking).
@@ -298,7 +326,15 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
             for (auto &e : a->ext) same_gpu &= e.r.tier == TIER_GPU && e.r.owner_gpu == s.device;
             t.variant = (same_gpu && len <= (256ull << 20)) ? XFER_LDS : XFER_REG;
         }
-        err = xfer_launch(x, t, st);
+        XferDone dn;
+        if (done && async && len <= s.launch_flag_max && s.launch_flags && s.lane_flags && st != s.stream &&
+            a->lane >= 0 && a->ev) {
+            dn.flag = s.lane_flags + (size_t)a->lane * 16;
+            dn.cnt = s.lane_cnt + (size_t)a->lane * 32;
+            dn.val = ++s.lane_flag_seq[(size_t)a->lane];
+        }
+        err = xfer_launch(x, t, st, dn.flag ? &dn : nullptr);
+        if (err == hipSuccess && done) *done = dn;
     } else {
         service_park();
         segments(a, rem_off, len, segs);

@@ -178,6 +178,47 @@ def test_copy_service_gang(mesh_factory, monkeypatch, blocks):
         a.free()
 
 
+def test_launch_flag_completion(mesh_factory, monkeypatch):
+    """Blocking launch-path ops complete on the kernel-published lane flag
+    (service off): odd sizes/offsets up to the flag limit and above it (event
+    path), six allocations over four lanes driven from three threads at once,
+    so later launches on a lane overtake the flag value a waiter looks for."""
+    import threading
+
+    monkeypatch.setenv("OCM_SERVICE_MAX", "0")
+    m = mesh_factory(2, gpus=[0, 0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 12 << 20
+        allocs = [c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n) for _ in range(6)]
+        errors = []
+
+        def worker(k):
+            try:
+                for j, (size, off) in enumerate([(4096, 0), (100000, 12), ((1 << 20) + 4, 4096), (4 << 20, 0),
+                                                  ((8 << 20) + 64, 1 << 20)]):
+                    for a in allocs[k::3]:
+                        seed = 1000 + 10 * k + j
+                        a.fill(seed=seed)
+                        a.put(off, off, size)
+                        a.fill(seed=0)
+                        a.get(off, off, size)
+                        bad = a.check(seed=seed, offset=off, nbytes=size - size % 4, first_word=off // 4)
+                        if bad:
+                            errors.append((k, size, off, bad))
+            except Exception as e:  # noqa: BLE001 - reported below
+                errors.append(repr(e))
+
+        threads = [threading.Thread(target=worker, args=(k,)) for k in range(3)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=100)
+        assert not any(t.is_alive() for t in threads), "a blocking op never completed"
+        assert not errors, errors
+        for a in allocs:
+            a.free()
+
+
 def test_tensor_views_on_peer_memory(mesh_factory):
     """Zero-copy torch views: compute directly on the remote half (another
     daemon's HBM via IPC) and move it with one-sided ops."""

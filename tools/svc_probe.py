@@ -1,7 +1,9 @@
 """Resident copy service vs kernel launches: blocking put/get latency by size.
 
 Each configuration runs in its own process (the library reads OCM_SERVICE_*
-at ocm_init): the launch path only (OCM_SERVICE_MAX=0), and the service with
+at ocm_init): the launch path only (OCM_SERVICE_MAX=0), completed by the
+kernel-published flag (default) or by the runtime event (OCM_LAUNCH_FLAG=0),
+and the service with
 a gang of 1..256 workgroups taking every op up to 64 MiB. Pairs: a loopback
 HBM pair (the daemon's HBM, IPC-imported) and a pinned host-tier pair (PCIe),
 data verified at every size before timing.
@@ -18,7 +20,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 SIZES = [4096 << i for i in range(15)]  # 4 KiB .. 64 MiB
-CONFIGS = {"launch": {"OCM_SERVICE_MAX": "0"}}
+CONFIGS = {"launch": {"OCM_SERVICE_MAX": "0"}, "launch_event": {"OCM_SERVICE_MAX": "0", "OCM_LAUNCH_FLAG": "0"}}
 for g in (1, 16, 32, 64, 128, 256):
     CONFIGS[f"svc_g{g}"] = {"OCM_SERVICE_MAX": str(64 << 20), "OCM_SERVICE_BLOCKS": str(g)}
 
