@@ -58,6 +58,7 @@ struct DaemonConfig {
     std::string mesh_key;            // OCM_MESH_KEY: shared secret mixed into the mesh HELLO token
     std::string state_file;          // rank0: directory checkpoint (resume after a rank0 restart)
     int state_interval_ms = 20;      // max staleness of that checkpoint while the directory changes
+    int spin_us = 50;                // after activity, poll without sleeping this long (0: always block)
 };
 
 int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err);

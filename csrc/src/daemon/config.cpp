@@ -44,6 +44,7 @@ static const char *kUsage =
     "  --ready-file PATH        written once the mesh is complete\n"
     "  --watch-pid PID          exit when this process exits\n"
     "  --zero                   zero memory on allocation                      [OCM_ZERO_ON_ALLOC]\n"
+    "  --spin-us US             poll without sleeping for US after activity (default 50, 0 = off) [OCM_DAEMON_SPIN_US]\n"
     "sizes accept K/M/G/T suffixes; OCM_MESH_KEY sets the mesh authentication secret";
 
 int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err) {
@@ -70,6 +71,7 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
     if (const char *v = env("OCM_STATE_FILE")) cfg->state_file = v;
     if (const char *v = env("OCM_MESH_KEY")) cfg->mesh_key = v;
     if (const char *v = env("OCM_STATE_INTERVAL_MS")) cfg->state_interval_ms = std::atoi(v);
+    if (const char *v = env("OCM_DAEMON_SPIN_US")) cfg->spin_us = std::atoi(v);
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         if (a == "-h" || a == "--help") {
@@ -133,6 +135,9 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
             cfg->watch_pid = std::atoi(v.c_str());
         } else if (a == "--zero") {
             cfg->zero_on_alloc = true;
+        } else if (a == "--spin-us") {
+            if (!val(&v)) return -1;
+            cfg->spin_us = std::atoi(v.c_str());
         } else if (!a.empty() && a[0] == '-') {
             *err = "unknown option " + a;
             return -1;

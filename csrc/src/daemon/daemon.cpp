@@ -322,6 +322,12 @@ int Daemon::run() {
 
 int Daemon::loop() {
     struct epoll_event evs[64];
+    // Bounded post-activity polling: for spin_us after the last event the loop
+    // polls epoll without sleeping, so the next record of a burst (an app's
+    // alloc/free sequence, the owner's reply) skips the scheduler wake-up. Idle
+    // daemons block as before; nothing spins without recent traffic.
+    const uint64_t spin_ns = cfg_.spin_us > 0 ? (uint64_t)cfg_.spin_us * 1000 : 0;
+    uint64_t last_event_ns = 0;
     while (!stop_) {
         while (!self_q_.empty() && !stop_) {
             Msg m = self_q_.front();
@@ -334,7 +340,9 @@ int Daemon::loop() {
         int timeout = 1000;
         if (r0_lost_) timeout = 100;
         if (gov_ && !cfg_.state_file.empty() && gov_->version() != saved_version_) timeout = cfg_.state_interval_ms;
-        int n = epoll_wait(ep_, evs, 64, self_q_.empty() ? timeout : 0);
+        const bool spinning = spin_ns && now_ns() - last_event_ns < spin_ns;
+        int n = epoll_wait(ep_, evs, 64, (self_q_.empty() && !spinning) ? timeout : 0);
+        if (n > 0 && spin_ns) last_event_ns = now_ns();
         sweep_timeouts();
         return_idle_leases();
         if (n < 0) {

@@ -176,6 +176,7 @@ struct State {
     uint64_t pool_keep = 8ull << 30;       // bytes kept reserved across frees
     hipEvent_t done = nullptr;
     int rpc_timeout_ms = 60000;
+    uint64_t rpc_spin_ns = 50000;          // OCM_RPC_SPIN_US: poll for a reply this long before sleeping
     uint64_t pinned_keep = 2ull << 30;     // idle pinned chunks kept for reuse
     class PinnedArena *pinned = nullptr;   // created on first use
 };

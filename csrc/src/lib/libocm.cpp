@@ -2,8 +2,8 @@
 //
 // Parity with reference src/lib.c (struct lib_alloc, ocm_init/tini/alloc/free,
 // accessors, ocm_copy, ocm_copy_onesided). MI355X design:
-//   * control: one mailbox RPC to the local ocmd (seq-matched, blocking
-//     mq_timedreceive — no spinning), multi-record replies for striped pairs;
+//   * control: one mailbox RPC to the local ocmd (seq-matched; a bounded poll
+//     for the reply, then a blocking wait), multi-record replies for striped pairs;
 //   * registration: remote HBM extents are imported once per slab with
 //     hipIpcOpenMemHandle (lazy peer access) and cached; host-tier extents are
 //     mmap'ed from the owner's memfd and hipHostRegister'ed (device-mapped);
@@ -33,6 +33,7 @@ int ocm_init(void) {
     s.daemon_rank = dr && *dr ? std::atoi(dr) : (lr && *lr ? std::atoi(lr) : 0);
     s.daemon_mbox = daemon_mailbox_name(s.daemon_rank, s.ns);
     s.rpc_timeout_ms = env_int("OCM_RPC_TIMEOUT_MS", 60000);
+    s.rpc_spin_ns = (uint64_t)std::max(0, env_int("OCM_RPC_SPIN_US", 50)) * 1000;
     const int connect_ms = env_int("OCM_CONNECT_TIMEOUT_MS", 10000);
     // Connect to the daemon mailbox, retrying while it starts (reference: 10 x 10 ms).
     long deadline = now_ms() + connect_ms;

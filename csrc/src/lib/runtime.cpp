@@ -38,6 +38,19 @@ int rpc(Msg &req, Msg *reply, int timeout_ms) {
     State &s = S();
     req.seq = ++s.seq;
     if (s.chan.send(&req, kMsgBytes, timeout_ms) != 1) OCM_FAIL(-1, "mailbox send to daemon failed");
+    // A reply usually lands within a few microseconds: poll for it (bounded,
+    // OCM_RPC_SPIN_US) before sleeping in poll(2), which adds a wake-up.
+    if (s.rpc_spin_ns) {
+        const uint64_t t0 = now_ns();
+        do {
+            const int rc = s.chan.recv(reply, kMsgBytes, 0);
+            if (rc < 0) return -1;
+            if (rc == 1) {
+                if (reply->seq == req.seq && reply->type != MSG_EXTENT) return 0;
+                OCM_LOG("dropping stale reply %s seq %llu", msg_type_str(reply->type), (unsigned long long)reply->seq);
+            }
+        } while (now_ns() - t0 < s.rpc_spin_ns);
+    }
     const long deadline = now_ms() + timeout_ms;
     for (;;) {
         long left = deadline - now_ms();
