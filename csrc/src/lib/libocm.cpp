@@ -751,6 +751,26 @@ double ocm_x_time_device_copy(int device, void *dst, const void *src, uint64_t b
 
 // Wall-clock seconds per blocking one-sided op, measured inside the library
 // (no Python in the loop): the sweep primitive of bench.py.
+// Per-sample wall time (seconds) of ocm_alloc_ex and the matching ocm_free,
+// timed in C so callers (bench.py) report the API's latency, not their FFI's.
+// Returns the number of samples taken (< samples on the first failure).
+int ocm_x_alloc_latency(ocm_alloc_param_t ap, const struct ocm_alloc_ex_params *ex, int samples, double *alloc_s,
+                        double *free_s) {
+    for (int i = 0; i < samples; i++) {
+        struct timespec t0, t1, t2;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        ocm_alloc_t a = ocm_alloc_ex(ap, ex);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        if (!a) return i;
+        const int rc = ocm_free(a);
+        clock_gettime(CLOCK_MONOTONIC, &t2);
+        if (rc != 0) return i;
+        alloc_s[i] = (double)(t1.tv_sec - t0.tv_sec) + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-9;
+        free_s[i] = (double)(t2.tv_sec - t1.tv_sec) + (double)(t2.tv_nsec - t1.tv_nsec) * 1e-9;
+    }
+    return samples;
+}
+
 double ocm_x_time_onesided(ocm_alloc_t a, ocm_param_t p, int iters) {
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);

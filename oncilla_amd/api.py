@@ -169,6 +169,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_xfer": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, u64, u64, i32, i32, i32, i32]),
             "ocm_x_time_device_copy": (ctypes.c_double, [i32, vp, vp, u64, i32, i32, i32, i32]),
             "ocm_x_time_onesided": (ctypes.c_double, [vp, ctypes.POINTER(OcmParams), i32]),
+            "ocm_x_alloc_latency": (i32, [ctypes.POINTER(OcmAllocParams), ctypes.POINTER(OcmAllocExParams), i32,
+                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
             "ocm_x_set_tuning": (None, [i32, i32, i32]),
@@ -524,6 +526,18 @@ class Client:
     def plan(self) -> Plan:
         """A new transfer plan (hipGraph replay of fixed batch schedules)."""
         return Plan(self)
+
+    def alloc_latency(self, kind: int, samples: int, local_bytes: int = 0, remote_bytes: int = 0,
+                      flags: int = 0) -> tuple:
+        """Per-sample seconds of ocm_alloc_ex and the matching ocm_free, timed in C."""
+        ap = OcmAllocParams(local_bytes, remote_bytes, kind)
+        ex = OcmAllocExParams(-1, flags, 0, 0, 0)
+        a = (ctypes.c_double * samples)()
+        f = (ctypes.c_double * samples)()
+        n = self.lib.ocm_x_alloc_latency(ctypes.byref(ap), ctypes.byref(ex), samples, a, f)
+        if n != samples:
+            raise OcmError(f"ocm_alloc/ocm_free failed after {n} samples: " + last_error())
+        return list(a), list(f)
 
     def alloc(self, kind: int, local_bytes: int = 0, remote_bytes: int = 0, remote_rank: int = -1, flags: int = 0,
               stripe_width: int = 0, stripe_unit: int = 0) -> Allocation:
