@@ -14,7 +14,36 @@
 #include "ocm/log.h"
 #include "ocm/sock.h"
 
+// Requests on different connections (an app's parallel streams, or its next op
+// on another stream) touch the same slab bytes from different server threads.
+// Their order is set by the app, which waits for each response before it sends
+// a request that depends on it; TSan cannot see that through the sockets, so
+// every request acquires, and every completed one releases, a per-server token.
+#if defined(__has_feature)
+#if __has_feature(thread_sanitizer)
+#define OCM_TSAN 1
+extern "C" void __tsan_acquire(void *addr);
+extern "C" void __tsan_release(void *addr);
+#endif
+#endif
+#ifndef OCM_TSAN
+#define OCM_TSAN 0
+#endif
+
 namespace ocm {
+
+namespace {
+inline void hb_acquire([[maybe_unused]] void *tok) {
+#if OCM_TSAN
+    __tsan_acquire(tok);
+#endif
+}
+inline void hb_release([[maybe_unused]] void *tok) {
+#if OCM_TSAN
+    __tsan_release(tok);
+#endif
+}
+}  // namespace
 
 bool parse_net_handle(const uint8_t *handle, std::string *ip, int *port, uint64_t *token) {
     char buf[65] = {0};
@@ -112,6 +141,7 @@ void DataServer::serve(int fd) {
     while (authed && !stop_ && recv_all(fd, &q, sizeof(q)) == 1) {
         NetResp r{kNetMagic, 0, q.len};
         if (q.magic != kNetMagic) break;
+        hb_acquire(&token_);
         void *mem = nullptr;
         uint32_t tier = 0;
         if (q.op == NET_PING) {
@@ -136,6 +166,7 @@ void DataServer::serve(int fd) {
                 }
                 done += n;
             }
+            hb_release(&token_);
             if (!ok || send_all(fd, &r, sizeof(r)) != 1) break;
         } else if (q.op == NET_GET) {
             if (r.err) r.len = 0;
@@ -150,6 +181,7 @@ void DataServer::serve(int fd) {
                 }
                 done += n;
             }
+            hb_release(&token_);
             if (!ok) break;
         } else {
             break;

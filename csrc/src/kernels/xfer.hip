@@ -64,7 +64,22 @@ __device__ __forceinline__ void span_copy(char *__restrict__ dst, const char *__
 #pragma unroll
             for (int k = 0; k < kUnroll; k++) store16<NT>(d + base + (uint64_t)k * kThreads + tid, v[k]);
         }
-        for (uint64_t i = base + tid; i < nv; i += kThreads) store16<NT>(d + i, load16(s + i));
+        if (base < nv) {
+            // Remainder (< kThreads x kUnroll vectors): every load issued before
+            // the first store, so a partial tile costs one memory round trip,
+            // not one per 4 KiB (a GET of host-tier memory pays PCIe latency each).
+            u32x4 v[kUnroll];
+#pragma unroll
+            for (int k = 0; k < kUnroll; k++) {
+                const uint64_t i = base + (uint64_t)k * kThreads + tid;
+                if (i < nv) v[k] = load16(s + i);
+            }
+#pragma unroll
+            for (int k = 0; k < kUnroll; k++) {
+                const uint64_t i = base + (uint64_t)k * kThreads + tid;
+                if (i < nv) store16<NT>(d + i, v[k]);
+            }
+        }
         const uint64_t tail = n & 15u;
         if ((uint64_t)tid < tail) dst[(nv << 4) + tid] = src[(nv << 4) + tid];
     } else {

@@ -53,6 +53,13 @@ constexpr int kServiceSoloTilesDefault = 2;
 // system-scope writeback costs more than it saves (16 MiB: 30.9 against 15.8 us).
 constexpr uint64_t kLaunchFlagMaxDefault = 4ull << 20;
 
+// One data-server connection of the network tier, with its own pinned staging
+// buffer for device-side local halves (allocated on first device use).
+struct NetConn {
+    int fd = -1;
+    void *stage = nullptr;
+};
+
 struct Extent {
     Region r;
     char *dptr = nullptr;  // device-usable address of the extent start (nullptr: none)
@@ -156,8 +163,9 @@ struct State {
     uint64_t svc_max = kServiceMaxDefault;
     unsigned long long svc_idle_ticks = 200000ull;  // 2 ms at 100 MHz: live only during bursts of small ops
     // network tier
-    std::map<std::string, int> net_conns;  // "ip:port" -> connected socket
-    void *net_stage = nullptr;             // pinned staging buffer (device-side local halves)
+    std::map<std::string, NetConn> net_conns;  // "ip:port#stream" -> connection
+    int net_streams = 4;                       // OCM_NET_STREAMS: parallel connections per owner
+    uint64_t net_split_min = 1ull << 20;       // OCM_NET_SPLIT_MIN: smallest part worth its own stream
     // Local GPU halves: stream-ordered pool (no device-wide sync in free, freed
     // blocks reused without a new VA mapping). Reference K8: cudaMalloc/cudaFree.
     hipMemPool_t pool = nullptr;
@@ -276,8 +284,8 @@ int run_batch(lib_alloc *a, XferBatchArgs &args, std::vector<XferBatchOp> &v, bo
 int batch_put_abs(lib_alloc *dst, std::vector<XferBatchOp> &v);
 
 // ---- network tier (net.cpp)
-int net_conn(const std::string &ep, uint64_t token);
 void net_drop(const std::string &ep);
+void net_close_all();
 int net_piece(const Extent &e, bool put, char *lin, Loc lloc, uint64_t ext_off, uint64_t len);
 
 #pragma GCC visibility pop

@@ -34,6 +34,8 @@ int ocm_init(void) {
     s.daemon_mbox = daemon_mailbox_name(s.daemon_rank, s.ns);
     s.rpc_timeout_ms = env_int("OCM_RPC_TIMEOUT_MS", 60000);
     s.rpc_spin_ns = (uint64_t)std::max(0, env_int("OCM_RPC_SPIN_US", 50)) * 1000;
+    s.net_streams = std::max(1, std::min(env_int("OCM_NET_STREAMS", 4), 64));
+    if (const char *ns = std::getenv("OCM_NET_SPLIT_MIN")) s.net_split_min = std::max(4096ull, std::strtoull(ns, nullptr, 0));
     const int connect_ms = env_int("OCM_CONNECT_TIMEOUT_MS", 10000);
     // Connect to the daemon mailbox, retrying while it starts (reference: 10 x 10 ms).
     long deadline = now_ms() + connect_ms;
@@ -123,13 +125,7 @@ int ocm_tini(void) {
     }
     s.imports.clear();
     service_stop();
-    for (auto &kv : s.net_conns) close(kv.second);
-    s.net_conns.clear();
-    if (s.net_stage) {
-        DeviceGuard g(s.device);
-        (void)hipHostFree(s.net_stage);
-        s.net_stage = nullptr;
-    }
+    net_close_all();
     for (auto st : s.lanes) {
         DeviceGuard g(s.device);
         (void)hipStreamSynchronize(st);

@@ -83,3 +83,23 @@ def test_owner_loss_fails_network_ops(mesh_factory):
             for _ in range(50):  # the first op may still drain into the socket buffer
                 a.put(0, 0, 1 << 20)
                 a.get(0, 0, 1 << 20)
+
+
+@pytest.mark.parametrize("streams", ["1", "3"])
+def test_parallel_streams_odd_split(mesh_factory, monkeypatch, streams):
+    """Large network-tier ops are cut into parts on parallel connections
+    (OCM_NET_STREAMS); odd sizes and offsets must land byte-exact."""
+    monkeypatch.setenv("OCM_NET_STREAMS", streams)
+    monkeypatch.setenv("OCM_NET_SPLIT_MIN", str(1 << 20))
+    m = mesh_factory(2, rank_env=hosts("nodeA", "nodeB"))
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        n = 16 << 20
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=n, remote_bytes=n)
+        assert a.remote_info()["extents"][0]["net"]
+        for i, (size, loff, roff) in enumerate([((5 << 20) + 123, 4, 4096 + 7), (n - 8, 0, 8), (3 << 20, 12, 0)]):
+            a.fill(seed=50 + i)
+            a.put(loff, roff, size)
+            a.fill(seed=0)
+            a.get(loff, roff, size)
+            assert a.check(seed=50 + i, offset=loff, nbytes=size - size % 4, first_word=loff // 4) == 0, size
+        a.free()
