@@ -33,9 +33,6 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# (variant 1 register / 2 LDS-DMA, grid cap 0 = default, nontemporal stores)
-TUNING_GRID = {"reg_default": (1, 0, 1), "reg_b256": (1, 256, 1), "reg_b1024": (1, 1024, 1), "reg_b2048": (1, 2048, 1),
-               "reg_nt0": (1, 0, 0), "lds_default": (2, 0, 1), "lds_b512": (2, 512, 1)}
 METRIC = "remote put/get GiB/s + p50 ocm_alloc latency, 4 KiB-1 GiB, 1/2/4/8 MI355X"
 GiB = float(1 << 30)
 
@@ -53,7 +50,9 @@ def parse():
                     help="auto: governor placement; loopback: the rank's own daemon HBM (IPC); host: pinned host tier")
     ap.add_argument("--alloc-samples", type=int, default=200)
     ap.add_argument("--no-characterize", action="store_true")
-    ap.add_argument("--no-tuning-sweep", action="store_true", help="skip the N>1 xGMI tuning extras")
+    ap.add_argument("--no-autotune", action="store_true",
+                    help="N>1: skip the setup-time kernel autotune over the xGMI links (library defaults)")
+    ap.add_argument("--no-hw-baseline", action="store_true", help="skip the N>1 runtime peer-copy extras")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -84,31 +83,6 @@ def _local(fn):
         return fn(), None
     except Exception as e:  # noqa: BLE001 - recorded, never fatal
         return None, repr(e)[:200]
-
-
-def xgmi_tuning_extras(pair, dist, world: int, max_bytes: int) -> dict:
-    """put/get GiB/s of each kernel configuration, all ranks at once (all-to-all load)."""
-    from oncilla_amd import api
-
-    n_t = min(256 << 20, max_bytes)
-    out = {}
-    for name, (variant, blocks, nt) in TUNING_GRID.items():
-        _, et = _local(lambda: api.set_tuning(variant, blocks, bool(nt)))
-        if dist is not None:
-            dist.barrier()
-        tp, ep = _local(lambda: pair.time_onesided(1, n_t, 3))
-        if dist is not None:
-            dist.barrier()
-        tg, eg = _local(lambda: pair.time_onesided(0, n_t, 3))
-        res = gather_obj(dist, {"put": tp, "get": tg, "err": et or ep or eg}, world)
-        errs = [r["err"] for r in res if r["err"]]
-        if errs:
-            out[name] = {"error": errs[0]}
-        else:
-            out[name] = {"put_GiBps": round(world * n_t / max(r["put"] for r in res) / GiB, 2),
-                         "get_GiBps": round(world * n_t / max(r["get"] for r in res) / GiB, 2)}
-    _local(lambda: api.set_tuning())
-    return out
 
 
 def hw_baseline_extras(dist, world: int, rank: int, local_rank: int) -> dict:
@@ -228,6 +202,13 @@ def main() -> int:
         pair = client.alloc(remote_kind, local_bytes=pair_bytes, remote_bytes=pair_bytes, flags=rflags)
         info = pair.remote_info()
 
+        # ---- setup (untimed): pick the put/get kernel configuration over the
+        # xGMI links, every rank at once (all-to-all load), slowest rank decides ----
+        tuned = None
+        if use_gpu and world > 1 and not args.no_autotune:
+            tuned = wl.autotune(pair, min(256 << 20, max_bytes), reps=3,
+                                gather=lambda obj: gather_obj(dist, obj, world))
+
         # verify: pattern -> put -> clobber -> get -> check
         pair.fill(seed=1234 + rank, nbytes=max_bytes)
         pair.put(0, 0, max_bytes)
@@ -276,9 +257,8 @@ def main() -> int:
         # ---- extras for N > 1, after the timed region (never affect the metric) ----
         # Every rank reaches every collective below even when its local part
         # fails, so a failure is recorded instead of deadlocking the job.
-        tuning, baseline = {}, {}
-        if use_gpu and world > 1 and not args.no_tuning_sweep:
-            tuning = xgmi_tuning_extras(pair, dist, world, max_bytes)
+        baseline = {}
+        if use_gpu and world > 1 and not args.no_hw_baseline:
             baseline = hw_baseline_extras(dist, world, rank, local_rank)
         pair.free()
         if dist is not None:
@@ -318,8 +298,8 @@ def main() -> int:
             "local_alloc_p50_us": round(max(s["lat_local"]["alloc_p50_us"] for s in stats), 2),
             "sweep": sweep,
         }
-        if tuning:
-            result["xgmi_tuning_256MiB"] = tuning
+        if tuned:
+            result["autotune"] = tuned
         if baseline:
             result["hw_baseline"] = baseline
     finally:

@@ -148,6 +148,9 @@ struct State {
     std::map<SlabKey, Mapping> imports;
     std::set<lib_alloc *> allocs;
     XferTuning tuning;
+    // Per-direction override ([0] get, [1] put) for one-sided kernel ops,
+    // set by an autotune (variant XFER_AUTO: use `tuning`).
+    XferTuning dir_tuning[2];
     bool host_engine_kernel = false;
     uint64_t host_kernel_max = 0;  // measured: SDMA beats the kernel on registered host slabs
     int sync_mode = 0;             // 0 stream sync, 1 spin on an event, 2 blocking event sync

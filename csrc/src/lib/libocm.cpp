@@ -623,6 +623,22 @@ void ocm_x_set_tuning(int variant, int blocks, int nt) {
     s.tuning.variant = variant;
     s.tuning.max_blocks = blocks;
     s.tuning.nontemporal = nt != 0;
+    s.dir_tuning[0] = s.dir_tuning[1] = XferTuning{};
+}
+
+// Per-direction override of one-sided kernel ops (dir 0 get, 1 put), e.g. the
+// winner of an autotune over the xGMI links; variant 0 clears it.
+int ocm_x_set_tuning_dir(int dir, int variant, int blocks, int nt) {
+    if (dir != 0 && dir != 1) return -1;
+    if (variant < XFER_AUTO || variant > XFER_LDS || blocks < 0) return -1;
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    XferTuning t;
+    t.variant = variant;
+    t.max_blocks = blocks;
+    t.nontemporal = nt != 0;
+    s.dir_tuning[dir] = t;
+    return 0;
 }
 
 // Link type (hipExtLinkType) and hop count between two devices; -1 on error.

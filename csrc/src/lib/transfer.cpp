@@ -317,7 +317,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
             if (sh < 0) OCM_FAIL(-1, "stripe unit %llu is not a power of two", (unsigned long long)a->stripe_unit);
             x.unit_shift = (uint32_t)sh;
         }
-        XferTuning t = s.tuning;
+        XferTuning t = s.dir_tuning[put ? 1 : 0].variant != XFER_AUTO ? s.dir_tuning[put ? 1 : 0] : s.tuning;
         if (t.variant == XFER_AUTO) {
             // Measured (profiles/ksweep_r01.json): LDS-DMA staging wins HBM->HBM
             // copies up to ~256 MiB on the same GPU; everything else (peer HBM

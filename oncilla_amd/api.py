@@ -174,6 +174,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
             "ocm_x_set_tuning": (None, [i32, i32, i32]),
+            "ocm_x_set_tuning_dir": (i32, [i32, i32, i32, i32]),
             "ocm_x_batch": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, ctypes.POINTER(u64), i32, i32]),
             "ocm_x_link_info": (i32, [i32, i32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
         }
@@ -271,6 +272,13 @@ def batch_ops(ops) -> BatchOps:
 def set_tuning(variant: int = 0, blocks: int = 0, nontemporal: bool = True) -> None:
     """Transfer-kernel tuning for this process (0 auto / 1 register / 2 LDS-DMA; grid cap; nt stores)."""
     load().ocm_x_set_tuning(variant, blocks, 1 if nontemporal else 0)
+
+
+def set_tuning_dir(op_flag: int, variant: int = 0, blocks: int = 0, nontemporal: bool = True) -> None:
+    """Per-direction override for one-sided kernel ops (op_flag 0 get, 1 put); variant 0 clears it.
+    ``set_tuning`` clears both overrides."""
+    if load().ocm_x_set_tuning_dir(op_flag, variant, blocks, 1 if nontemporal else 0) != 0:
+        raise ValueError(f"bad tuning: op_flag={op_flag} variant={variant} blocks={blocks}")
 
 
 def link_info(dev: int, peer: int) -> Optional[dict]:

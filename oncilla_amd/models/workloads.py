@@ -71,6 +71,62 @@ def characterize(alloc: api.Allocation, sizes: Iterable[int], target_s: float = 
     return out
 
 
+# Kernel configurations an autotune chooses from: (variant 0 auto / 1 register /
+# 2 LDS-DMA, grid cap 0 = default, nontemporal destination stores).
+TUNING_CANDIDATES = {"auto": (0, 0, 1), "reg_b256": (1, 256, 1), "reg_b1024": (1, 1024, 1),
+                     "reg_b2048": (1, 2048, 1), "reg_nt0": (1, 0, 0), "lds_default": (2, 0, 1),
+                     "lds_b512": (2, 512, 1)}
+
+
+def autotune(alloc: api.Allocation, nbytes: int, reps: int = 3, gather=None, candidates: dict | None = None) -> dict:
+    """Pick the transfer-kernel configuration per direction for allocations like `alloc`.
+
+    Every candidate is timed for get and put of `nbytes` (after one untimed op,
+    which also pays any first touch of imported slabs). With `gather` (an
+    all-gather of one picklable object over the job) every rank measures at
+    the same time, so the numbers include the all-to-all load on the xGMI
+    links, and a candidate's time is the slowest rank's. A candidate that
+    fails on any rank is out. The fastest per direction is installed with
+    `api.set_tuning_dir`; "auto" (the library default) is always a candidate,
+    so the choice is never slower than the default as measured. Overwrites the
+    first `nbytes` of both halves.
+    """
+    cands = dict(candidates or TUNING_CANDIDATES)
+    cands.setdefault("auto", (0, 0, 1))
+    gather = gather or (lambda obj: [obj])
+    table = {}
+    for name, (variant, blocks, nt) in cands.items():
+        row = {}
+        for op, key in ((0, "get"), (1, "put")):
+            t, err = None, None
+            try:
+                api.set_tuning_dir(op, variant, blocks, bool(nt))
+                alloc.time_onesided(op, nbytes, 1)
+            except Exception as e:  # noqa: BLE001 - recorded; every rank still reaches every gather
+                err = repr(e)[:160]
+            gather(None)  # start together
+            if err is None:
+                try:
+                    t = alloc.time_onesided(op, nbytes, reps)
+                except Exception as e:  # noqa: BLE001
+                    err = repr(e)[:160]
+            res = gather((t, err))
+            errs = [r[1] for r in res if r[1]]
+            row[key] = {"error": errs[0]} if errs else {"s": max(r[0] for r in res)}
+        table[name] = row
+    best = {}
+    for op, key in ((0, "get"), (1, "put")):
+        ok = {n: r[key]["s"] for n, r in table.items() if "s" in r[key]}
+        pick = min(ok, key=ok.get) if ok else "auto"
+        variant, blocks, nt = cands[pick]
+        api.set_tuning_dir(op, variant, blocks, bool(nt))
+        best[key] = pick
+    ranks = len(gather(None))
+    return {"get": best["get"], "put": best["put"], "bytes": nbytes, "ranks": ranks,
+            "GiBps": {n: {k: (round(ranks * nbytes / v["s"] / (1 << 30), 2) if "s" in v else v)
+                          for k, v in r.items()} for n, r in table.items()}}
+
+
 def spill_probe(client: api.Client, chunk_bytes: int, max_chunks: int) -> dict:
     """Allocate remote chunks until HBM capacity runs out; count host-tier spills."""
     allocs, tiers = [], {api.OCM_TIER_GPU: 0, api.OCM_TIER_HOST: 0}

@@ -46,13 +46,45 @@ def test_bench_extras_helpers_run(native):
     sys.path.insert(0, REPO)
     import bench
 
-    class FakePair:
-        def time_onesided(self, op, n, iters):
-            return 1e-3
-
-    t = bench.xgmi_tuning_extras(FakePair(), None, 2, 1 << 20)
-    assert set(t) == set(bench.TUNING_GRID)
-    assert all("put_GiBps" in v and "error" not in v for v in t.values()), t
     b = bench.hw_baseline_extras(None, 2, 0, 0)
     assert isinstance(b, dict)
     assert bench._local(lambda: 1 / 0)[1].startswith("ZeroDivisionError")
+
+
+def test_autotune_picks_fastest_by_slowest_rank(native, monkeypatch):
+    """workloads.autotune: per-direction pick by the slowest rank, failing candidates
+    excluded, and the same number of collectives on every path (no deadlock)."""
+    from oncilla_amd import api
+    from oncilla_amd.models import workloads as wl
+
+    cur = {}
+    monkeypatch.setattr(api, "set_tuning_dir", lambda op, v, b, nt: cur.__setitem__(op, (v, b, nt)))
+    # seconds per (variant, blocks, nt, op) on this rank; the "other rank" is 2x slower on reg_b256 puts
+    cands = {"auto": (0, 0, 1), "reg_b256": (1, 256, 1), "lds_default": (2, 0, 1), "broken": (1, 64, 0)}
+    mine = {(0, 0, 1): (3.0, 3.0), (1, 256, 1): (2.0, 1.0), (2, 0, 1): (1.5, 2.5)}
+
+    class FakePair:
+        last = None
+
+        def time_onesided(self, op, n, iters):
+            cfg = self.last = cur[op]
+            if cfg == (1, 64, 0):
+                raise RuntimeError("launch failed")
+            return mine[cfg][op]
+
+    pair = FakePair()
+    calls = []
+
+    def gather(obj):  # two ranks; the other one is 4x slower with reg_b256
+        calls.append(obj)
+        if isinstance(obj, tuple) and obj[0] is not None and pair.last == (1, 256, 1):
+            return [obj, (obj[0] * 4.0, None)]
+        return [obj, obj]
+
+    r = wl.autotune(pair, 1 << 20, gather=gather, candidates=cands)
+    assert r["get"] == "lds_default", r
+    assert r["put"] == "lds_default", r  # reg_b256 is fastest here but not on the other rank
+    assert "error" in r["GiBps"]["broken"]["get"] and "error" in r["GiBps"]["broken"]["put"]
+    # 2 gathers per (candidate, direction) + 1 for the rank count
+    assert len(calls) == 2 * 2 * len(cands) + 1
+    assert cur[0] == cands[r["get"]] and cur[1] == cands[r["put"]]
