@@ -112,14 +112,20 @@ hipError_t xfer_batch_launch(const XferBatchArgs &a, const XferTuning &t, hipStr
 
 // ---- persistent copy service (low-latency blocking one-sided ops) ----
 // A resident gang of `blocks` workgroups. Workgroup 0 polls a 128-byte request
-// record in host-pinned coherent memory: {seq, sum, args}. One wave reads the
-// whole record in a single pass; `sum` (a hash of seq and the args, written
-// before seq) proves the args it read belong to that seq, so a request costs
-// one PCIe read round trip, not two. Requests of at most `solo_tiles` tiles
-// are copied by workgroup 0 alone; larger ones are published to the rest of
-// the gang through a device-memory box (agent-scope release/acquire), every
-// workgroup copies its share of tiles, and the last one to finish (device
-// counter) makes the bytes visible system-wide and publishes `done = seq`.
+// record {seq, sum, args} (ServiceReq). One wave reads the whole record in a
+// single pass; `sum` (a hash of seq and the args) proves the args it read
+// belong to that seq, so torn or reordered writes of the record (the host's
+// write-combining buffer may reorder them) are simply read again.
+// Where the record lives: preferably in fine-grained HBM of the service's own
+// GPU that the CPU writes through the PCIe BAR (the kernel then polls its own
+// memory: 4 KiB op 4.26 -> 2.76 us, tools/vram_doorbell_probe.hip,
+// profiles/vram_doorbell_r01.json); otherwise in the first 128 bytes of the
+// host-pinned ServiceSlot, polled across PCIe.
+// Requests of at most `solo_tiles` tiles are copied by workgroup 0 alone;
+// larger ones are published to the rest of the gang through a device-memory
+// box (agent-scope release/acquire), every workgroup copies its share of
+// tiles, and the last one to finish (device counter) makes the bytes visible
+// system-wide and publishes `done = seq` in the host-pinned slot.
 // Bounded: workgroup 0 exits on kServiceStop or after `idle_ticks` of
 // s_memrealtime (100 MHz) without work, and takes the gang with it; `exited`
 // records the first seq it did not serve.
@@ -127,10 +133,15 @@ constexpr unsigned long long kServiceStop = ~0ull;
 constexpr int kServiceArgWords = (int)((sizeof(XferArgs) + 7) / 8);
 static_assert(kServiceArgWords <= 14, "service request record holds 14 argument words");
 
-struct alignas(128) ServiceSlot {
+struct alignas(128) ServiceReq {
     unsigned long long seq;           // host -> device, written last
     unsigned long long sum;           // service_sum(seq, args)
     unsigned long long args[14];      // XferArgs, host -> device
+};
+static_assert(sizeof(ServiceReq) == 128, "service request layout");
+
+struct alignas(128) ServiceSlot {
+    ServiceReq req;                   // the request record when it is not in HBM
     unsigned long long done;          // device -> host (own cache line)
     unsigned long long exited;        // device -> host: first seq NOT served when it left
     unsigned long long pad[14];
@@ -148,10 +159,13 @@ struct alignas(128) ServiceBox {
     unsigned long long pad2[2];
 };
 
-// Post one request (args, then sum, then seq with release) for the service.
-void service_post(ServiceSlot *slot, const XferArgs &a, unsigned long long seq);
+// Post one request (args, sum, then seq with release) and flush the CPU's
+// write-combining buffers, so a BAR-mapped record reaches the GPU now.
+void service_post(ServiceReq *req, const XferArgs &a, unsigned long long seq);
+// Store one word of the record (seq: 0 to re-arm, kServiceStop) and flush.
+void service_store_seq(ServiceReq *req, unsigned long long seq);
 
-hipError_t service_launch(ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
+hipError_t service_launch(ServiceReq *req, ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
                           unsigned long long idle_ticks, unsigned blocks, unsigned solo_tiles, hipStream_t stream);
 
 // Deterministic 32-bit word pattern (word i of a buffer) for data verification.

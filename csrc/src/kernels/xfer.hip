@@ -471,7 +471,7 @@ __device__ __forceinline__ void service_gang_done(ServiceSlot *slot, ServiceBox 
     }
 }
 
-__global__ __launch_bounds__(kThreads) void service_kernel(ServiceSlot *slot, ServiceBox *box,
+__global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq, ServiceSlot *slot, ServiceBox *box,
                                                            unsigned long long first_seq,
                                                            unsigned long long idle_ticks, unsigned solo_tiles) {
     __shared__ __attribute__((aligned(16))) unsigned long long sh[16];
@@ -517,7 +517,7 @@ __global__ __launch_bounds__(kThreads) void service_kernel(ServiceSlot *slot, Se
     }
     unsigned long long expect = first_seq;
     unsigned long long idle_start = __builtin_amdgcn_s_memrealtime();
-    unsigned long long *req = reinterpret_cast<unsigned long long *>(slot);
+    const unsigned long long *req = reinterpret_cast<const unsigned long long *>(rq);
     for (;;) {
         if (tid < 64) {
             // One wave reads the whole request record per poll (lanes 0..15).
@@ -576,24 +576,30 @@ __global__ __launch_bounds__(kThreads) void service_kernel(ServiceSlot *slot, Se
 
 }  // namespace
 
-void service_post(ServiceSlot *slot, const XferArgs &a, unsigned long long seq) {
+void service_post(ServiceReq *req, const XferArgs &a, unsigned long long seq) {
     unsigned long long w[kServiceArgWords] = {};
     std::memcpy(w, &a, sizeof(a));
     unsigned long long h = service_mix(0, seq);
     for (int i = 0; i < kServiceArgWords; i++) {
         h = service_mix(h, w[i]);
-        __atomic_store_n(&slot->args[i], w[i], __ATOMIC_RELAXED);
+        __atomic_store_n(&req->args[i], w[i], __ATOMIC_RELAXED);
     }
-    __atomic_store_n(&slot->sum, h, __ATOMIC_RELAXED);
-    __atomic_store_n(&slot->seq, seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&req->sum, h, __ATOMIC_RELAXED);
+    __atomic_store_n(&req->seq, seq, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();  // drain write-combining buffers (BAR-mapped HBM record)
 }
 
-hipError_t service_launch(ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
+void service_store_seq(ServiceReq *req, unsigned long long seq) {
+    __atomic_store_n(&req->seq, seq, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
+}
+
+hipError_t service_launch(ServiceReq *req, ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
                           unsigned long long idle_ticks, unsigned blocks, unsigned solo_tiles, hipStream_t stream) {
-    if (!slot || !box || blocks == 0) return hipErrorInvalidValue;
+    if (!req || !slot || !box || blocks == 0) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(box, 0, sizeof(ServiceBox), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(service_kernel, dim3(blocks), dim3(kThreads), 0, stream, slot, box, first_seq, idle_ticks,
+    hipLaunchKernelGGL(service_kernel, dim3(blocks), dim3(kThreads), 0, stream, req, slot, box, first_seq, idle_ticks,
                        solo_tiles);
     return hipGetLastError();
 }

@@ -157,6 +157,8 @@ struct State {
     OpCounters ctr;
     // persistent copy service (small blocking one-sided ops)
     ServiceSlot *svc = nullptr;
+    ServiceReq *svc_req = nullptr;   // request record: BAR-mapped HBM, or &svc->req
+    bool svc_req_hbm = false;
     ServiceBox *svc_box = nullptr;   // device-memory mailbox of the gang
     hipStream_t svc_stream = nullptr;
     unsigned svc_blocks = kServiceBlocksDefault;          // gang size (OCM_SERVICE_BLOCKS)

@@ -126,6 +126,51 @@ int sync_stream() {
 
 // ---- persistent copy service ----
 
+// True when [p, p + n) lies in one CPU mapping with write permission
+// (/proc/self/maps). Device memory the runtime did not map for the CPU is
+// either absent there or a PROT_NONE reservation.
+static bool cpu_writable(const void *p, size_t n) {
+    FILE *f = std::fopen("/proc/self/maps", "r");
+    if (!f) return false;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p), b = a + n;
+    char line[512];
+    bool ok = false;
+    while (std::fgets(line, sizeof(line), f)) {
+        unsigned long lo = 0, hi = 0;
+        char perms[8] = {};
+        if (std::sscanf(line, "%lx-%lx %7s", &lo, &hi, perms) != 3) continue;
+        if (a >= lo && b <= hi) {
+            ok = perms[0] == 'r' && perms[1] == 'w';
+            break;
+        }
+    }
+    std::fclose(f);
+    return ok;
+}
+
+// The copy service's request record: fine-grained HBM of this GPU written by
+// the CPU through the BAR when the runtime maps it for the CPU (the kernel
+// then polls local memory), else the host-pinned slot. OCM_SERVICE_DOORBELL=host
+// forces the latter.
+static void service_pick_doorbell(State &s) {
+    s.svc_req = &s.svc->req;
+    s.svc_req_hbm = false;
+    const char *mode = std::getenv("OCM_SERVICE_DOORBELL");
+    if (mode && !std::strcmp(mode, "host")) return;
+    void *p = nullptr;
+    if (hipExtMallocWithFlags(&p, sizeof(ServiceReq), hipDeviceMallocFinegrained) != hipSuccess || !p) {
+        (void)hipGetLastError();
+        return;
+    }
+    if (!cpu_writable(p, sizeof(ServiceReq)) || hipMemset(p, 0, sizeof(ServiceReq)) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(p);
+        return;
+    }
+    s.svc_req = static_cast<ServiceReq *>(p);
+    s.svc_req_hbm = true;
+}
+
 int service_start(unsigned long long first_seq) {
     State &s = S();
     DeviceGuard g(s.device);
@@ -138,6 +183,7 @@ int service_start(unsigned long long first_seq) {
             OCM_FAIL(-1, "copy service: no coherent host memory");
         }
         std::memset(s.svc, 0, sizeof(ServiceSlot));
+        service_pick_doorbell(s);
         if (hipMalloc(reinterpret_cast<void **>(&s.svc_box), sizeof(ServiceBox)) != hipSuccess) {
             (void)hipGetLastError();
             s.svc_box = nullptr;
@@ -151,8 +197,8 @@ int service_start(unsigned long long first_seq) {
         }
     }
     __atomic_store_n(&s.svc->exited, 0ull, __ATOMIC_RELEASE);
-    __atomic_store_n(&s.svc->seq, 0ull, __ATOMIC_RELEASE);  // clear a STOP left by a parked instance
-    if (service_launch(s.svc, s.svc_box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_solo_tiles, s.svc_stream) !=
+    service_store_seq(s.svc_req, 0ull);  // clear a STOP left by a parked instance
+    if (service_launch(s.svc_req, s.svc, s.svc_box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_solo_tiles, s.svc_stream) !=
         hipSuccess) {
         (void)hipGetLastError();
         s.svc_max = 0;
@@ -168,7 +214,7 @@ void service_park() {
     State &s = S();
     if (!s.svc || !s.svc_running) return;
     DeviceGuard g(s.device);
-    __atomic_store_n(&s.svc->seq, kServiceStop, __ATOMIC_RELEASE);
+    service_store_seq(s.svc_req, kServiceStop);
     (void)hipStreamSynchronize(s.svc_stream);
     s.svc_running = false;
 }
@@ -178,11 +224,14 @@ void service_stop() {
     if (!s.svc) return;
     DeviceGuard g(s.device);
     if (s.svc_running) {
-        __atomic_store_n(&s.svc->seq, kServiceStop, __ATOMIC_RELEASE);
+        service_store_seq(s.svc_req, kServiceStop);
         (void)hipStreamSynchronize(s.svc_stream);
         s.svc_running = false;
     }
     (void)hipStreamDestroy(s.svc_stream);
+    if (s.svc_req_hbm) (void)hipFree(s.svc_req);
+    s.svc_req = nullptr;
+    s.svc_req_hbm = false;
     (void)hipHostFree(s.svc);
     if (s.svc_box) (void)hipFree(s.svc_box);
     s.svc = nullptr;
@@ -196,7 +245,7 @@ int service_xfer(XferArgs x) {
     if (xfer_normalize(x) != hipSuccess) OCM_FAIL(-1, "invalid transfer");
     const unsigned long long seq = ++s.svc_seq;
     if (!s.svc_running && service_start(seq) != 0) return -1;
-    service_post(s.svc, x, seq);
+    service_post(s.svc_req, x, seq);
     const uint64_t t0 = now_ns();
     for (unsigned spins = 1;; spins++) {
         if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
@@ -210,7 +259,7 @@ int service_xfer(XferArgs x) {
                 s.svc_running = false;
                 if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
                 if (service_start(seq) != 0) return -1;
-                service_post(s.svc, x, seq);  // start cleared the doorbell: re-post
+                service_post(s.svc_req, x, seq);  // start cleared the doorbell: re-post
             }
             if (now_ns() - t0 > 10ull * 1000000000ull) OCM_FAIL(-1, "copy service did not complete a transfer in 10 s");
         }

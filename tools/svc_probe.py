@@ -21,6 +21,9 @@ sys.path.insert(0, REPO)
 
 SIZES = [4096 << i for i in range(15)]  # 4 KiB .. 64 MiB
 CONFIGS = {"launch": {"OCM_SERVICE_MAX": "0"}, "launch_event": {"OCM_SERVICE_MAX": "0", "OCM_LAUNCH_FLAG": "0"}}
+# library defaults; and the same with the request record in host memory instead of BAR-mapped HBM
+CONFIGS["default"] = {}
+CONFIGS["default_hostbell"] = {"OCM_SERVICE_DOORBELL": "host"}
 for g in (1, 16, 32, 64, 128, 256):
     CONFIGS[f"svc_g{g}"] = {"OCM_SERVICE_MAX": str(64 << 20), "OCM_SERVICE_BLOCKS": str(g)}
 
