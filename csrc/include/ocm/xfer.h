@@ -112,15 +112,16 @@ hipError_t xfer_batch_launch(const XferBatchArgs &a, const XferTuning &t, hipStr
 
 // ---- persistent copy service (low-latency blocking one-sided ops) ----
 // A resident gang of `blocks` workgroups. Workgroup 0 polls a 128-byte request
-// record {seq, sum, args} (ServiceReq). One wave reads the whole record in a
+// record {args, sum, seq} (ServiceReq). One wave reads the whole record in a
 // single pass; `sum` (a hash of seq and the args) proves the args it read
 // belong to that seq, so torn or reordered writes of the record (the host's
 // write-combining buffer may reorder them) are simply read again.
-// Where the record lives: preferably in fine-grained HBM of the service's own
-// GPU that the CPU writes through the PCIe BAR (the kernel then polls its own
-// memory: 4 KiB op 4.26 -> 2.76 us, tools/vram_doorbell_probe.hip,
-// profiles/vram_doorbell_r01.json); otherwise in the first 128 bytes of the
-// host-pinned ServiceSlot, polled across PCIe.
+// Where the record lives: in the first 128 bytes of the host-pinned
+// ServiceSlot, polled across PCIe (default), or in fine-grained HBM of the
+// service's own GPU that the CPU writes through the PCIe BAR
+// (OCM_SERVICE_DOORBELL=hbm; then one lane polls the seq word in local memory).
+// Measured both ways: profiles/vram_doorbell_r01.json (bare probe: HBM wins),
+// profiles/svc_doorbell_r01.json (library: host wins by 0.4-0.7 us).
 // Requests of at most `solo_tiles` tiles are copied by workgroup 0 alone;
 // larger ones are published to the rest of the gang through a device-memory
 // box (agent-scope release/acquire), every workgroup copies its share of
@@ -134,17 +135,20 @@ constexpr int kServiceArgWords = (int)((sizeof(XferArgs) + 7) / 8);
 static_assert(kServiceArgWords <= 14, "service request record holds 14 argument words");
 
 struct alignas(128) ServiceReq {
-    unsigned long long seq;           // host -> device, written last
-    unsigned long long sum;           // service_sum(seq, args)
-    unsigned long long args[14];      // XferArgs, host -> device
+    unsigned long long args[14];      // XferArgs, host -> device (words 0..13)
+    unsigned long long sum;           // service_sum(seq, args) (word 14)
+    unsigned long long seq;           // host -> device, written last (word 15, second cache line)
 };
 static_assert(sizeof(ServiceReq) == 128, "service request layout");
+static_assert(__builtin_offsetof(ServiceReq, seq) == 120 && __builtin_offsetof(ServiceReq, sum) == 112,
+              "the kernel reads seq/sum as words 15/14");
 
 struct alignas(128) ServiceSlot {
     ServiceReq req;                   // the request record when it is not in HBM
     unsigned long long done;          // device -> host (own cache line)
     unsigned long long exited;        // device -> host: first seq NOT served when it left
-    unsigned long long pad[14];
+    unsigned long long gpu_ticks;     // device -> host: sum of doorbell-seen -> done ticks (100 MHz)
+    unsigned long long pad[13];
 };
 static_assert(sizeof(ServiceSlot) == 256, "service slot layout");
 
@@ -165,8 +169,10 @@ void service_post(ServiceReq *req, const XferArgs &a, unsigned long long seq);
 // Store one word of the record (seq: 0 to re-arm, kServiceStop) and flush.
 void service_store_seq(ServiceReq *req, unsigned long long seq);
 
+// hbm_bell: `req` is in this GPU's HBM (poll its seq word alone, then read the record).
 hipError_t service_launch(ServiceReq *req, ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
-                          unsigned long long idle_ticks, unsigned blocks, unsigned solo_tiles, hipStream_t stream);
+                          unsigned long long idle_ticks, unsigned blocks, unsigned solo_tiles, bool hbm_bell,
+                          hipStream_t stream);
 
 // Deterministic 32-bit word pattern (word i of a buffer) for data verification.
 hipError_t pattern_fill(void *p, uint64_t words, uint64_t first_word, uint32_t seed, hipStream_t stream);

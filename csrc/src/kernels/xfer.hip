@@ -473,7 +473,8 @@ __device__ __forceinline__ void service_gang_done(ServiceSlot *slot, ServiceBox 
 
 __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq, ServiceSlot *slot, ServiceBox *box,
                                                            unsigned long long first_seq,
-                                                           unsigned long long idle_ticks, unsigned solo_tiles) {
+                                                           unsigned long long idle_ticks, unsigned solo_tiles,
+                                                           unsigned hbm_bell) {
     __shared__ __attribute__((aligned(16))) unsigned long long sh[16];
     const int tid = threadIdx.x;
     if (blockIdx.x != 0) {
@@ -517,20 +518,36 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
     }
     unsigned long long expect = first_seq;
     unsigned long long idle_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long ticks_sum = __hip_atomic_load(&slot->gpu_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned long long *req = reinterpret_cast<const unsigned long long *>(rq);
     for (;;) {
         if (tid < 64) {
             // One wave reads the whole request record per poll (lanes 0..15).
+            // A record in this GPU's HBM is polled through its seq word alone
+            // (one lane, cheap local reads) and read whole once seq moved.
             unsigned long long w = 0, s;
             for (;;) {
+                if (hbm_bell) {
+                    unsigned long long q = 0;
+                    if (tid == 0) q = __hip_atomic_load(req + 15, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    q = readlane64(q, 0);
+                    if (q != expect && q != kServiceStop) {
+                        if (__builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks) {
+                            s = kServiceStop;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                }
                 if (tid < 16) w = __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                s = readlane64(w, 0);
+                s = readlane64(w, 15);
                 if (s == kServiceStop) break;
                 if (s == expect) {
                     unsigned long long h = service_mix(0, s);
 #pragma unroll
-                    for (int i = 0; i < kServiceArgWords; i++) h = service_mix(h, readlane64(w, 2 + i));
-                    if (h == readlane64(w, 1)) break;
+                    for (int i = 0; i < kServiceArgWords; i++) h = service_mix(h, readlane64(w, i));
+                    if (h == readlane64(w, 14)) break;
                     continue;  // seq landed before the args: read the record again
                 }
                 if (__builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks) {
@@ -540,12 +557,13 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                 __builtin_amdgcn_s_sleep(8);  // ~0.2 us between PCIe polls
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // order the data loads after the doorbell
-            if (tid < 16) sh[tid] = w;
+            if (tid < kServiceArgWords) sh[2 + tid] = w;  // args -> sh[2..]
             if (tid == 0) sh[0] = s;
         }
         __syncthreads();
         const unsigned long long s = sh[0];
         if (s == kServiceStop) break;
+        const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
         const uint64_t ntiles = service_tiles(*reinterpret_cast<const XferArgs *>(sh + 2));
         if (gridDim.x > 1 && ntiles > solo_tiles) {
             const unsigned long long active = ntiles < gridDim.x ? ntiles : gridDim.x;
@@ -557,7 +575,7 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
             __syncthreads();
             if (tid == 0) __hip_atomic_store(&box->seq, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             service_copy(sh, 0, active);
-            service_gang_done(slot, box, s, active);
+            service_gang_done(slot, box, s, active);  // gpu_ticks: until workgroup 0's share is out
         } else {
             service_copy(sh, 0, 1);
             // Make the bytes visible to the host, other kernels and DMA (system scope).
@@ -565,6 +583,10 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
             if (tid == 0) __hip_atomic_store(&slot->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         idle_start = __builtin_amdgcn_s_memrealtime();  // every lane: the idle test must stay wave-uniform
+        // Diagnostic, after `done` so it never delays it: a running sum in a
+        // register, published with a plain store (no PCIe atomic round trip).
+        ticks_sum += idle_start - t_seen;
+        if (tid == 0) __hip_atomic_store(&slot->gpu_ticks, ticks_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         expect++;
         __syncthreads();  // sh is rewritten by the next poll
     }
@@ -577,16 +599,20 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
 }  // namespace
 
 void service_post(ServiceReq *req, const XferArgs &a, unsigned long long seq) {
-    unsigned long long w[kServiceArgWords] = {};
+    unsigned long long w[14] = {};
     std::memcpy(w, &a, sizeof(a));
     unsigned long long h = service_mix(0, seq);
-    for (int i = 0; i < kServiceArgWords; i++) {
-        h = service_mix(h, w[i]);
-        __atomic_store_n(&req->args[i], w[i], __ATOMIC_RELAXED);
-    }
+    for (int i = 0; i < kServiceArgWords; i++) h = service_mix(h, w[i]);
+    // Line 0 (args 0..7) first and fenced, then line 1 (args 8..13, sum, seq):
+    // write-combining may flush a BAR-mapped record's lines in any order, and a
+    // poll that saw seq ahead of its args would fail the hash and cost another
+    // round trip. Host memory keeps x86 store order anyway.
+    for (int i = 0; i < 8; i++) __atomic_store_n(&req->args[i], w[i], __ATOMIC_RELAXED);
+    __builtin_ia32_sfence();
+    for (int i = 8; i < 14; i++) __atomic_store_n(&req->args[i], w[i], __ATOMIC_RELAXED);
     __atomic_store_n(&req->sum, h, __ATOMIC_RELAXED);
     __atomic_store_n(&req->seq, seq, __ATOMIC_RELEASE);
-    __builtin_ia32_sfence();  // drain write-combining buffers (BAR-mapped HBM record)
+    __builtin_ia32_sfence();  // drain write-combining buffers now
 }
 
 void service_store_seq(ServiceReq *req, unsigned long long seq) {
@@ -595,12 +621,13 @@ void service_store_seq(ServiceReq *req, unsigned long long seq) {
 }
 
 hipError_t service_launch(ServiceReq *req, ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
-                          unsigned long long idle_ticks, unsigned blocks, unsigned solo_tiles, hipStream_t stream) {
+                          unsigned long long idle_ticks, unsigned blocks, unsigned solo_tiles, bool hbm_bell,
+                          hipStream_t stream) {
     if (!req || !slot || !box || blocks == 0) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(box, 0, sizeof(ServiceBox), stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(service_kernel, dim3(blocks), dim3(kThreads), 0, stream, req, slot, box, first_seq, idle_ticks,
-                       solo_tiles);
+                       solo_tiles, hbm_bell ? 1u : 0u);
     return hipGetLastError();
 }
 // ---- verification patterns (benchmarks and tests check data without a host round trip) ----

@@ -165,6 +165,7 @@ struct State {
     unsigned svc_solo_tiles = kServiceSoloTilesDefault;  // requests of <= this many tiles stay on workgroup 0
     bool svc_running = false;
     unsigned long long svc_seq = 0;
+    uint64_t svc_ops = 0, svc_ns_post = 0, svc_ns_wait = 0;  // service diagnostics (ocm_x_service_stats)
     uint64_t svc_max = kServiceMaxDefault;
     unsigned long long svc_idle_ticks = 200000ull;  // 2 ms at 100 MHz: live only during bursts of small ops
     // network tier

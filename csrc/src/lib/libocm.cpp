@@ -615,6 +615,18 @@ void ocm_x_counters(uint64_t out[17]) {
     std::memcpy(out, v, sizeof(v));
 }
 
+// Copy-service diagnostics: {ops, ns posting requests, ns waiting for done,
+// GPU ticks (100 MHz) from doorbell seen to done published, doorbell in HBM}.
+void ocm_x_service_stats(uint64_t out[5]) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    out[0] = s.svc_ops;
+    out[1] = s.svc_ns_post;
+    out[2] = s.svc_ns_wait;
+    out[3] = s.svc ? __atomic_load_n(&s.svc->gpu_ticks, __ATOMIC_ACQUIRE) : 0;
+    out[4] = s.svc_req_hbm ? 1 : 0;
+}
+
 // Transfer tuning at runtime (benchmarks): variant 0 auto / 1 reg / 2 lds,
 // blocks 0 = per-path default, nt = nontemporal destination stores.
 void ocm_x_set_tuning(int variant, int blocks, int nt) {

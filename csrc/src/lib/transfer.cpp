@@ -148,15 +148,17 @@ static bool cpu_writable(const void *p, size_t n) {
     return ok;
 }
 
-// The copy service's request record: fine-grained HBM of this GPU written by
-// the CPU through the BAR when the runtime maps it for the CPU (the kernel
-// then polls local memory), else the host-pinned slot. OCM_SERVICE_DOORBELL=host
-// forces the latter.
+// The copy service's request record: the host-pinned slot (default), or with
+// OCM_SERVICE_DOORBELL=hbm fine-grained HBM of this GPU that the CPU writes
+// through the BAR (if the runtime maps it for the CPU). A bare probe
+// (tools/vram_doorbell_probe.hip) round-trips 1.5 us faster with the HBM
+// record, but inside the library the host record measured 0.4-0.7 us faster
+// per 4 KiB op, same core, interleaved runs (profiles/svc_doorbell_r01.json).
 static void service_pick_doorbell(State &s) {
     s.svc_req = &s.svc->req;
     s.svc_req_hbm = false;
     const char *mode = std::getenv("OCM_SERVICE_DOORBELL");
-    if (mode && !std::strcmp(mode, "host")) return;
+    if (!mode || std::strcmp(mode, "hbm") != 0) return;
     void *p = nullptr;
     if (hipExtMallocWithFlags(&p, sizeof(ServiceReq), hipDeviceMallocFinegrained) != hipSuccess || !p) {
         (void)hipGetLastError();
@@ -198,7 +200,8 @@ int service_start(unsigned long long first_seq) {
     }
     __atomic_store_n(&s.svc->exited, 0ull, __ATOMIC_RELEASE);
     service_store_seq(s.svc_req, 0ull);  // clear a STOP left by a parked instance
-    if (service_launch(s.svc_req, s.svc, s.svc_box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_solo_tiles, s.svc_stream) !=
+    if (service_launch(s.svc_req, s.svc, s.svc_box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_solo_tiles, s.svc_req_hbm,
+                       s.svc_stream) !=
         hipSuccess) {
         (void)hipGetLastError();
         s.svc_max = 0;
@@ -245,10 +248,16 @@ int service_xfer(XferArgs x) {
     if (xfer_normalize(x) != hipSuccess) OCM_FAIL(-1, "invalid transfer");
     const unsigned long long seq = ++s.svc_seq;
     if (!s.svc_running && service_start(seq) != 0) return -1;
-    service_post(s.svc_req, x, seq);
     const uint64_t t0 = now_ns();
+    service_post(s.svc_req, x, seq);
+    const uint64_t t_posted = now_ns();
     for (unsigned spins = 1;; spins++) {
-        if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
+        if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) {
+            s.svc_ops++;
+            s.svc_ns_post += t_posted - t0;
+            s.svc_ns_wait += now_ns() - t_posted;
+            return 0;
+        }
         if ((spins & 1023) == 0) {
             // The kernel leaves after idle_ticks without work; if it left before
             // taking this request, start a new one at this seq.

@@ -173,6 +173,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
+            "ocm_x_service_stats": (None, [ctypes.POINTER(u64)]),
             "ocm_x_set_tuning": (None, [i32, i32, i32]),
             "ocm_x_set_tuning_dir": (i32, [i32, i32, i32, i32]),
             "ocm_x_batch": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, ctypes.POINTER(u64), i32, i32]),
@@ -294,6 +295,17 @@ def counters() -> dict:
     out = (ctypes.c_uint64 * len(COUNTER_KEYS))()
     load().ocm_x_counters(out)
     return dict(zip(COUNTER_KEYS, [int(v) for v in out]))
+
+
+def service_stats() -> dict:
+    """Copy-service diagnostics of this process: ops served, mean host time to post a
+    request, mean host wait for its completion, mean GPU time from doorbell seen to
+    completion published (microseconds), and where the doorbell record lives."""
+    out = (ctypes.c_uint64 * 5)()
+    load().ocm_x_service_stats(out)
+    n = int(out[0])
+    return {"ops": n, "post_us": out[1] / n / 1e3 if n else None, "wait_us": out[2] / n / 1e3 if n else None,
+            "gpu_us": out[3] / 100.0 / n if n else None, "doorbell": "hbm" if out[4] else "host"}
 
 
 def layout() -> dict:

@@ -10,6 +10,8 @@ data verified at every size before timing.
 
     python tools/svc_probe.py [--out profiles/svc_probe_r01.json] [--tiers hbm,host] [--configs launch,svc_g32]
 """
+from __future__ import annotations
+
 import argparse
 import json
 import os
@@ -21,20 +23,28 @@ sys.path.insert(0, REPO)
 
 SIZES = [4096 << i for i in range(15)]  # 4 KiB .. 64 MiB
 CONFIGS = {"launch": {"OCM_SERVICE_MAX": "0"}, "launch_event": {"OCM_SERVICE_MAX": "0", "OCM_LAUNCH_FLAG": "0"}}
-# library defaults; and the same with the request record in host memory instead of BAR-mapped HBM
+# library defaults; the same with the request record in BAR-mapped HBM instead of host memory;
+# roctx ranges forced on
 CONFIGS["default"] = {}
-CONFIGS["default_hostbell"] = {"OCM_SERVICE_DOORBELL": "host"}
+CONFIGS["default_hbmbell"] = {"OCM_SERVICE_DOORBELL": "hbm"}
+CONFIGS["default_roctx"] = {"OCM_TRACE": "1"}
+CONFIGS["g1"] = {"OCM_SERVICE_BLOCKS": "1"}
+CONFIGS["g1_hbmbell"] = {"OCM_SERVICE_BLOCKS": "1", "OCM_SERVICE_DOORBELL": "hbm"}
 for g in (1, 16, 32, 64, 128, 256):
     CONFIGS[f"svc_g{g}"] = {"OCM_SERVICE_MAX": str(64 << 20), "OCM_SERVICE_BLOCKS": str(g)}
 
 
-def child(tier: str) -> None:
+def child(tier: str, cpu: int | None = None) -> None:
     from oncilla_amd import api
     from oncilla_amd.parallel.mesh import Mesh
 
     out = {}
     with Mesh(1, gpus=[0]) as m:
         with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+            if cpu is not None:
+                # This (the calling) thread on a fixed core for every configuration:
+                # host <-> GPU latency depends on the core's distance to the GPU.
+                os.sched_setaffinity(0, {cpu})
             sizes = SIZES if tier == "hbm" else SIZES[:13]
             n = sizes[-1] + 8192
             flags = api.OCM_ALLOC_LOOPBACK if tier == "hbm" else api.OCM_ALLOC_HOST_TIER
@@ -53,6 +63,19 @@ def child(tier: str) -> None:
                 put = min(a.time_onesided(1, s, it) for _ in range(3))
                 get = min(a.time_onesided(0, s, it) for _ in range(3))
                 out[str(s)] = {"put_us": round(put * 1e6, 2), "get_us": round(get * 1e6, 2)}
+            # where a 4 KiB blocking put spends its time (library diagnostics, deltas over 2000 ops)
+            b0 = api.service_stats()
+            t = a.time_onesided(1, 4096, 2000)
+            b1 = api.service_stats()
+            if b1["ops"] > b0["ops"]:
+                k = b1["ops"] - b0["ops"]
+
+                def mean(key):
+                    return round((b1[key] * b1["ops"] - (b0[key] or 0) * b0["ops"]) / k, 3)
+
+                out["breakdown_4k_put"] = {"call_us": round(t * 1e6, 3), "post_us": mean("post_us"),
+                                           "wait_us": mean("wait_us"), "gpu_us": mean("gpu_us"),
+                                           "doorbell": b1["doorbell"]}
             a.free()
     print(json.dumps(out))
 
@@ -63,22 +86,29 @@ def main() -> None:
     ap.add_argument("--child", default=None, choices=["hbm", "host"])
     ap.add_argument("--tiers", default="hbm,host")
     ap.add_argument("--configs", default=",".join(CONFIGS))
+    ap.add_argument("--repeat", type=int, default=1, help="run the configuration list this many times, interleaved")
+    ap.add_argument("--pin", action="store_true", help="run every configuration on the same CPU core")
+    ap.add_argument("--cpu", type=int, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.child:
-        child(args.child)
+        child(args.child, args.cpu)
         return
     res = {}
+    cpu = min(os.sched_getaffinity(0)) if args.pin else None
     for tier in args.tiers.split(","):
-        for name in args.configs.split(","):
-            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", tier],
-                               env=dict(os.environ, **CONFIGS[name]), capture_output=True, text=True, timeout=300)
-            key = f"{tier}/{name}"
-            if r.returncode != 0:
-                res[key] = {"error": (r.stdout + r.stderr)[-800:]}
-                print(key, "FAILED", res[key]["error"], file=sys.stderr, flush=True)
-                break
-            res[key] = json.loads(r.stdout.strip().splitlines()[-1])
-            print(key, json.dumps(res[key]), flush=True)
+        for rep in range(args.repeat):
+            for name in args.configs.split(","):
+                cmd = [sys.executable, os.path.abspath(__file__), "--child", tier]
+                if cpu is not None:
+                    cmd += ["--cpu", str(cpu)]
+                r = subprocess.run(cmd, env=dict(os.environ, **CONFIGS[name]), capture_output=True, text=True, timeout=300)
+                key = f"{tier}/{name}" + (f"#{rep}" if args.repeat > 1 else "")
+                if r.returncode != 0:
+                    res[key] = {"error": (r.stdout + r.stderr)[-800:]}
+                    print(key, "FAILED", res[key]["error"], file=sys.stderr, flush=True)
+                    break
+                res[key] = json.loads(r.stdout.strip().splitlines()[-1])
+                print(key, json.dumps(res[key]), flush=True)
     line = json.dumps(res)
     if args.out:
         with open(args.out, "w") as f:

@@ -11,6 +11,7 @@
 // Every spin is bounded: the kernel exits on STOP or after 2 s idle; the host
 // gives up after 1 s per op and then stops the kernel.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 #include <setjmp.h>
 #include <signal.h>
 
@@ -95,6 +96,22 @@ static bool cpu_can_touch(void *p) {
     return ok;
 }
 
+// Host write styles of a 128-byte request record (words 0 = seq and 1 = bytes
+// are what the kernel reads; the rest stands in for the copy arguments).
+__attribute__((target("avx2"))) static void write_avx(Req *r, const unsigned long long *rec) {
+    for (int i = 0; i < 4; i++)
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(r) + i, _mm256_load_si256(reinterpret_cast<const __m256i *>(rec) + i));
+}
+__attribute__((target("avx512f"))) static void write_avx512(Req *r, const unsigned long long *rec) {
+    for (int i = 0; i < 2; i++)
+        _mm512_stream_si512(reinterpret_cast<__m512i *>(r) + i, _mm512_load_si512(reinterpret_cast<const __m512i *>(rec) + i));
+}
+static void write_words(Req *r, const unsigned long long *rec) {
+    unsigned long long *q = reinterpret_cast<unsigned long long *>(r);
+    for (int i = 15; i >= 1; i--) __atomic_store_n(q + i, rec[i], __ATOMIC_RELAXED);
+    __atomic_store_n(q, rec[0], __ATOMIC_RELEASE);
+}
+
 static double pct(std::vector<double> &v, double q) {
     if (v.empty()) return -1.0;
     std::sort(v.begin(), v.end());
@@ -137,8 +154,11 @@ int main() {
             (void)hipFree(r);
             continue;
         }
-        for (int variant = 0; variant <= 3; variant++) {
-            const int sleep_poll = variant == 1, fence = variant >= 2 ? variant - 1 : 0;
+        for (int variant = 0; variant <= 6; variant++) {
+            const int sleep_poll = variant == 1, fence = (variant == 2 || variant == 3) ? variant - 1 : 0;
+            const int style = variant >= 4 ? variant - 3 : 0;  // 1 words, 2 avx, 3 avx512
+            if (style == 2 && !__builtin_cpu_supports("avx2")) continue;
+            if (style == 3 && !__builtin_cpu_supports("avx512f")) continue;
             std::memset((void *)d, 0, sizeof(Done));
             if (m.flags)
                 (void)hipMemset(r, 0, sizeof(Req));
@@ -153,9 +173,19 @@ int main() {
             for (; i <= 20000 && !fails; i++) {
                 const unsigned long long bytes = (i & 1) ? 4096 : 0;
                 auto t0 = std::chrono::steady_clock::now();
-                __atomic_store_n(&r->bytes, bytes, __ATOMIC_RELAXED);
-                __atomic_store_n(&r->seq, i, __ATOMIC_RELEASE);
-                if (m.flags) __builtin_ia32_sfence();  // BAR mappings may be write-combined
+                alignas(64) unsigned long long rec[16] = {i, bytes};
+                for (int k = 2; k < 16; k++) rec[k] = i * 31 + k;
+                if (style == 0) {
+                    __atomic_store_n(&r->bytes, bytes, __ATOMIC_RELAXED);
+                    __atomic_store_n(&r->seq, i, __ATOMIC_RELEASE);
+                } else if (style == 1) {
+                    write_words(r, rec);
+                } else if (style == 2) {
+                    write_avx(r, rec);
+                } else {
+                    write_avx512(r, rec);
+                }
+                _mm_sfence();  // BAR mappings may be write-combined; NT stores need it anyway
                 for (;;) {
                     if (__atomic_load_n(&d->done, __ATOMIC_ACQUIRE) == i) break;
                     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
@@ -172,9 +202,9 @@ int main() {
             (void)hipStreamSynchronize(st);
             fprintf(stderr, "%s sleep%d: stopped\n", m.name, sleep_poll);
             snprintf(buf, sizeof(buf),
-                     "\"%s_sleep%d_fence%d\": {\"p50_4k_us\": %.2f, \"p99_4k_us\": %.2f, \"p50_null_us\": %.2f, "
+                     "\"%s_sleep%d_fence%d_style%d\": {\"p50_4k_us\": %.2f, \"p99_4k_us\": %.2f, \"p50_null_us\": %.2f, "
                      "\"p99_null_us\": %.2f, \"fails\": %d}, ",
-                     m.name, sleep_poll, fence, pct(lat4k, 0.5), pct(lat4k, 0.99), pct(lat0, 0.5), pct(lat0, 0.99), fails);
+                     m.name, sleep_poll, fence, style, pct(lat4k, 0.5), pct(lat4k, 0.99), pct(lat0, 0.5), pct(lat0, 0.99), fails);
             out += buf;
             if (fails) rc = 1;
         }
