@@ -405,3 +405,63 @@ def test_host_tier_prefers_the_gpus_numa_node(mesh_factory):
         slab = [l for l in maps.splitlines() if "ocm_host_slab" in l]
         assert slab and all(f"prefer:{node}" in l for l in slab), slab
         a.free()
+
+
+@pytest.mark.parametrize("doorbell", ["host", "hbm"])
+def test_copy_service_doorbell_placement(mesh_factory, monkeypatch, doorbell):
+    """Small blocking ops with the service's request record in host memory
+    (default) or in BAR-mapped HBM (opt-in): data verified, and the library's
+    service diagnostics count every op and say where the record lives."""
+    if doorbell == "hbm":
+        monkeypatch.setenv("OCM_SERVICE_DOORBELL", "hbm")
+    else:
+        monkeypatch.delenv("OCM_SERVICE_DOORBELL", raising=False)
+    m = mesh_factory(2, gpus=[0, 0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 1 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n)
+        before = api.service_stats()["ops"]
+        for i, (size, off) in enumerate([(4096, 0), (100, 4), (65536 + 12, 4096), (256 << 10, 1 << 16)]):
+            a.fill(seed=40 + i)
+            a.put(off, off, size)
+            a.fill(seed=0)
+            a.get(off, off, size)
+            assert a.check(seed=40 + i, offset=off, nbytes=size - size % 4, first_word=off // 4) == 0, (size, off)
+        st = api.service_stats()
+        assert st["ops"] - before == 8, st
+        assert st["doorbell"] == doorbell, st
+        assert st["gpu_us"] is not None and 0 < st["gpu_us"] < 1000, st
+        a.free()
+
+
+def test_autotune_installs_a_per_direction_choice(mesh_factory):
+    """workloads.autotune on one process (no gather): every candidate runs on
+    the GPU, the winner per direction is installed, and put/get under it keep
+    the data intact (odd sizes and offsets, register and LDS variants)."""
+    from oncilla_amd.models import workloads as wl
+
+    m = mesh_factory(2, gpus=[0, 0], policy="stripe")
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 48 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n)
+        try:
+            r = wl.autotune(a, 32 << 20, reps=1)
+            assert r["get"] in wl.TUNING_CANDIDATES and r["put"] in wl.TUNING_CANDIDATES, r
+            assert all(isinstance(v, float) for row in r["GiBps"].values() for v in row.values()), r
+            for i, (size, off) in enumerate([(40 << 20, 0), ((8 << 20) + 4, 4096), ((33 << 20) - 4, 1 << 20)]):
+                a.fill(seed=70 + i)
+                a.put(off, off, size)
+                a.fill(seed=0)
+                a.get(off, off, size)
+                assert a.check(seed=70 + i, offset=off, nbytes=size - size % 4, first_word=off // 4) == 0, (r, size)
+            # explicit per-direction split: LDS-DMA puts, register gets
+            api.set_tuning_dir(1, 2, 0, True)
+            api.set_tuning_dir(0, 1, 256, False)
+            a.fill(seed=99)
+            a.put(0, 0, 40 << 20)
+            a.fill(seed=0)
+            a.get(0, 0, 40 << 20)
+            assert a.check(seed=99, nbytes=40 << 20) == 0
+        finally:
+            api.set_tuning()
+            a.free()
