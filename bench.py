@@ -193,6 +193,7 @@ def main() -> int:
         lat_remote = wl.alloc_latency(client, remote_kind, args.alloc_samples, local_bytes=64 << 10,
                                       remote_bytes=1 << 20)
         lat_local = wl.alloc_latency(client, api.OCM_LOCAL_HOST, args.alloc_samples, local_bytes=1 << 20)
+        leases, _ = _local(lambda: client.stats()["lease_allocs"])
         if dist is not None:
             dist.barrier()
 
@@ -241,7 +242,7 @@ def main() -> int:
 
         # max over ranks of elapsed, sum of bytes
         stats = gather_obj(dist, {"elapsed": elapsed, "moved": moved, "lat": lat_remote, "lat_local": lat_local,
-                                  "extents": info["extents"]}, world)
+                                  "extents": info["extents"], "leases": leases}, world)
         t_max = max(s["elapsed"] for s in stats)
         total = sum(s["moved"] for s in stats)
 
@@ -296,6 +297,8 @@ def main() -> int:
             "alloc_p99_us": round(max(s["lat"]["alloc_p99_us"] for s in stats), 2),
             "free_p50_us": round(max(s["lat"]["free_p50_us"] for s in stats), 2),
             "local_alloc_p50_us": round(max(s["lat_local"]["alloc_p50_us"] for s in stats), 2),
+            "alloc_p50_us_per_rank": [round(s["lat"]["alloc_p50_us"], 2) for s in stats],
+            "lease_allocs_per_rank": [s["leases"] for s in stats],
             "sweep": sweep,
         }
         if tuned:

@@ -23,17 +23,23 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpu", action="store_true")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--meshes", default="1,2", help="daemon counts to run")
+    ap.add_argument("--policy", default=None, help="placement policy (default: the mesh default)")
+    ap.add_argument("--modes", default="poll,block")
     args = ap.parse_args()
     res = {}
-    for name, env in {"poll": {}, "block": {"OCM_RPC_SPIN_US": "0", "OCM_DAEMON_SPIN_US": "0"}}.items():
+    modes = {"poll": {}, "block": {"OCM_RPC_SPIN_US": "0", "OCM_DAEMON_SPIN_US": "0"}}
+    for name in args.modes.split(","):
+        env = modes[name]
         for k in ("OCM_RPC_SPIN_US", "OCM_DAEMON_SPIN_US"):
             os.environ.pop(k, None)
         os.environ.update(env)
         if not args.gpu:
             os.environ["OCM_NO_GPU"] = "1"
-        for n in (1, 2):
+        for n in [int(x) for x in args.meshes.split(",")]:
             gpus = [0] * n if args.gpu else None
-            with Mesh(n, gpus=gpus) as m:
+            kw = {"policy": args.policy} if args.policy else {}
+            with Mesh(n, gpus=gpus, **kw) as m:
                 cenv = m.client_env(0)
                 if args.gpu:
                     cenv["OCM_GPU"] = "0"
