@@ -204,9 +204,10 @@ def main() -> int:
         info = pair.remote_info()
 
         # ---- setup (untimed): pick the put/get kernel configuration over the
-        # xGMI links, every rank at once (all-to-all load), slowest rank decides ----
+        # xGMI links, every rank at once (all-to-all load), slowest rank decides.
+        # CPU runs (memcpy data path) do it too, so the multi-rank protocol is tested ----
         tuned = None
-        if use_gpu and world > 1 and not args.no_autotune:
+        if world > 1 and not args.no_autotune:
             tuned = wl.autotune(pair, min(256 << 20, max_bytes), reps=3,
                                 gather=lambda obj: gather_obj(dist, obj, world))
 

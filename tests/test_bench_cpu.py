@@ -38,6 +38,9 @@ def test_bench_multi_rank(native, n):
     res = _last_json(r.stdout)
     assert res["n_gpus"] == n and res["value"] > 0 and res["config"]["parallelism"] == f"stripe{n}"
     assert res["config"]["extents_per_pair"] == n - 1  # 8 MiB+1 pair = 9 stripe units: every peer gets one
+    # the setup-time autotune ran its all-rank protocol and agreed on one pick per direction
+    assert res["autotune"]["ranks"] == n and res["autotune"]["get"] in res["autotune"]["GiBps"], res["autotune"]
+    assert len(res["alloc_p50_us_per_rank"]) == n
 
 
 def test_bench_extras_helpers_run(native):
