@@ -1,3 +1,7 @@
+// TCP helpers for the mesh links and the network-tier data server.
+// Reference parity: conn_connect / localbind / accept / put / get of
+// src/sock.c:18-261 (inc/sock.h:30-47), with connect timeouts and non-blocking
+// record framing added.
 #include "ocm/sock.h"
 
 #include <arpa/inet.h>

@@ -1,4 +1,7 @@
 // ocmd app protocol: CONNECT/DISCONNECT (crash reclaim), REQ_ALLOC, REQ_FREE, STATS.
+// Reference parity: the app registry and process_msg dispatch of src/main.c:46-104
+// and mem_new_request src/mem.c:514-530; crash reclaim was a TODO there
+// (src/main.c:6-7, README:68-69).
 #include "ocm/daemon.h"
 
 #include <fcntl.h>

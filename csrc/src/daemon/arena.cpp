@@ -1,3 +1,8 @@
+// ocmd memory arenas: 4 GiB HBM slabs (hipMalloc, IPC-exported once) and
+// memfd host-tier slabs, sub-allocated with coalescing ranges.
+// Reference parity: the server side of alloc_ate / dealloc_ate
+// src/alloc.c:150-282 (malloc + ibv_reg_mr / rma2_register of every buffer
+// there, src/rdma_server.c:40-236), including the leak it fixes (src/alloc.c:171).
 #include "ocm/arena.h"
 
 #include <hip/hip_runtime_api.h>

@@ -2,6 +2,9 @@
 // the epoll event loop, event sources and message routing. Protocol handlers
 // live in apps.cpp (app <-> daemon), mesh.cpp (daemon <-> daemon), lease.cpp
 // (capacity leases) and resume.cpp (rank0 checkpoint / rejoin).
+// Reference parity: daemon main and mailbox poller src/main.c:106-224 (a
+// 500 us usleep poll there, src/main.c:112-126; epoll here), daemon core
+// src/mem.c:485-535 (mem_init / mem_new_request / mem_fin, inc/mem.h:29-33).
 #include "ocm/daemon.h"
 
 #include <fcntl.h>

@@ -1,6 +1,11 @@
 // ocmd mesh protocol: rank0 placement (ADD_NODE, REQ_ALLOC, PLACE_FAIL),
 // owner DO_ALLOC/DO_FREE, origin completion, peer loss, timeouts and the
 // tick control transport.
+// Reference parity: the inter-daemon protocol of src/mem.c:53-535 (a TCP
+// connection and a thread per RPC there; persistent links and one event loop
+// here), alloc_find placement src/alloc.c:76-140 (Governor::place),
+// alloc_ate / dealloc_ate src/alloc.c:150-282 (owner_do_alloc / owner_do_free),
+// message states inc/msg.h:24-45.
 #include "ocm/daemon.h"
 
 #include <fcntl.h>

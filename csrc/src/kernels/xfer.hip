@@ -12,6 +12,10 @@
 // the tile size (a power of two <= stripe unit), so a tile never crosses a
 // stripe unit and maps to one contiguous range on both sides. Workgroups
 // grid-stride over tiles; per-tile extent/offset math runs once per workgroup.
+// Reference parity: the one-sided data movers they replace are ib_read /
+// ib_write (one signaled RDMA READ/WRITE work request, post_send src/rdma.c:47-92)
+// and extoll_read / extoll_write (8 MiB chunks, 2 outstanding, extoll_rma2_transfer
+// src/extoll.c:40-167).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>

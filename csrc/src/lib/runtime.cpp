@@ -1,6 +1,8 @@
 // libocm process state, mailbox RPC to the local ocmd, the import cache of
 // remote extents (hipIpcOpenMemHandle / memfd + hipHostRegister), and the
 // local halves of allocations (stream-ordered pool, pinned host, malloc).
+// Reference parity: ocm_init / ocm_tini src/lib.c:97-165, the local half of
+// ocm_alloc src/lib.c:174-344 (malloc / cudaMalloc / ib_new+ib_connect there).
 #include "internal.h"
 
 namespace ocmlib {

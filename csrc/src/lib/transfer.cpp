@@ -1,6 +1,11 @@
 // libocm copy engine: striped segments, per-allocation lanes and events, the
 // resident copy service, one-sided transfers (gfx950 kernels / DMA / CPU)
 // and process-local copies.
+// Reference parity: ocm_copy src/lib.c:501-665 and ocm_copy_onesided
+// src/lib.c:669-723, whose RDMA/RMA legs (ib_read/ib_write over post_send,
+// src/rdma.c:47-92,241-302; extoll_read/extoll_write over extoll_rma2_transfer,
+// src/extoll.c:40-167,286-310, 8 MiB x 2 outstanding) become
+// gfx950 kernel launches or the resident copy service here.
 #include "internal.h"
 
 namespace ocmlib {

@@ -1,4 +1,8 @@
 // Raw xGMI backend (see ocm/xgmi.h). Exported from libocm.so.
+// Reference parity: the ib_* API of inc/io/rdma.h:36-45 (src/rdma.c:46-302,
+// src/rdma_server.c:40-236, src/rdma_client.c:39-252) and the extoll_* API of
+// inc/io/extoll.h:50-59 (src/extoll*.c): new / connect / read / write /
+// disconnect over IPC-mapped peer HBM instead of verbs QPs or RMA2 ports.
 #include "ocm/xgmi.h"
 
 #include <fcntl.h>
