@@ -110,6 +110,22 @@ def test_bench_gpu_small():
     assert res["config"]["device"] == "gpu" and res["value"] > 0
 
 
+def test_bench_two_ranks_sharing_one_gpu():
+    """The driver's N>1 launch shape (torch.distributed.run, one ocmd per rank,
+    striped remote halves, setup-time autotune, the all-rank gathers) on one
+    GPU: both ranks and both daemons share GPU 0 (OCM_BENCH_SHARE_GPU)."""
+    env = dict(os.environ, OCM_BENCH_SHARE_GPU="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29641", os.path.join(REPO, "bench.py"),
+                        "--gpus", "2", "--steps", "1", "--warmup", "1", "--max-bytes", str(32 << 20),
+                        "--alloc-samples", "50", "--no-characterize", "--no-hw-baseline"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["n_gpus"] == 2 and res["value"] > 0 and res["config"]["remote_tier"] == "hbm", res
+    assert res["autotune"]["ranks"] == 2 and res["autotune"]["put"] in res["autotune"]["GiBps"], res["autotune"]
+
+
 @pytest.mark.parametrize("policy", ["ring", "stripe"])
 def test_copy_service_small_ops(mesh_factory, policy):
     """Small blocking put/get run on the resident copy service; interleave them
