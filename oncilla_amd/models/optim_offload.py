@@ -1,0 +1,162 @@
+"""Adam with its moments in disaggregated memory (a training workload).
+
+Adam keeps two fp32 moments per parameter: 8 bytes per parameter on top of the
+weights, which is what runs a large model out of HBM first. Here the moments live
+in the *remote half* of oncilla allocations: HBM striped over the node's other
+MI355X (xGMI), the pinned host tier (PCIe), or another node. The GPU holds only
+two staging slots of `chunk_elems` moments each.
+
+A step walks the flat parameter space in chunks. Chunk k uses slot k % 2, and
+each slot is its own allocation, so it has its own copy lane and event:
+
+    slot X = allocs[k % 2]
+    torch stream waits for X's lane (the get of chunk k)       X.stream_signal()
+    Adam update of chunk k on the torch stream (views of X)
+    X's lane waits for that update                              X.stream_wait()
+    put chunk k back; get chunk k + 2 into the same slot        async, in order on X's lane
+
+So the get of chunk k + 1 (slot k + 1 % 2, other lane) overlaps the update of chunk
+k, and the write-back of chunk k overlaps the update of chunk k + 1. Nothing waits
+on the host inside a step.
+
+The update is torch.optim.Adam's (L2 weight decay, bias correction; reference
+behaviour: torch/optim/adam.py single-tensor path), so results match it to
+float32 rounding (tests/test_optim_offload.py). The reference runtime has no
+training workloads; this is a use of the API beyond it.
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable
+
+from .. import api
+
+
+class OffloadedAdam:
+    def __init__(self, params: Iterable, client: api.Client, lr: float = 1e-3, betas=(0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 0.0, chunk_elems: int = 16 << 20, flags: int = 0):
+        import torch
+
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("no parameters to optimize")
+        for p in self.params:
+            if p.dtype != torch.float32 or not p.is_contiguous():
+                raise ValueError("OffloadedAdam takes contiguous float32 parameters")
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.t = 0
+        self.total = sum(p.numel() for p in self.params)
+        self.C = max(1, min(int(chunk_elems), self.total))
+        self.nchunks = (self.total + self.C - 1) // self.C
+        self.slot_bytes = 8 * self.C  # [m (C floats) | v (C floats)]
+        on_gpu = client.device >= 0
+        kind = api.OCM_REMOTE_GPU if on_gpu else api.OCM_REMOTE_RDMA
+        self.allocs = []
+        for parity in range(min(2, self.nchunks)):
+            n_mine = (self.nchunks - parity + 1) // 2
+            self.allocs.append(client.alloc(kind, local_bytes=self.slot_bytes, remote_bytes=n_mine * self.slot_bytes,
+                                            flags=flags))
+        self.slots = [a.local_tensor(torch.float32) for a in self.allocs]
+        # chunk k -> [(param, lo, hi, offset in chunk)]
+        self.segments = []
+        bounds, start = [], 0
+        for p in self.params:
+            bounds.append((p, start, start + p.numel()))
+            start += p.numel()
+        for k in range(self.nchunks):
+            c0, c1 = k * self.C, min((k + 1) * self.C, self.total)
+            segs = [(p, max(c0, b0) - b0, min(c1, b1) - b0, max(c0, b0) - c0) for p, b0, b1 in bounds
+                    if b0 < c1 and b1 > c0]
+            self.segments.append(segs)
+        # zero moments in the remote halves
+        for s in self.slots:
+            s.zero_()
+        if on_gpu:
+            torch.cuda.synchronize(client.device)
+        for k in range(self.nchunks):
+            self.allocs[k % 2].put(0, (k // 2) * self.slot_bytes, self.chunk_bytes(k))
+
+    def chunk_bytes(self, k: int) -> int:
+        """Bytes of chunk k's record: its m half in full, then v up to the chunk's length."""
+        n = min(self.C, self.total - k * self.C)
+        return 4 * self.C + 4 * n
+
+    def _get(self, k: int) -> None:
+        self.allocs[k % 2].get(0, (k // 2) * self.slot_bytes, self.chunk_bytes(k), async_=True)
+
+    def _put(self, k: int) -> None:
+        self.allocs[k % 2].put(0, (k // 2) * self.slot_bytes, self.chunk_bytes(k), async_=True)
+
+    def _update(self, k: int) -> None:
+        b1, b2 = self.betas
+        bc1 = 1 - b1 ** self.t
+        bc2 = 1 - b2 ** self.t
+        step_size = self.lr / bc1
+        slot = self.slots[k % 2]
+        for p, lo, hi, off in self.segments[k]:
+            if p.grad is None:
+                continue
+            n = hi - lo
+            pv = p.data.view(-1)[lo:hi]
+            g = p.grad.view(-1)[lo:hi]
+            if self.weight_decay:
+                g = g.add(pv, alpha=self.weight_decay)
+            m = slot[off:off + n]
+            v = slot[self.C + off:self.C + off + n]
+            m.mul_(b1).add_(g, alpha=1 - b1)
+            v.mul_(b2).addcmul_(g, g, value=1 - b2)
+            denom = (v.sqrt() / math.sqrt(bc2)).add_(self.eps)
+            pv.addcdiv_(m, denom, value=-step_size)
+
+    def step(self) -> None:
+        """One Adam step over every parameter; queued on torch's current stream (GPU) without a host wait."""
+        self.t += 1
+        # Prefetch chunks 0 and 1. Each slot's lane already orders these gets after
+        # the previous step's write-back of that slot, which waited for its update;
+        # nothing here waits for backward, so the prefetch can overlap it.
+        for k in range(min(2, self.nchunks)):
+            self._get(k)
+        for k in range(self.nchunks):
+            x = self.allocs[k % 2]
+            x.stream_signal()   # torch waits for chunk k's moments
+            self._update(k)
+            x.stream_wait()     # the write-back waits for the update
+            self._put(k)
+            if k + 2 < self.nchunks:
+                self._get(k + 2)
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        for p in self.params:
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()
+
+    def synchronize(self) -> None:
+        """Wait on the host for every queued write-back."""
+        for a in self.allocs:
+            a.wait()
+
+    def moments(self, param_index: int):
+        """(exp_avg, exp_avg_sq) of one parameter, gathered from remote memory (tests, checkpoints)."""
+        import torch
+
+        self.synchronize()
+        p = self.params[param_index]
+        start = sum(q.numel() for q in self.params[:param_index])
+        m = torch.empty(p.numel(), dtype=torch.float32)
+        v = torch.empty(p.numel(), dtype=torch.float32)
+        for k in range(start // self.C, (start + p.numel() - 1) // self.C + 1):
+            self.allocs[k % 2].get(0, (k // 2) * self.slot_bytes, self.chunk_bytes(k))
+            slot = self.slots[k % 2].cpu()
+            for q, lo, hi, off in self.segments[k]:
+                if q is p:
+                    m[lo:hi] = slot[off:off + hi - lo]
+                    v[lo:hi] = slot[self.C + off:self.C + off + hi - lo]
+        return m.view_as(p), v.view_as(p)
+
+    def close(self) -> None:
+        self.synchronize()
+        for a in self.allocs:
+            a.free()
+        self.allocs = []
