@@ -1,0 +1,32 @@
+// Fused optimizer kernels that update parameters in place while their state
+// lives in a remote (striped) oncilla allocation: the kernel reads and writes
+// the state straight from peer HBM over xGMI (or the pinned host tier), with
+// no staging copy. See csrc/src/kernels/optim.hip.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+#include "ocm/xfer.h"
+
+namespace ocm {
+
+struct AdamArgs {
+    float *p;                        // parameters (this GPU), n elements, 16-byte aligned
+    const float *g;                  // gradients (this GPU), n elements, 16-byte aligned
+    char *ext[kXferMaxExtents];      // extent bases of the striped state space
+    uint32_t n_ext;
+    uint32_t unit_shift;             // log2(stripe unit) when n_ext > 1
+    uint64_t m_off, v_off;           // byte offsets of element 0's exp_avg / exp_avg_sq (16-byte aligned)
+    uint64_t n;                      // elements
+    float b1, b2, eps, wd;           // betas, eps, L2 weight decay
+    float step_size;                 // lr / (1 - b1^t)
+    float inv_sqrt_bc2;              // 1 / sqrt(1 - b2^t)
+};
+
+// torch.optim.Adam's update (L2 weight decay, bias correction), one pass:
+// reads p, g (local) and m, v (remote), writes p (local) and m, v (remote).
+hipError_t adam_remote_launch(const AdamArgs &a, hipStream_t stream);
+
+}  // namespace ocm

@@ -1,0 +1,112 @@
+// gfx950 fused Adam over remote optimizer state (see ocm/optim.h).
+//
+// Each lane owns 4 consecutive elements: 16-byte loads of p and g from local
+// HBM and of exp_avg / exp_avg_sq from the state's extents (peer HBM over
+// xGMI, or pinned host memory over PCIe), the update in registers, 16-byte
+// stores back. A 16-byte vector never crosses a stripe unit (units are powers
+// of two >= 16 and the offsets are 16-byte aligned), so the extent math runs
+// once per vector. Lanes keep kVec vectors in flight before the first use,
+// which covers the xGMI round trip. The tail (n % 4) is done by lane 0 of
+// the last workgroup, element by element.
+#include <hip/hip_runtime.h>
+
+#include "ocm/optim.h"
+
+namespace ocm {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kVec = 4;  // vectors per lane per iteration
+
+__device__ __forceinline__ char *state_ptr(const AdamArgs &a, uint64_t x) {
+    if (a.n_ext == 1) return a.ext[0] + x;
+    const uint64_t u = x >> a.unit_shift;
+    const uint64_t mask = (1ull << a.unit_shift) - 1;
+    return a.ext[u % a.n_ext] + (((u / a.n_ext) << a.unit_shift) | (x & mask));
+}
+
+__device__ __forceinline__ float adam1(float &p, float g, float &m, float &v, const AdamArgs &a) {
+    g = a.wd != 0.f ? g + a.wd * p : g;
+    m = m + (1.f - a.b1) * (g - m);  // torch: exp_avg.lerp_(grad, 1 - beta1)
+    v = a.b2 * v + (1.f - a.b2) * g * g;
+    const float denom = sqrtf(v) * a.inv_sqrt_bc2 + a.eps;
+    p = p - a.step_size * (m / denom);
+    return p;
+}
+
+__global__ __launch_bounds__(kThreads) void adam_remote_kernel(AdamArgs a) {
+    const uint64_t nvec = a.n >> 2;
+    const uint64_t lanes = (uint64_t)gridDim.x * kThreads;
+    const uint64_t tid = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    f32x4 *p4 = reinterpret_cast<f32x4 *>(a.p);
+    const f32x4 *g4 = reinterpret_cast<const f32x4 *>(a.g);
+    for (uint64_t base = tid; base < nvec; base += lanes * kVec) {
+        f32x4 p[kVec], g[kVec], m[kVec], v[kVec];
+        f32x4 *mp[kVec], *vp[kVec];
+#pragma unroll
+        for (int k = 0; k < kVec; k++) {
+            const uint64_t i = base + (uint64_t)k * lanes;
+            if (i < nvec) {
+                mp[k] = reinterpret_cast<f32x4 *>(state_ptr(a, a.m_off + (i << 4)));
+                vp[k] = reinterpret_cast<f32x4 *>(state_ptr(a, a.v_off + (i << 4)));
+                m[k] = __builtin_nontemporal_load(mp[k]);
+                v[k] = __builtin_nontemporal_load(vp[k]);
+                p[k] = p4[i];
+                g[k] = __builtin_nontemporal_load(g4 + i);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kVec; k++) {
+            const uint64_t i = base + (uint64_t)k * lanes;
+            if (i < nvec) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    float pj = p[k][j], mj = m[k][j], vj = v[k][j];
+                    adam1(pj, g[k][j], mj, vj, a);
+                    p[k][j] = pj;
+                    m[k][j] = mj;
+                    v[k][j] = vj;
+                }
+                p4[i] = p[k];
+                __builtin_nontemporal_store(m[k], mp[k]);
+                __builtin_nontemporal_store(v[k], vp[k]);
+            }
+        }
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        for (uint64_t i = nvec << 2; i < a.n; i++) {
+            float *mq = reinterpret_cast<float *>(state_ptr(a, a.m_off + 4 * i));
+            float *vq = reinterpret_cast<float *>(state_ptr(a, a.v_off + 4 * i));
+            float pj = a.p[i], mj = *mq, vj = *vq;
+            adam1(pj, a.g[i], mj, vj, a);
+            a.p[i] = pj;
+            *mq = mj;
+            *vq = vj;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t adam_remote_launch(const AdamArgs &a, hipStream_t stream) {
+    if (a.n == 0) return hipSuccess;
+    if (a.n_ext < 1 || a.n_ext > (uint32_t)kXferMaxExtents) return hipErrorInvalidValue;
+    if (a.n_ext > 1 && a.unit_shift < 4) return hipErrorInvalidValue;
+    if (((uintptr_t)a.p | (uintptr_t)a.g | a.m_off | a.v_off) & 15u) return hipErrorInvalidValue;
+    const uint64_t nvec = a.n >> 2;
+    uint64_t want = (nvec + (uint64_t)kThreads * kVec - 1) / ((uint64_t)kThreads * kVec);
+    if (want < 1) want = 1;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    const uint64_t cap = (uint64_t)cus * 4;
+    const unsigned grid = (unsigned)(want < cap ? want : cap);
+    hipLaunchKernelGGL(adam_remote_kernel, dim3(grid), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace ocm

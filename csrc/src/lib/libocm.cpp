@@ -14,6 +14,7 @@
 // (src/lib.c:461), NULL deref before check in ocm_free (:357-359), stub
 // copy_in/out (:491-499), swapped GPU->RMA offsets (:654).
 #include "internal.h"
+#include "ocm/optim.h"
 
 using namespace ocm;
 using namespace ocmlib;
@@ -613,6 +614,50 @@ void ocm_x_counters(uint64_t out[17]) {
                             c.n_copy, c.bytes_copy, c.ns_put,  c.ns_get,      c.ns_alloc,    c.ns_free,
                             c.n_batch, c.n_batch_ops, c.bytes_batch, c.ns_batch, c.n_batch_launches};
     std::memcpy(out, v, sizeof(v));
+}
+
+// Fused Adam over optimizer state kept in the remote half of `a` (see
+// ocm/optim.h): p/g are this GPU's parameters and gradients (n floats),
+// exp_avg / exp_avg_sq of element 0 sit at byte offsets m_off / v_off of the
+// remote half. hp = {b1, b2, eps, weight_decay, step_size, 1/sqrt(bias_correction2)}.
+// Queued on `stream` (e.g. torch's current stream); no host wait.
+int ocm_x_adam(ocm_alloc_t a, float *p, const float *g, uint64_t n, uint64_t m_off, uint64_t v_off,
+               const float hp[6], void *stream) {
+    State &s = S();
+    if (!a || !p || !g || !hp) OCM_FAIL(-1, "ocm_x_adam: null argument");
+    if (s.device < 0) OCM_FAIL(-1, "ocm_x_adam needs a GPU");
+    if (!is_pair(a->kind) || a->ext.empty() || !a->all_dev_ok)
+        OCM_FAIL(-1, "ocm_x_adam needs a remote half this GPU can address (HBM or host tier, not another node)");
+    if (n > (UINT64_MAX >> 3) || m_off > a->remote_bytes || 4 * n > a->remote_bytes - m_off ||
+        v_off > a->remote_bytes || 4 * n > a->remote_bytes - v_off)
+        OCM_FAIL(-1, "ocm_x_adam: state range exceeds the remote half (%zu bytes)", a->remote_bytes);
+    if (a->ext.size() > (size_t)kXferMaxExtents) OCM_FAIL(-1, "ocm_x_adam: too many extents");
+    AdamArgs x;
+    std::memset(&x, 0, sizeof(x));
+    x.p = p;
+    x.g = g;
+    for (size_t i = 0; i < a->ext.size(); i++) x.ext[i] = a->ext[i].dptr;
+    x.n_ext = (uint32_t)a->ext.size();
+    if (x.n_ext > 1) {
+        const int sh = log2_exact(a->stripe_unit);
+        if (sh < 4) OCM_FAIL(-1, "ocm_x_adam: stripe unit %llu unusable", (unsigned long long)a->stripe_unit);
+        x.unit_shift = (uint32_t)sh;
+    }
+    x.m_off = m_off;
+    x.v_off = v_off;
+    x.n = n;
+    x.b1 = hp[0];
+    x.b2 = hp[1];
+    x.eps = hp[2];
+    x.wd = hp[3];
+    x.step_size = hp[4];
+    x.inv_sqrt_bc2 = hp[5];
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (wait_alloc(a) != 0) return -1;  // queued async ops on this allocation come first
+    DeviceGuard dg(s.device);
+    const hipError_t e = adam_remote_launch(x, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) OCM_FAIL(-1, "ocm_x_adam launch: %s", hipGetErrorString(e));
+    return 0;
 }
 
 // Copy-service diagnostics: {ops, ns posting requests, ns waiting for done,

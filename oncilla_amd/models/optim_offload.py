@@ -19,6 +19,13 @@ So the get of chunk k + 1 (slot k + 1 % 2, other lane) overlaps the update of ch
 k, and the write-back of chunk k overlaps the update of chunk k + 1. Nothing waits
 on the host inside a step.
 
+mode="fused" (default on a GPU) skips the staging altogether: one gfx950 kernel
+per parameter (ocm_x_adam, csrc/src/kernels/optim.hip) reads p and g from local
+HBM and exp_avg / exp_avg_sq straight from the remote half (peer HBM over xGMI or
+the pinned host tier), updates in registers and writes everything back: one pass,
+no copies, no extra local HBM traffic. mode="staged" is the path above (CPU
+processes, and state on another node, which a kernel cannot address).
+
 The update is torch.optim.Adam's (L2 weight decay, bias correction; reference
 behaviour: torch/optim/adam.py single-tensor path), so results match it to
 float32 rounding (tests/test_optim_offload.py). The reference runtime has no
@@ -34,7 +41,8 @@ from .. import api
 
 class OffloadedAdam:
     def __init__(self, params: Iterable, client: api.Client, lr: float = 1e-3, betas=(0.9, 0.999),
-                 eps: float = 1e-8, weight_decay: float = 0.0, chunk_elems: int = 16 << 20, flags: int = 0):
+                 eps: float = 1e-8, weight_decay: float = 0.0, chunk_elems: int = 16 << 20, flags: int = 0,
+                 mode: str = "auto", stripe_unit: int = 0):
         import torch
 
         self.params = [p for p in params if p.requires_grad]
@@ -51,11 +59,19 @@ class OffloadedAdam:
         self.slot_bytes = 8 * self.C  # [m (C floats) | v (C floats)]
         on_gpu = client.device >= 0
         kind = api.OCM_REMOTE_GPU if on_gpu else api.OCM_REMOTE_RDMA
+        self.mode = ("fused" if on_gpu else "staged") if mode == "auto" else mode
+        if self.mode not in ("fused", "staged"):
+            raise ValueError(f"mode {mode!r}")
+        if self.mode == "fused":
+            if not on_gpu:
+                raise ValueError("mode='fused' needs a GPU client")
+            self._init_fused(client, kind, flags, stripe_unit)
+            return
         self.allocs = []
         for parity in range(min(2, self.nchunks)):
             n_mine = (self.nchunks - parity + 1) // 2
             self.allocs.append(client.alloc(kind, local_bytes=self.slot_bytes, remote_bytes=n_mine * self.slot_bytes,
-                                            flags=flags))
+                                            flags=flags, stripe_unit=stripe_unit))
         self.slots = [a.local_tensor(torch.float32) for a in self.allocs]
         # chunk k -> [(param, lo, hi, offset in chunk)]
         self.segments = []
@@ -75,6 +91,37 @@ class OffloadedAdam:
             torch.cuda.synchronize(client.device)
         for k in range(self.nchunks):
             self.allocs[k % 2].put(0, (k // 2) * self.slot_bytes, self.chunk_bytes(k))
+
+    # ---- fused mode: state addressed in place by the update kernel ----
+    _PAD = 64  # elements: every parameter's state starts 256-byte aligned
+
+    def _init_fused(self, client, kind, flags, stripe_unit) -> None:
+        import torch
+
+        self.starts, pos = [], 0
+        for p in self.params:
+            self.starts.append(pos)
+            pos += (p.numel() + self._PAD - 1) // self._PAD * self._PAD
+        self.padded = pos
+        remote = 8 * self.padded  # [exp_avg (padded) | exp_avg_sq (padded)]
+        self.stage = min(remote, 64 << 20)
+        self.allocs = [client.alloc(kind, local_bytes=self.stage, remote_bytes=remote, flags=flags,
+                                    stripe_unit=stripe_unit)]
+        a = self.allocs[0]
+        a.local_tensor(torch.uint8).zero_()
+        torch.cuda.synchronize(client.device)
+        for off in range(0, remote, self.stage):
+            a.put(0, off, min(self.stage, remote - off))
+
+    def _step_fused(self) -> None:
+        b1, b2 = self.betas
+        hp = (b1, b2, self.eps, self.weight_decay, self.lr / (1 - b1 ** self.t), 1 / math.sqrt(1 - b2 ** self.t))
+        a = self.allocs[0]
+        for p, start in zip(self.params, self.starts):
+            if p.grad is None:
+                continue
+            g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+            a.adam(p.data, g, 4 * start, 4 * (self.padded + start), hp)
 
     def chunk_bytes(self, k: int) -> int:
         """Bytes of chunk k's record: its m half in full, then v up to the chunk's length."""
@@ -111,6 +158,9 @@ class OffloadedAdam:
     def step(self) -> None:
         """One Adam step over every parameter; queued on torch's current stream (GPU) without a host wait."""
         self.t += 1
+        if self.mode == "fused":
+            self._step_fused()
+            return
         # Prefetch chunks 0 and 1. Each slot's lane already orders these gets after
         # the previous step's write-back of that slot, which waited for its update;
         # nothing here waits for backward, so the prefetch can overlap it.
@@ -133,7 +183,11 @@ class OffloadedAdam:
                 p.grad.zero_()
 
     def synchronize(self) -> None:
-        """Wait on the host for every queued write-back."""
+        """Wait on the host for every queued write-back (fused mode: for the update kernels)."""
+        if self.mode == "fused":
+            import torch
+
+            torch.cuda.synchronize(self.params[0].device)
         for a in self.allocs:
             a.wait()
 
@@ -143,6 +197,18 @@ class OffloadedAdam:
 
         self.synchronize()
         p = self.params[param_index]
+        if self.mode == "fused":
+            torch.cuda.synchronize(p.device)  # the update kernels ran on torch's stream
+            a, n = self.allocs[0], p.numel()
+            out = []
+            for base in (4 * self.starts[param_index], 4 * (self.padded + self.starts[param_index])):
+                t = torch.empty(n, dtype=torch.float32)
+                for e0 in range(0, n, self.stage // 4):
+                    e1 = min(n, e0 + self.stage // 4)
+                    a.get(0, base + 4 * e0, 4 * (e1 - e0))
+                    t[e0:e1] = a.local_tensor(torch.float32)[:e1 - e0].cpu()
+                out.append(t.view_as(p))
+            return out[0], out[1]
         start = sum(q.numel() for q in self.params[:param_index])
         m = torch.empty(p.numel(), dtype=torch.float32)
         v = torch.empty(p.numel(), dtype=torch.float32)

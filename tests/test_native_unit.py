@@ -2,6 +2,8 @@
 geometry, host-tier arena) and the ABI layout seen from Python."""
 import ctypes
 
+import pytest
+
 from oncilla_amd import api
 
 
@@ -23,7 +25,8 @@ def test_abi_layout(native):
             api.OCM_LOCAL_GPU, api.OCM_REMOTE_GPU) == tuple(range(1, 8))
 
 
-def test_kernels_use_no_scratch():
+@pytest.mark.parametrize("src,min_kernels", [("xfer.hip", 9), ("optim.hip", 1)])
+def test_kernels_use_no_scratch(src, min_kernels):
     # Resource check of every gfx950 kernel: a dynamically indexed local array
     # (e.g. a copied extent table) lands in scratch and costs a memory round
     # trip per access on the hot path. The compiler reports it per kernel.
@@ -33,12 +36,12 @@ def test_kernels_use_no_scratch():
 
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                        f"-I{repo}/csrc/include", "-c", f"{repo}/csrc/src/kernels/xfer.hip", "-o", os.devnull,
+                        f"-I{repo}/csrc/include", "-c", f"{repo}/csrc/src/kernels/{src}", "-o", os.devnull,
                         "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     names = re.findall(r"Function Name: (\S+)", r.stderr)
     scratch = [int(v) for v in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", r.stderr)]
     spills = [int(v) for v in re.findall(r"VGPRs Spill: (\d+)", r.stderr)]
-    assert len(names) >= 9 and len(scratch) == len(names)
+    assert len(names) >= min_kernels and len(scratch) == len(names)
     assert all(s == 0 for s in scratch), dict(zip(names, scratch))
     assert all(s == 0 for s in spills), dict(zip(names, spills))
