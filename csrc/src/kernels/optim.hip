@@ -5,10 +5,12 @@
 // xGMI, or pinned host memory over PCIe), the update in registers, 16-byte
 // stores back. A 16-byte vector never crosses a stripe unit (units are powers
 // of two >= 16 and the offsets are 16-byte aligned), so the extent math runs
-// once per vector. Lanes keep kVec vectors in flight before the first use,
+// once per vector. Lanes keep kVec (4) vectors in flight before the first use,
 // which covers the xGMI round trip. The tail (n % 4) is done by lane 0 of
 // the last workgroup, element by element.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "ocm/optim.h"
 
@@ -19,7 +21,6 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
-constexpr int kVec = 4;  // vectors per lane per iteration
 
 __device__ __forceinline__ char *state_ptr(const AdamArgs &a, uint64_t x) {
     if (a.n_ext == 1) return a.ext[0] + x;
@@ -37,6 +38,7 @@ __device__ __forceinline__ float adam1(float &p, float g, float &m, float &v, co
     return p;
 }
 
+template <int kVec>  // vectors per lane in flight per iteration
 __global__ __launch_bounds__(kThreads) void adam_remote_kernel(AdamArgs a) {
     const uint64_t nvec = a.n >> 2;
     const uint64_t lanes = (uint64_t)gridDim.x * kThreads;
@@ -91,21 +93,35 @@ __global__ __launch_bounds__(kThreads) void adam_remote_kernel(AdamArgs a) {
 
 }  // namespace
 
+static int env_int(const char *k, int dflt) {
+    const char *v = std::getenv(k);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
 hipError_t adam_remote_launch(const AdamArgs &a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     if (a.n_ext < 1 || a.n_ext > (uint32_t)kXferMaxExtents) return hipErrorInvalidValue;
     if (a.n_ext > 1 && a.unit_shift < 4) return hipErrorInvalidValue;
     if (((uintptr_t)a.p | (uintptr_t)a.g | a.m_off | a.v_off) & 15u) return hipErrorInvalidValue;
+    // Measured (profiles/optim_offload_r01.json "adam_kernel_sweep"): 4 vectors
+    // per lane and 2 workgroups per CU are the fastest on HBM state (1.40 ms for
+    // 256 Mi params); 8 vectors per lane is 4x slower. Knobs kept for re-tuning.
+    static const int vec = env_int("OCM_ADAM_VEC", 4);
+    static const int per_cu = env_int("OCM_ADAM_BLOCKS_PER_CU", 2);
+    const int v = vec == 2 ? 2 : 4;
     const uint64_t nvec = a.n >> 2;
-    uint64_t want = (nvec + (uint64_t)kThreads * kVec - 1) / ((uint64_t)kThreads * kVec);
+    uint64_t want = (nvec + (uint64_t)kThreads * v - 1) / ((uint64_t)kThreads * v);
     if (want < 1) want = 1;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
-    const uint64_t cap = (uint64_t)cus * 4;
+    const uint64_t cap = (uint64_t)cus * (uint64_t)(per_cu > 0 ? per_cu : 2);
     const unsigned grid = (unsigned)(want < cap ? want : cap);
-    hipLaunchKernelGGL(adam_remote_kernel, dim3(grid), dim3(kThreads), 0, stream, a);
+    if (v == 2)
+        hipLaunchKernelGGL(adam_remote_kernel<2>, dim3(grid), dim3(kThreads), 0, stream, a);
+    else
+        hipLaunchKernelGGL(adam_remote_kernel<4>, dim3(grid), dim3(kThreads), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -36,6 +36,7 @@ def main() -> None:
     ap.add_argument("--chunk", default="16777216,67108864")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--fused-hbm-only", action="store_true", help="only the fused kernel on HBM state (tuning sweeps)")
     args = ap.parse_args()
     dev = "cuda:0"
     n_params = 4
@@ -55,7 +56,7 @@ def main() -> None:
         return (time.perf_counter() - t0) / args.steps
 
     res = {"elems": args.elems, "moment_bytes": 8 * args.elems, "steps": args.steps}
-    for name, kw in (("torch_resident_ms", {}), ("torch_fused_resident_ms", {"fused": True})):
+    for name, kw in (() if args.fused_hbm_only else (("torch_resident_ms", {}), ("torch_fused_resident_ms", {"fused": True}))):
         try:
             opt = torch.optim.Adam(params, lr=1e-3, **kw)
             res[name] = round(timed(opt.step) * 1e3, 3)
@@ -66,8 +67,8 @@ def main() -> None:
     print(json.dumps(res), flush=True)
     with Mesh(2, gpus=[0, 0]) as m:
         with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
-            for name, flags in (("ocm_hbm", 0), ("ocm_host", api.OCM_ALLOC_HOST_TIER)):
-                for chunk in [0] + [int(x) for x in args.chunk.split(",")]:
+            for name, flags in (("ocm_hbm", 0),) + ((("ocm_host", api.OCM_ALLOC_HOST_TIER),) if not args.fused_hbm_only else ()):
+                for chunk in [0] + ([int(x) for x in args.chunk.split(",")] if not args.fused_hbm_only else []):
                     mode = "fused" if chunk == 0 else "staged"
                     o = OffloadedAdam(params, c, lr=1e-3, chunk_elems=chunk or 1, flags=flags, mode=mode)
                     tier = o.allocs[0].remote_info()["extents"][0]["tier"]
