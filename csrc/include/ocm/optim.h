@@ -13,8 +13,8 @@
 namespace ocm {
 
 struct AdamArgs {
-    float *p;                        // parameters (this GPU), n elements, 16-byte aligned
-    const float *g;                  // gradients (this GPU), n elements, 16-byte aligned
+    float *p;                        // parameters (this GPU), n elements, 16-byte aligned (bf16: 8-byte)
+    const float *g;                  // gradients (this GPU), n elements, 16-byte aligned (bf16: 8-byte)
     char *ext[kXferMaxExtents];      // extent bases of the striped state space
     uint32_t n_ext;
     uint32_t unit_shift;             // log2(stripe unit) when n_ext > 1
@@ -23,10 +23,14 @@ struct AdamArgs {
     float b1, b2, eps, wd;           // betas, eps, L2 weight decay
     float step_size;                 // lr / (1 - b1^t)
     float inv_sqrt_bc2;              // 1 / sqrt(1 - b2^t)
+    uint32_t bf16;                   // 1: p and g are bf16; fp32 master weights at w_off in the state
+    uint64_t w_off;                  // byte offset of element 0's master weight (bf16 mode, 16-byte aligned)
 };
 
 // torch.optim.Adam's update (L2 weight decay, bias correction), one pass:
 // reads p, g (local) and m, v (remote), writes p (local) and m, v (remote).
+// bf16 mode: the update runs on the fp32 master weights (remote) and p gets
+// their bf16 rounding (round to nearest even).
 hipError_t adam_remote_launch(const AdamArgs &a, hipStream_t stream);
 
 }  // namespace ocm

@@ -91,6 +91,83 @@ __global__ __launch_bounds__(kThreads) void adam_remote_kernel(AdamArgs a) {
     }
 }
 
+// ---- mixed precision: bf16 parameters and gradients here, fp32 master
+// weights and moments in the remote half. Local footprint 4 bytes/parameter
+// (bf16 p + g), remote 12; one pass updates the master, the moments and the
+// bf16 copy (round to nearest even, like torch's .to(torch.bfloat16)).
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf16_to_f32(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+
+__device__ __forceinline__ unsigned short f32_to_bf16(float f) {
+    unsigned u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40u);  // quiet NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (unsigned short)(u >> 16);
+}
+
+template <int kVec>
+__global__ __launch_bounds__(kThreads) void adam_remote_bf16_kernel(AdamArgs a) {
+    const uint64_t nvec = a.n >> 2;
+    const uint64_t lanes = (uint64_t)gridDim.x * kThreads;
+    const uint64_t tid = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    u16x4 *p4 = reinterpret_cast<u16x4 *>(a.p);
+    const u16x4 *g4 = reinterpret_cast<const u16x4 *>(a.g);
+    for (uint64_t base = tid; base < nvec; base += lanes * kVec) {
+        f32x4 w[kVec], m[kVec], v[kVec];
+        u16x4 g[kVec];
+        f32x4 *wp[kVec], *mp[kVec], *vp[kVec];
+#pragma unroll
+        for (int k = 0; k < kVec; k++) {
+            const uint64_t i = base + (uint64_t)k * lanes;
+            if (i < nvec) {
+                wp[k] = reinterpret_cast<f32x4 *>(state_ptr(a, a.w_off + (i << 4)));
+                mp[k] = reinterpret_cast<f32x4 *>(state_ptr(a, a.m_off + (i << 4)));
+                vp[k] = reinterpret_cast<f32x4 *>(state_ptr(a, a.v_off + (i << 4)));
+                w[k] = __builtin_nontemporal_load(wp[k]);
+                m[k] = __builtin_nontemporal_load(mp[k]);
+                v[k] = __builtin_nontemporal_load(vp[k]);
+                g[k] = __builtin_nontemporal_load(g4 + i);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kVec; k++) {
+            const uint64_t i = base + (uint64_t)k * lanes;
+            if (i < nvec) {
+                u16x4 out;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    float wj = w[k][j], mj = m[k][j], vj = v[k][j];
+                    adam1(wj, bf16_to_f32(g[k][j]), mj, vj, a);
+                    w[k][j] = wj;
+                    m[k][j] = mj;
+                    v[k][j] = vj;
+                    out[j] = f32_to_bf16(wj);
+                }
+                p4[i] = out;
+                __builtin_nontemporal_store(w[k], wp[k]);
+                __builtin_nontemporal_store(m[k], mp[k]);
+                __builtin_nontemporal_store(v[k], vp[k]);
+            }
+        }
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        unsigned short *p16 = reinterpret_cast<unsigned short *>(a.p);
+        const unsigned short *g16 = reinterpret_cast<const unsigned short *>(a.g);
+        for (uint64_t i = nvec << 2; i < a.n; i++) {
+            float *wq = reinterpret_cast<float *>(state_ptr(a, a.w_off + 4 * i));
+            float *mq = reinterpret_cast<float *>(state_ptr(a, a.m_off + 4 * i));
+            float *vq = reinterpret_cast<float *>(state_ptr(a, a.v_off + 4 * i));
+            float wj = *wq, mj = *mq, vj = *vq;
+            adam1(wj, bf16_to_f32(g16[i]), mj, vj, a);
+            *wq = wj;
+            *mq = mj;
+            *vq = vj;
+            p16[i] = f32_to_bf16(wj);
+        }
+    }
+}
+
 }  // namespace
 
 static int env_int(const char *k, int dflt) {
@@ -102,7 +179,9 @@ hipError_t adam_remote_launch(const AdamArgs &a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     if (a.n_ext < 1 || a.n_ext > (uint32_t)kXferMaxExtents) return hipErrorInvalidValue;
     if (a.n_ext > 1 && a.unit_shift < 4) return hipErrorInvalidValue;
-    if (((uintptr_t)a.p | (uintptr_t)a.g | a.m_off | a.v_off) & 15u) return hipErrorInvalidValue;
+    if (a.bf16 ? ((((uintptr_t)a.p | (uintptr_t)a.g) & 7u) || ((a.w_off | a.m_off | a.v_off) & 15u))
+               : (((uintptr_t)a.p | (uintptr_t)a.g | a.m_off | a.v_off) & 15u))
+        return hipErrorInvalidValue;
     // Measured (profiles/optim_offload_r01.json "adam_kernel_sweep"): 4 vectors
     // per lane and 2 workgroups per CU are the fastest on HBM state (1.40 ms for
     // 256 Mi params); 8 vectors per lane is 4x slower. Knobs kept for re-tuning.
@@ -118,7 +197,9 @@ hipError_t adam_remote_launch(const AdamArgs &a, hipStream_t stream) {
         cus = 256;
     const uint64_t cap = (uint64_t)cus * (uint64_t)(per_cu > 0 ? per_cu : 2);
     const unsigned grid = (unsigned)(want < cap ? want : cap);
-    if (v == 2)
+    if (a.bf16)
+        hipLaunchKernelGGL(adam_remote_bf16_kernel<4>, dim3(grid), dim3(kThreads), 0, stream, a);
+    else if (v == 2)
         hipLaunchKernelGGL(adam_remote_kernel<2>, dim3(grid), dim3(kThreads), 0, stream, a);
     else
         hipLaunchKernelGGL(adam_remote_kernel<4>, dim3(grid), dim3(kThreads), 0, stream, a);

@@ -621,21 +621,39 @@ void ocm_x_counters(uint64_t out[17]) {
 // exp_avg / exp_avg_sq of element 0 sit at byte offsets m_off / v_off of the
 // remote half. hp = {b1, b2, eps, weight_decay, step_size, 1/sqrt(bias_correction2)}.
 // Queued on `stream` (e.g. torch's current stream); no host wait.
+static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64_t w_off, uint64_t m_off,
+                       uint64_t v_off, const float hp[6], void *stream, bool bf16);
+
 int ocm_x_adam(ocm_alloc_t a, float *p, const float *g, uint64_t n, uint64_t m_off, uint64_t v_off,
                const float hp[6], void *stream) {
+    return adam_common(a, p, g, n, 0, m_off, v_off, hp, stream, false);
+}
+
+// Mixed precision: p / g are bf16 on this GPU, the fp32 master weights sit at
+// byte offset w_off of the remote half next to the moments.
+int ocm_x_adam_bf16(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64_t w_off, uint64_t m_off,
+                    uint64_t v_off, const float hp[6], void *stream) {
+    return adam_common(a, p, g, n, w_off, m_off, v_off, hp, stream, true);
+}
+
+static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64_t w_off, uint64_t m_off,
+                       uint64_t v_off, const float hp[6], void *stream, bool bf16) {
     State &s = S();
     if (!a || !p || !g || !hp) OCM_FAIL(-1, "ocm_x_adam: null argument");
     if (s.device < 0) OCM_FAIL(-1, "ocm_x_adam needs a GPU");
     if (!is_pair(a->kind) || a->ext.empty() || !a->all_dev_ok)
         OCM_FAIL(-1, "ocm_x_adam needs a remote half this GPU can address (HBM or host tier, not another node)");
     if (n > (UINT64_MAX >> 3) || m_off > a->remote_bytes || 4 * n > a->remote_bytes - m_off ||
-        v_off > a->remote_bytes || 4 * n > a->remote_bytes - v_off)
+        v_off > a->remote_bytes || 4 * n > a->remote_bytes - v_off ||
+        (bf16 && (w_off > a->remote_bytes || 4 * n > a->remote_bytes - w_off)))
         OCM_FAIL(-1, "ocm_x_adam: state range exceeds the remote half (%zu bytes)", a->remote_bytes);
     if (a->ext.size() > (size_t)kXferMaxExtents) OCM_FAIL(-1, "ocm_x_adam: too many extents");
     AdamArgs x;
     std::memset(&x, 0, sizeof(x));
-    x.p = p;
-    x.g = g;
+    x.p = static_cast<float *>(p);
+    x.g = static_cast<const float *>(g);
+    x.bf16 = bf16 ? 1u : 0u;
+    x.w_off = w_off;
     for (size_t i = 0; i < a->ext.size(); i++) x.ext[i] = a->ext[i].dptr;
     x.n_ext = (uint32_t)a->ext.size();
     if (x.n_ext > 1) {

@@ -175,6 +175,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
             "ocm_x_service_stats": (None, [ctypes.POINTER(u64)]),
             "ocm_x_adam": (i32, [vp, vp, vp, u64, u64, u64, ctypes.POINTER(ctypes.c_float), vp]),
+            "ocm_x_adam_bf16": (i32, [vp, vp, vp, u64, u64, u64, u64, ctypes.POINTER(ctypes.c_float), vp]),
             "ocm_x_set_tuning": (None, [i32, i32, i32]),
             "ocm_x_set_tuning_dir": (i32, [i32, i32, i32, i32]),
             "ocm_x_batch": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, ctypes.POINTER(u64), i32, i32]),
@@ -419,14 +420,25 @@ class Allocation:
         if self._c.lib.ocm_copy_onesided_batch(self.handle, arr.array, arr.n, OCM_BATCH_ASYNC if async_ else 0) != 0:
             raise OcmError("ocm_copy_onesided_batch: " + last_error())
 
-    def adam(self, p, g, m_off: int, v_off: int, hp, stream=None) -> None:
-        """Fused Adam on GPU tensors p/g (float32, contiguous) with exp_avg / exp_avg_sq at byte
-        offsets m_off / v_off of the remote half, read and written in place (ocm_x_adam).
-        hp = (b1, b2, eps, weight_decay, step_size, 1/sqrt(bias_correction2)). Queued on `stream`
-        (default: torch's current stream)."""
+    def adam(self, p, g, m_off: int, v_off: int, hp, stream=None, w_off: Optional[int] = None) -> None:
+        """Fused Adam on GPU tensors p/g (contiguous) with exp_avg / exp_avg_sq at byte offsets
+        m_off / v_off of the remote half, read and written in place (ocm_x_adam). float32 p/g are
+        updated directly; bfloat16 p/g need w_off, the fp32 master weights in the remote half,
+        which the update runs on (ocm_x_adam_bf16). hp = (b1, b2, eps, weight_decay, step_size,
+        1/sqrt(bias_correction2)). Queued on `stream` (default: torch's current stream)."""
+        import torch
+
         h = (ctypes.c_float * 6)(*hp)
-        if self._c.lib.ocm_x_adam(self.handle, ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(g.data_ptr()),
-                                  p.numel(), m_off, v_off, h, self._stream_handle(stream)) != 0:
+        pp, gp, st = ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(g.data_ptr()), self._stream_handle(stream)
+        if p.dtype == torch.bfloat16:
+            if w_off is None or g.dtype != torch.bfloat16:
+                raise ValueError("bf16 parameters need bf16 gradients and w_off (fp32 master weights)")
+            rc = self._c.lib.ocm_x_adam_bf16(self.handle, pp, gp, p.numel(), w_off, m_off, v_off, h, st)
+        elif p.dtype == torch.float32 and g.dtype == torch.float32:
+            rc = self._c.lib.ocm_x_adam(self.handle, pp, gp, p.numel(), m_off, v_off, h, st)
+        else:
+            raise ValueError(f"unsupported dtypes {p.dtype} / {g.dtype}")
+        if rc != 0:
             raise OcmError("ocm_x_adam: " + last_error())
 
     def time_onesided(self, op_flag: int, nbytes: int, iters: int, local_offset: int = 0, remote_offset: int = 0) -> float:

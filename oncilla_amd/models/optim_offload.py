@@ -23,7 +23,9 @@ mode="fused" (default on a GPU) skips the staging altogether: one gfx950 kernel
 per parameter (ocm_x_adam, csrc/src/kernels/optim.hip) reads p and g from local
 HBM and exp_avg / exp_avg_sq straight from the remote half (peer HBM over xGMI or
 the pinned host tier), updates in registers and writes everything back: one pass,
-no copies, no extra local HBM traffic. mode="staged" is the path above (CPU
+no copies, no extra local HBM traffic. bfloat16 parameters keep fp32 master
+weights next to the moments in remote memory (mixed precision: 4 bytes per
+parameter stay local, bf16 p and g; 12 go remote). mode="staged" is the path above (CPU
 processes, and state on another node, which a kernel cannot address).
 
 The update is torch.optim.Adam's (L2 weight decay, bias correction; reference
@@ -48,9 +50,14 @@ class OffloadedAdam:
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
             raise ValueError("no parameters to optimize")
+        self.bf16 = all(p.dtype == torch.bfloat16 for p in self.params)
         for p in self.params:
-            if p.dtype != torch.float32 or not p.is_contiguous():
-                raise ValueError("OffloadedAdam takes contiguous float32 parameters")
+            if p.dtype not in (torch.float32, torch.bfloat16) or not p.is_contiguous():
+                raise ValueError("OffloadedAdam takes contiguous float32 or bfloat16 parameters")
+        if not self.bf16 and any(p.dtype != torch.float32 for p in self.params):
+            raise ValueError("mixed float32 / bfloat16 parameter lists are not supported")
+        if self.bf16 and mode == "staged":
+            raise ValueError("bfloat16 parameters use mode='fused' (fp32 master weights in remote memory)")
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.t = 0
         self.total = sum(p.numel() for p in self.params)
@@ -103,7 +110,9 @@ class OffloadedAdam:
             self.starts.append(pos)
             pos += (p.numel() + self._PAD - 1) // self._PAD * self._PAD
         self.padded = pos
-        remote = 8 * self.padded  # [exp_avg (padded) | exp_avg_sq (padded)]
+        # [exp_avg | exp_avg_sq] (padded), and for bf16 parameters [.. | fp32 master weights]
+        self.arrays = 3 if self.bf16 else 2
+        remote = 4 * self.arrays * self.padded
         self.stage = min(remote, 64 << 20)
         self.allocs = [client.alloc(kind, local_bytes=self.stage, remote_bytes=remote, flags=flags,
                                     stripe_unit=stripe_unit)]
@@ -112,6 +121,17 @@ class OffloadedAdam:
         torch.cuda.synchronize(client.device)
         for off in range(0, remote, self.stage):
             a.put(0, off, min(self.stage, remote - off))
+        if self.bf16:
+            # master weights start as the fp32 value of the bf16 parameters
+            buf = a.local_tensor(torch.float32)
+            step = self.stage // 4
+            for p, start in zip(self.params, self.starts):
+                flat = p.data.view(-1)
+                for e0 in range(0, p.numel(), step):
+                    e1 = min(p.numel(), e0 + step)
+                    buf[:e1 - e0].copy_(flat[e0:e1].float())
+                    torch.cuda.synchronize(client.device)
+                    a.put(0, 4 * (2 * self.padded + start + e0), 4 * (e1 - e0))
 
     def _step_fused(self) -> None:
         b1, b2 = self.betas
@@ -121,7 +141,8 @@ class OffloadedAdam:
             if p.grad is None:
                 continue
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-            a.adam(p.data, g, 4 * start, 4 * (self.padded + start), hp)
+            w_off = 4 * (2 * self.padded + start) if self.bf16 else None
+            a.adam(p.data, g, 4 * start, 4 * (self.padded + start), hp, w_off=w_off)
 
     def chunk_bytes(self, k: int) -> int:
         """Bytes of chunk k's record: its m half in full, then v up to the chunk's length."""
@@ -191,6 +212,24 @@ class OffloadedAdam:
         for a in self.allocs:
             a.wait()
 
+    def _read_fused(self, base: int, n: int):
+        import torch
+
+        a, t = self.allocs[0], torch.empty(n, dtype=torch.float32)
+        for e0 in range(0, n, self.stage // 4):
+            e1 = min(n, e0 + self.stage // 4)
+            a.get(0, base + 4 * e0, 4 * (e1 - e0))
+            t[e0:e1] = a.local_tensor(torch.float32)[:e1 - e0].cpu()
+        return t
+
+    def master(self, param_index: int):
+        """fp32 master weights of a bfloat16 parameter (fused mode), gathered from remote memory."""
+        if not self.bf16:
+            raise ValueError("master weights exist for bfloat16 parameters only")
+        self.synchronize()
+        p = self.params[param_index]
+        return self._read_fused(4 * (2 * self.padded + self.starts[param_index]), p.numel()).view(p.shape)
+
     def moments(self, param_index: int):
         """(exp_avg, exp_avg_sq) of one parameter, gathered from remote memory (tests, checkpoints)."""
         import torch
@@ -198,17 +237,8 @@ class OffloadedAdam:
         self.synchronize()
         p = self.params[param_index]
         if self.mode == "fused":
-            torch.cuda.synchronize(p.device)  # the update kernels ran on torch's stream
-            a, n = self.allocs[0], p.numel()
-            out = []
-            for base in (4 * self.starts[param_index], 4 * (self.padded + self.starts[param_index])):
-                t = torch.empty(n, dtype=torch.float32)
-                for e0 in range(0, n, self.stage // 4):
-                    e1 = min(n, e0 + self.stage // 4)
-                    a.get(0, base + 4 * e0, 4 * (e1 - e0))
-                    t[e0:e1] = a.local_tensor(torch.float32)[:e1 - e0].cpu()
-                out.append(t.view_as(p))
-            return out[0], out[1]
+            n, s0 = p.numel(), self.starts[param_index]
+            return (self._read_fused(4 * s0, n).view(p.shape), self._read_fused(4 * (self.padded + s0), n).view(p.shape))
         start = sum(q.numel() for q in self.params[:param_index])
         m = torch.empty(p.numel(), dtype=torch.float32)
         v = torch.empty(p.numel(), dtype=torch.float32)

@@ -17,7 +17,7 @@ def _model(device, seed=0):
 def _grads(params, step, device):
     g = torch.Generator().manual_seed(100 + step)
     for p in params:
-        p.grad = torch.randn(p.shape, generator=g).to(device)
+        p.grad = torch.randn(p.shape, generator=g).to(device=device, dtype=p.dtype)
 
 
 def _run(client, device, chunk, weight_decay, steps=4, **kw):
@@ -94,5 +94,42 @@ def test_fused_adam_on_striped_and_host_tier_state(mesh_factory, flags):
                 mm, vv = opt.moments(i)
                 torch.testing.assert_close(mm, opt_ref.state[a]["exp_avg"].cpu(), rtol=1e-5, atol=1e-7)
                 torch.testing.assert_close(vv, opt_ref.state[a]["exp_avg_sq"].cpu(), rtol=1e-4, atol=1e-6)
+        finally:
+            opt.close()
+
+
+@pytest.mark.gpu
+def test_fused_adam_bf16_params_with_remote_fp32_master(mesh_factory):
+    """Mixed precision: bf16 parameters and gradients on the GPU, fp32 master
+    weights and moments in another daemon's HBM. Oracle: torch.optim.Adam on
+    fp32 copies fed the same (bf16-valued) gradients; parameters = master
+    rounded to bf16."""
+    m = mesh_factory(2, gpus=[0, 0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        master_ref = _model("cuda:0", seed=5)
+        mine = [p.detach().to(torch.bfloat16).requires_grad_() for p in master_ref]
+        # the oracle starts from the same (bf16-representable) values
+        with torch.no_grad():
+            for r, q in zip(master_ref, mine):
+                r.copy_(q.float())
+        opt_ref = torch.optim.Adam(master_ref, lr=3e-3, weight_decay=0.01)
+        opt = OffloadedAdam(mine, c, lr=3e-3, weight_decay=0.01)
+        try:
+            assert opt.mode == "fused" and opt.bf16
+            for s in range(4):
+                _grads(mine, s, "cuda:0")
+                for q in mine:
+                    q.grad = q.grad.to(torch.bfloat16)
+                for r, q in zip(master_ref, mine):
+                    r.grad = q.grad.float()
+                opt_ref.step()
+                opt.step()
+            opt.synchronize()
+            for i, (r, q) in enumerate(zip(master_ref, mine)):
+                torch.testing.assert_close(opt.master(i), r.detach().cpu(), rtol=1e-5, atol=1e-6)
+                torch.testing.assert_close(q.detach().cpu(), r.detach().to(torch.bfloat16).cpu())
+                mm, vv = opt.moments(i)
+                torch.testing.assert_close(mm, opt_ref.state[r]["exp_avg"].cpu(), rtol=1e-5, atol=1e-7)
+                torch.testing.assert_close(vv, opt_ref.state[r]["exp_avg_sq"].cpu(), rtol=1e-4, atol=1e-6)
         finally:
             opt.close()

@@ -80,6 +80,18 @@ def main() -> None:
                     res[key.replace("_ms", "_GiBps")] = round(2 * 8 * args.elems / t / (1 << 30), 2)
                     res[f"{name}_tier"] = {1: "host", 2: "hbm"}[tier]
                     print(key, res[key], flush=True)
+            if not args.fused_hbm_only:
+                # mixed precision: bf16 params / grads here, fp32 master + moments remote (3 GiB)
+                p16 = [p.detach().to(torch.bfloat16).requires_grad_() for p in params]
+                for q, p in zip(p16, params):
+                    q.grad = p.grad.to(torch.bfloat16)
+                o = OffloadedAdam(p16, c, lr=1e-3)
+                t = timed(o.step)
+                o.close()
+                res["ocm_hbm_fused_bf16_ms"] = round(t * 1e3, 3)
+                res["ocm_hbm_fused_bf16_local_bytes_per_param"] = 4
+                print("ocm_hbm_fused_bf16_ms", res["ocm_hbm_fused_bf16_ms"], flush=True)
+                del p16
     line = json.dumps(res)
     if args.out:
         with open(args.out, "w") as f:
