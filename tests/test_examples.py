@@ -56,3 +56,18 @@ def test_cli_mesh_and_stats(native):
         p.send_signal(signal.SIGINT)
         p.wait(timeout=30)
     assert p.returncode == 0
+
+
+def test_train_offload_cpu(native):
+    out = _run([sys.executable, os.path.join(REPO, "examples", "train_offload.py"), "--steps", "150"],
+               env=dict(os.environ, OCM_NO_GPU="1"))
+    assert "mode=staged" in out and "loss" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bf16", [False, True])
+def test_train_offload_gpu(native, bf16):
+    env = {k: v for k, v in os.environ.items() if k != "OCM_NO_GPU"}
+    out = _run([sys.executable, os.path.join(REPO, "examples", "train_offload.py"), "--gpu", "0", "--steps", "150"]
+               + (["--bf16"] if bf16 else []), env=env)
+    assert "mode=fused" in out and "peer HBM" in out
