@@ -25,9 +25,12 @@ struct AdamArgs {
     float inv_sqrt_bc2;              // 1 / sqrt(1 - b2^t)
     uint32_t bf16;                   // 1: p and g are bf16; fp32 master weights at w_off in the state
     uint64_t w_off;                  // byte offset of element 0's master weight (bf16 mode, 16-byte aligned)
+    uint32_t decoupled;              // 1: AdamW (p *= decay before the step; wd unused)
+    float decay;                     // 1 - lr * weight_decay (AdamW)
 };
 
-// torch.optim.Adam's update (L2 weight decay, bias correction), one pass:
+// torch.optim.Adam's update (L2 weight decay, bias correction), or AdamW's
+// (decoupled weight decay) with `decoupled`, one pass:
 // reads p, g (local) and m, v (remote), writes p (local) and m, v (remote).
 // bf16 mode: the update runs on the fp32 master weights (remote) and p gets
 // their bf16 rounding (round to nearest even).

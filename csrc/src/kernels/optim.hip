@@ -30,7 +30,10 @@ __device__ __forceinline__ char *state_ptr(const AdamArgs &a, uint64_t x) {
 }
 
 __device__ __forceinline__ float adam1(float &p, float g, float &m, float &v, const AdamArgs &a) {
-    g = a.wd != 0.f ? g + a.wd * p : g;
+    if (a.decoupled)
+        p = p * a.decay;  // AdamW: p *= 1 - lr * weight_decay, gradient untouched
+    else if (a.wd != 0.f)
+        g = g + a.wd * p;  // Adam: L2 term in the gradient
     m = m + (1.f - a.b1) * (g - m);  // torch: exp_avg.lerp_(grad, 1 - beta1)
     v = a.b2 * v + (1.f - a.b2) * g * g;
     const float denom = sqrtf(v) * a.inv_sqrt_bc2 + a.eps;

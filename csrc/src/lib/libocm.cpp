@@ -619,25 +619,27 @@ void ocm_x_counters(uint64_t out[17]) {
 // Fused Adam over optimizer state kept in the remote half of `a` (see
 // ocm/optim.h): p/g are this GPU's parameters and gradients (n floats),
 // exp_avg / exp_avg_sq of element 0 sit at byte offsets m_off / v_off of the
-// remote half. hp = {b1, b2, eps, weight_decay, step_size, 1/sqrt(bias_correction2)}.
+// remote half. hp = {b1, b2, eps, weight_decay, step_size, 1/sqrt(bias_correction2),
+// adamw_decay}: adamw_decay = 1 - lr * weight_decay selects AdamW (decoupled decay;
+// weight_decay then unused), 0 selects Adam with the L2 term.
 // Queued on `stream` (e.g. torch's current stream); no host wait.
 static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64_t w_off, uint64_t m_off,
-                       uint64_t v_off, const float hp[6], void *stream, bool bf16);
+                       uint64_t v_off, const float hp[7], void *stream, bool bf16);
 
 int ocm_x_adam(ocm_alloc_t a, float *p, const float *g, uint64_t n, uint64_t m_off, uint64_t v_off,
-               const float hp[6], void *stream) {
+               const float hp[7], void *stream) {
     return adam_common(a, p, g, n, 0, m_off, v_off, hp, stream, false);
 }
 
 // Mixed precision: p / g are bf16 on this GPU, the fp32 master weights sit at
 // byte offset w_off of the remote half next to the moments.
 int ocm_x_adam_bf16(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64_t w_off, uint64_t m_off,
-                    uint64_t v_off, const float hp[6], void *stream) {
+                    uint64_t v_off, const float hp[7], void *stream) {
     return adam_common(a, p, g, n, w_off, m_off, v_off, hp, stream, true);
 }
 
 static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64_t w_off, uint64_t m_off,
-                       uint64_t v_off, const float hp[6], void *stream, bool bf16) {
+                       uint64_t v_off, const float hp[7], void *stream, bool bf16) {
     State &s = S();
     if (!a || !p || !g || !hp) OCM_FAIL(-1, "ocm_x_adam: null argument");
     if (s.device < 0) OCM_FAIL(-1, "ocm_x_adam needs a GPU");
@@ -670,6 +672,8 @@ static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64
     x.wd = hp[3];
     x.step_size = hp[4];
     x.inv_sqrt_bc2 = hp[5];
+    x.decoupled = hp[6] != 0.f ? 1u : 0u;
+    x.decay = hp[6];
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (wait_alloc(a) != 0) return -1;  // queued async ops on this allocation come first
     DeviceGuard dg(s.device);

@@ -425,10 +425,12 @@ class Allocation:
         m_off / v_off of the remote half, read and written in place (ocm_x_adam). float32 p/g are
         updated directly; bfloat16 p/g need w_off, the fp32 master weights in the remote half,
         which the update runs on (ocm_x_adam_bf16). hp = (b1, b2, eps, weight_decay, step_size,
-        1/sqrt(bias_correction2)). Queued on `stream` (default: torch's current stream)."""
+        1/sqrt(bias_correction2)[, adamw_decay]); adamw_decay = 1 - lr * weight_decay selects AdamW.
+        Queued on `stream` (default: torch's current stream)."""
         import torch
 
-        h = (ctypes.c_float * 6)(*hp)
+        hp = tuple(hp) + (0.0,) * (7 - len(hp))
+        h = (ctypes.c_float * 7)(*hp)
         pp, gp, st = ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(g.data_ptr()), self._stream_handle(stream)
         if p.dtype == torch.bfloat16:
             if w_off is None or g.dtype != torch.bfloat16:

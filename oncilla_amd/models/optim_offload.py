@@ -42,9 +42,11 @@ from .. import api
 
 
 class OffloadedAdam:
+    """Adam (or AdamW with decoupled=True) with its state in disaggregated memory; see the module docstring."""
+
     def __init__(self, params: Iterable, client: api.Client, lr: float = 1e-3, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.0, chunk_elems: int = 16 << 20, flags: int = 0,
-                 mode: str = "auto", stripe_unit: int = 0):
+                 mode: str = "auto", stripe_unit: int = 0, decoupled: bool = False):
         import torch
 
         self.params = [p for p in params if p.requires_grad]
@@ -59,6 +61,7 @@ class OffloadedAdam:
         if self.bf16 and mode == "staged":
             raise ValueError("bfloat16 parameters use mode='fused' (fp32 master weights in remote memory)")
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.decoupled = decoupled  # AdamW (torch.optim.AdamW): decay the weights, not the gradient
         self.t = 0
         self.total = sum(p.numel() for p in self.params)
         self.C = max(1, min(int(chunk_elems), self.total))
@@ -135,7 +138,8 @@ class OffloadedAdam:
 
     def _step_fused(self) -> None:
         b1, b2 = self.betas
-        hp = (b1, b2, self.eps, self.weight_decay, self.lr / (1 - b1 ** self.t), 1 / math.sqrt(1 - b2 ** self.t))
+        hp = (b1, b2, self.eps, self.weight_decay, self.lr / (1 - b1 ** self.t), 1 / math.sqrt(1 - b2 ** self.t),
+              (1 - self.lr * self.weight_decay) if self.decoupled else 0.0)
         a = self.allocs[0]
         for p, start in zip(self.params, self.starts):
             if p.grad is None:
@@ -167,7 +171,9 @@ class OffloadedAdam:
             n = hi - lo
             pv = p.data.view(-1)[lo:hi]
             g = p.grad.view(-1)[lo:hi]
-            if self.weight_decay:
+            if self.decoupled:
+                pv.mul_(1 - self.lr * self.weight_decay)
+            elif self.weight_decay:
                 g = g.add(pv, alpha=self.weight_decay)
             m = slot[off:off + n]
             v = slot[self.C + off:self.C + off + n]
@@ -256,3 +262,11 @@ class OffloadedAdam:
         for a in self.allocs:
             a.free()
         self.allocs = []
+
+
+class OffloadedAdamW(OffloadedAdam):
+    """torch.optim.AdamW semantics (decoupled weight decay, default 1e-2) with offloaded state."""
+
+    def __init__(self, params, client, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2, **kw):
+        super().__init__(params, client, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decoupled=True, **kw)

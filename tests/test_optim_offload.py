@@ -5,7 +5,7 @@ import pytest
 import torch
 
 from oncilla_amd import api
-from oncilla_amd.models import OffloadedAdam
+from oncilla_amd.models import OffloadedAdam, OffloadedAdamW
 
 
 def _model(device, seed=0):
@@ -20,12 +20,12 @@ def _grads(params, step, device):
         p.grad = torch.randn(p.shape, generator=g).to(device=device, dtype=p.dtype)
 
 
-def _run(client, device, chunk, weight_decay, steps=4, **kw):
+def _run(client, device, chunk, weight_decay, steps=4, adamw=False, **kw):
     ref = _model(device)
     mine = [p.detach().clone().requires_grad_() for p in ref]
-    opt_ref = torch.optim.Adam(ref, lr=1e-2, betas=(0.8, 0.95), eps=1e-6, weight_decay=weight_decay)
-    opt = OffloadedAdam(mine, client, lr=1e-2, betas=(0.8, 0.95), eps=1e-6, weight_decay=weight_decay,
-                        chunk_elems=chunk, **kw)
+    ref_cls, cls = (torch.optim.AdamW, OffloadedAdamW) if adamw else (torch.optim.Adam, OffloadedAdam)
+    opt_ref = ref_cls(ref, lr=1e-2, betas=(0.8, 0.95), eps=1e-6, weight_decay=weight_decay)
+    opt = cls(mine, client, lr=1e-2, betas=(0.8, 0.95), eps=1e-6, weight_decay=weight_decay, chunk_elems=chunk, **kw)
     try:
         for s in range(steps):
             _grads(ref, s, device)
@@ -56,12 +56,20 @@ def test_offloaded_adam_matches_torch_cpu(mesh_factory, chunk, wd, monkeypatch):
         assert n == (2825 + chunk - 1) // chunk  # chunks span parameter boundaries
 
 
+def test_offloaded_adamw_matches_torch_cpu(mesh_factory, monkeypatch):
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    m = mesh_factory(2)
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        _run(c, "cpu", 700, 0.1, adamw=True)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,chunk", [("staged", 500), ("staged", 4096), ("fused", 0)])
-def test_offloaded_adam_matches_torch_gpu(mesh_factory, mode, chunk):
+@pytest.mark.parametrize("mode,chunk,adamw", [("staged", 500, False), ("staged", 4096, False), ("fused", 0, False),
+                                              ("fused", 0, True), ("staged", 700, True)])
+def test_offloaded_adam_matches_torch_gpu(mesh_factory, mode, chunk, adamw):
     m = mesh_factory(2, gpus=[0, 0])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
-        n = _run(c, "cuda:0", chunk or 1 << 20, 0.01, steps=5, mode=mode)
+        n = _run(c, "cuda:0", chunk or 1 << 20, 0.05 if adamw else 0.01, steps=5, mode=mode, adamw=adamw)
         assert n >= 1
 
 
