@@ -71,3 +71,21 @@ def test_train_offload_gpu(native, bf16):
     out = _run([sys.executable, os.path.join(REPO, "examples", "train_offload.py"), "--gpu", "0", "--steps", "150"]
                + (["--bf16"] if bf16 else []), env=env)
     assert "mode=fused" in out and "peer HBM" in out
+
+
+def _torchrun(n, port, extra, env=None):
+    return _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+                 "--master-addr", "127.0.0.1", "--master-port", str(port),
+                 os.path.join(REPO, "examples", "train_zero.py")] + extra, env=env)
+
+
+def test_train_zero_cpu(native):
+    out = _torchrun(2, 29661, ["--cpu"], env=dict(os.environ, OCM_NO_GPU="1"))
+    assert "2 ranks" in out and "host tier" in out and "mode=staged" in out
+
+
+@pytest.mark.gpu
+def test_train_zero_gpu_shared(native):
+    env = {k: v for k, v in os.environ.items() if k != "OCM_NO_GPU"}
+    out = _torchrun(2, 29662, ["--share-gpu"], env=env)
+    assert "2 ranks" in out and "peer HBM" in out and "mode=fused" in out
