@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--no-autotune", action="store_true",
                     help="N>1: skip the setup-time kernel autotune over the xGMI links (library defaults)")
     ap.add_argument("--no-hw-baseline", action="store_true", help="skip the N>1 runtime peer-copy extras")
+    ap.add_argument("--no-optim-extra", action="store_true", help="skip the fused remote-Adam extra")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -125,6 +126,56 @@ def hw_baseline_extras(dist, world: int, rank: int, local_rank: int) -> dict:
             out["links_from_rank0"] = links
     del bufs
     return out
+
+def optim_extra(client, dist, world: int, local_rank: int, elems: int = 64 << 20) -> dict:
+    """Fused remote-Adam step (models.OffloadedAdam) with the optimizer state placed by
+    the governor (striped over the peers' HBM for N>1: every rank at once, all-to-all
+    over xGMI; the host tier for N=1). After the timed region; never affects the metric."""
+    import torch
+
+    from oncilla_amd.models import OffloadedAdam
+
+    synced = [False]
+
+    def run():
+        p = torch.zeros(elems, device=f"cuda:{local_rank}").requires_grad_()
+        p.grad = torch.randn(elems, device=f"cuda:{local_rank}")
+        opt = OffloadedAdam([p], client, lr=1e-3)
+        try:
+            ext = opt.allocs[0].remote_info()["extents"]
+            for _ in range(2):
+                opt.step()
+            torch.cuda.synchronize(local_rank)
+            if dist is not None:
+                synced[0] = True
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                opt.step()
+            torch.cuda.synchronize(local_rank)
+            return {"s": (time.perf_counter() - t0) / 5, "extents": len(ext),
+                    "tier": "+".join(sorted({{1: "host", 2: "hbm"}[e["tier"]] for e in ext}))}
+        finally:
+            opt.close()
+
+    r, err = _local(run) if dist is None else (None, None)
+    if dist is not None:
+        # every rank reaches the barrier inside run() or this one, then the gather
+        try:
+            r = run()
+        except Exception as e:  # noqa: BLE001 - recorded
+            err = repr(e)[:200]
+            if not synced[0]:
+                dist.barrier()
+    res = gather_obj(dist, {"r": r, "err": err}, world)
+    errs = [x["err"] for x in res if x["err"]]
+    if errs:
+        return {"error": errs[0]}
+    t = max(x["r"]["s"] for x in res)
+    return {"params_per_rank": elems, "ms_per_step": round(t * 1e3, 3), "state_tier": res[0]["r"]["tier"],
+            "state_extents": res[0]["r"]["extents"],
+            "state_GiBps_per_rank": round(16 * elems / t / (1 << 30), 2)}
+
 
 def main() -> int:
     args = parse()
@@ -259,6 +310,9 @@ def main() -> int:
         # ---- extras for N > 1, after the timed region (never affect the metric) ----
         # Every rank reaches every collective below even when its local part
         # fails, so a failure is recorded instead of deadlocking the job.
+        optim = {}
+        if use_gpu and not args.no_optim_extra:
+            optim = optim_extra(client, dist, world, local_rank)
         baseline = {}
         if use_gpu and world > 1 and not args.no_hw_baseline:
             baseline = hw_baseline_extras(dist, world, rank, local_rank)
@@ -304,6 +358,8 @@ def main() -> int:
         }
         if tuned:
             result["autotune"] = tuned
+        if optim:
+            result["fused_remote_adam"] = optim
         if baseline:
             result["hw_baseline"] = baseline
     finally:
