@@ -34,6 +34,7 @@ enum XferVariant : int {
     XFER_AUTO = 0,
     XFER_REG = 1,    // register-staged, 8 x 16 B loads in flight per lane
     XFER_LDS = 2,    // LDS-DMA (global_load_lds_dwordx4) staged, wave-private double buffer
+    XFER_DMA = 3,    // no kernel: the runtime's copy engines, one hipMemcpyAsync per stripe segment
 };
 
 struct XferTuning {

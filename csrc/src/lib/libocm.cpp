@@ -709,7 +709,7 @@ void ocm_x_set_tuning(int variant, int blocks, int nt) {
 // winner of an autotune over the xGMI links; variant 0 clears it.
 int ocm_x_set_tuning_dir(int dir, int variant, int blocks, int nt) {
     if (dir != 0 && dir != 1) return -1;
-    if (variant < XFER_AUTO || variant > XFER_LDS || blocks < 0) return -1;
+    if (variant < XFER_AUTO || variant > XFER_DMA || blocks < 0) return -1;
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     XferTuning t;

@@ -342,10 +342,13 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     const bool lin_dev = lloc == LOC_DEVICE;
     // HBM extents: always the kernel. Host-tier extents: the kernel below
     // host_kernel_max (lower latency), the DMA engines above (higher peak).
-    const bool use_kernel = lin_dev && (a->any_gpu || s.host_engine_kernel || len <= s.host_kernel_max);
+    const XferTuning &dt = s.dir_tuning[put ? 1 : 0];
+    const bool dma_pick = (dt.variant != XFER_AUTO ? dt.variant : s.tuning.variant) == XFER_DMA;
+    const bool use_kernel =
+        lin_dev && !dma_pick && (a->any_gpu || s.host_engine_kernel || len <= s.host_kernel_max);
     hipError_t err = hipSuccess;
     // Small blocking ops go to the resident copy service (no launch, no stream sync).
-    if (lin_dev && a->all_dev_ok && !async && len <= s.svc_max) {
+    if (lin_dev && a->all_dev_ok && !async && len <= s.svc_max && !dma_pick) {
         XferArgs x;
         std::memset(&x, 0, sizeof(x));
         x.lin = lin;

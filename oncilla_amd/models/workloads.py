@@ -71,11 +71,12 @@ def characterize(alloc: api.Allocation, sizes: Iterable[int], target_s: float = 
     return out
 
 
-# Kernel configurations an autotune chooses from: (variant 0 auto / 1 register /
-# 2 LDS-DMA, grid cap 0 = default, nontemporal destination stores).
+# Configurations an autotune chooses from: (variant 0 auto / 1 register kernel /
+# 2 LDS-DMA kernel / 3 the runtime's copy engines, grid cap 0 = default,
+# nontemporal destination stores).
 TUNING_CANDIDATES = {"auto": (0, 0, 1), "reg_b256": (1, 256, 1), "reg_b1024": (1, 1024, 1),
                      "reg_b2048": (1, 2048, 1), "reg_nt0": (1, 0, 0), "lds_default": (2, 0, 1),
-                     "lds_b512": (2, 512, 1)}
+                     "lds_b512": (2, 512, 1), "dma": (3, 0, 1)}
 
 
 def autotune(alloc: api.Allocation, nbytes: int, reps: int = 3, gather=None, candidates: dict | None = None) -> dict:
