@@ -29,6 +29,24 @@ struct AdamArgs {
     float decay;                     // 1 - lr * weight_decay (AdamW)
 };
 
+// Many parameters in one launch: blockIdx.y picks the tensor (descriptors ride
+// in the kernarg segment), blockIdx.x strides within it. The common fields
+// (extents, hyper-parameters, bf16 / decoupled) come from `c`; its per-tensor
+// fields are unused.
+struct AdamTensor {
+    void *p;                         // fp32 or bf16 parameters (alignment as in AdamArgs)
+    const void *g;
+    uint64_t n, w_off, m_off, v_off;
+};
+constexpr int kAdamMaxTensors = 32;
+struct AdamMultiArgs {
+    AdamArgs c;
+    uint32_t count;
+    AdamTensor t[kAdamMaxTensors];
+};
+static_assert(sizeof(AdamMultiArgs) < 4096, "kernarg segment limit");
+hipError_t adam_remote_multi_launch(const AdamMultiArgs &a, hipStream_t stream);
+
 // torch.optim.Adam's update (L2 weight decay, bias correction), or AdamW's
 // (decoupled weight decay) with `decoupled`, one pass:
 // reads p, g (local) and m, v (remote), writes p (local) and m, v (remote).

@@ -171,6 +171,89 @@ __global__ __launch_bounds__(kThreads) void adam_remote_bf16_kernel(AdamArgs a) 
     }
 }
 
+// One launch for up to kAdamMaxTensors parameters (see AdamMultiArgs).
+template <bool kBf16>
+__global__ __launch_bounds__(kThreads) void adam_multi_kernel(AdamMultiArgs a) {
+    const AdamTensor &T = a.t[blockIdx.y];  // uniform: scalar loads from the kernarg segment
+    const AdamArgs &c = a.c;
+    const uint64_t nvec = T.n >> 2;
+    const uint64_t lanes = (uint64_t)gridDim.x * kThreads;
+    const uint64_t tid = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    constexpr int kV = 4;
+    for (uint64_t base = tid; base < nvec; base += lanes * kV) {
+        f32x4 w[kV], m[kV], v[kV], g[kV];
+        f32x4 *wp[kV], *mp[kV], *vp[kV];
+#pragma unroll
+        for (int k = 0; k < kV; k++) {
+            const uint64_t i = base + (uint64_t)k * lanes;
+            if (i < nvec) {
+                mp[k] = reinterpret_cast<f32x4 *>(state_ptr(c, T.m_off + (i << 4)));
+                vp[k] = reinterpret_cast<f32x4 *>(state_ptr(c, T.v_off + (i << 4)));
+                m[k] = __builtin_nontemporal_load(mp[k]);
+                v[k] = __builtin_nontemporal_load(vp[k]);
+                if constexpr (kBf16) {
+                    wp[k] = reinterpret_cast<f32x4 *>(state_ptr(c, T.w_off + (i << 4)));
+                    w[k] = __builtin_nontemporal_load(wp[k]);
+                    const u16x4 gh = __builtin_nontemporal_load(reinterpret_cast<const u16x4 *>(T.g) + i);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) g[k][j] = bf16_to_f32(gh[j]);
+                } else {
+                    w[k] = reinterpret_cast<const f32x4 *>(T.p)[i];
+                    g[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(T.g) + i);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kV; k++) {
+            const uint64_t i = base + (uint64_t)k * lanes;
+            if (i < nvec) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    float wj = w[k][j], mj = m[k][j], vj = v[k][j];
+                    adam1(wj, g[k][j], mj, vj, c);
+                    w[k][j] = wj;
+                    m[k][j] = mj;
+                    v[k][j] = vj;
+                }
+                if constexpr (kBf16) {
+                    u16x4 out;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) out[j] = f32_to_bf16(w[k][j]);
+                    reinterpret_cast<u16x4 *>(T.p)[i] = out;
+                    __builtin_nontemporal_store(w[k], wp[k]);
+                } else {
+                    reinterpret_cast<f32x4 *>(T.p)[i] = w[k];
+                }
+                __builtin_nontemporal_store(m[k], mp[k]);
+                __builtin_nontemporal_store(v[k], vp[k]);
+            }
+        }
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        for (uint64_t i = nvec << 2; i < T.n; i++) {
+            float *mq = reinterpret_cast<float *>(state_ptr(c, T.m_off + 4 * i));
+            float *vq = reinterpret_cast<float *>(state_ptr(c, T.v_off + 4 * i));
+            float mj = *mq, vj = *vq, wj, gj;
+            if constexpr (kBf16) {
+                wj = *reinterpret_cast<float *>(state_ptr(c, T.w_off + 4 * i));
+                gj = bf16_to_f32(static_cast<const unsigned short *>(T.g)[i]);
+            } else {
+                wj = static_cast<float *>(T.p)[i];
+                gj = static_cast<const float *>(T.g)[i];
+            }
+            adam1(wj, gj, mj, vj, c);
+            *mq = mj;
+            *vq = vj;
+            if constexpr (kBf16) {
+                *reinterpret_cast<float *>(state_ptr(c, T.w_off + 4 * i)) = wj;
+                static_cast<unsigned short *>(T.p)[i] = f32_to_bf16(wj);
+            } else {
+                static_cast<float *>(T.p)[i] = wj;
+            }
+        }
+    }
+}
+
 }  // namespace
 
 static int env_int(const char *k, int dflt) {
@@ -206,6 +289,41 @@ hipError_t adam_remote_launch(const AdamArgs &a, hipStream_t stream) {
         hipLaunchKernelGGL(adam_remote_kernel<2>, dim3(grid), dim3(kThreads), 0, stream, a);
     else
         hipLaunchKernelGGL(adam_remote_kernel<4>, dim3(grid), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t adam_remote_multi_launch(const AdamMultiArgs &a, hipStream_t stream) {
+    if (a.count == 0) return hipSuccess;
+    if (a.count > (uint32_t)kAdamMaxTensors) return hipErrorInvalidValue;
+    if (a.c.n_ext < 1 || a.c.n_ext > (uint32_t)kXferMaxExtents) return hipErrorInvalidValue;
+    if (a.c.n_ext > 1 && a.c.unit_shift < 4) return hipErrorInvalidValue;
+    uint64_t biggest = 0, total = 0;
+    for (uint32_t k = 0; k < a.count; k++) {
+        const AdamTensor &t = a.t[k];
+        const uintptr_t pal = a.c.bf16 ? 7u : 15u;
+        if ((((uintptr_t)t.p | (uintptr_t)t.g) & pal) || ((t.m_off | t.v_off | (a.c.bf16 ? t.w_off : 0)) & 15u))
+            return hipErrorInvalidValue;
+        if (t.n > biggest) biggest = t.n;
+        total += t.n;
+    }
+    if (biggest == 0) return hipSuccess;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    // Blocks per tensor (uniform over blockIdx.y): the tuned total of 2 workgroups
+    // per CU, shared in proportion to the biggest tensor's part of the work, so
+    // equal tensors split it evenly and one big tensor among small ones gets
+    // nearly all of it; the extra blocks of small tensors exit at once.
+    uint64_t want = ((biggest >> 2) + (uint64_t)kThreads * 4 - 1) / ((uint64_t)kThreads * 4);
+    if (want < 1) want = 1;
+    uint64_t cap = (uint64_t)((double)cus * 2.0 * (double)biggest / (double)total + 0.999);
+    if (cap < 1) cap = 1;
+    const unsigned gx = (unsigned)(want < cap ? want : cap);
+    if (a.c.bf16)
+        hipLaunchKernelGGL(adam_multi_kernel<true>, dim3(gx, a.count), dim3(kThreads), 0, stream, a);
+    else
+        hipLaunchKernelGGL(adam_multi_kernel<false>, dim3(gx, a.count), dim3(kThreads), 0, stream, a);
     return hipGetLastError();
 }
 

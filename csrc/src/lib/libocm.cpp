@@ -638,6 +638,56 @@ int ocm_x_adam_bf16(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64_t 
     return adam_common(a, p, g, n, w_off, m_off, v_off, hp, stream, true);
 }
 
+// Many parameters per launch (32 per kernel, descriptors in the kernarg
+// segment): p[i] / g[i] of n[i] elements, state at w_off[i] (bf16 only),
+// m_off[i], v_off[i] of the remote half. Same hp as ocm_x_adam.
+int ocm_x_adam_multi(ocm_alloc_t a, int count, void *const *p, const void *const *g, const uint64_t *n,
+                     const uint64_t *w_off, const uint64_t *m_off, const uint64_t *v_off, const float hp[7],
+                     int bf16, void *stream) {
+    State &s = S();
+    if (!a || count < 0 || (count && (!p || !g || !n || !m_off || !v_off || (bf16 && !w_off))) || !hp)
+        OCM_FAIL(-1, "ocm_x_adam_multi: null argument");
+    if (s.device < 0) OCM_FAIL(-1, "ocm_x_adam_multi needs a GPU");
+    if (!is_pair(a->kind) || a->ext.empty() || !a->all_dev_ok || a->ext.size() > (size_t)kXferMaxExtents)
+        OCM_FAIL(-1, "ocm_x_adam_multi needs a remote half this GPU can address");
+    const uint64_t rb = a->remote_bytes;
+    auto fits = [rb](uint64_t off, uint64_t len) { return off <= rb && len <= rb - off; };
+    AdamMultiArgs x;
+    std::memset(&x, 0, sizeof(x));
+    for (size_t i = 0; i < a->ext.size(); i++) x.c.ext[i] = a->ext[i].dptr;
+    x.c.n_ext = (uint32_t)a->ext.size();
+    if (x.c.n_ext > 1) {
+        const int sh = log2_exact(a->stripe_unit);
+        if (sh < 4) OCM_FAIL(-1, "ocm_x_adam_multi: stripe unit unusable");
+        x.c.unit_shift = (uint32_t)sh;
+    }
+    x.c.b1 = hp[0];
+    x.c.b2 = hp[1];
+    x.c.eps = hp[2];
+    x.c.wd = hp[3];
+    x.c.step_size = hp[4];
+    x.c.inv_sqrt_bc2 = hp[5];
+    x.c.decoupled = hp[6] != 0.f ? 1u : 0u;
+    x.c.decay = hp[6];
+    x.c.bf16 = bf16 ? 1u : 0u;
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (wait_alloc(a) != 0) return -1;
+    DeviceGuard dg(s.device);
+    for (int k0 = 0; k0 < count; k0 += kAdamMaxTensors) {
+        x.count = (uint32_t)std::min(count - k0, kAdamMaxTensors);
+        for (uint32_t j = 0; j < x.count; j++) {
+            const int i = k0 + (int)j;
+            if (n[i] > (UINT64_MAX >> 3) || !fits(m_off[i], 4 * n[i]) || !fits(v_off[i], 4 * n[i]) ||
+                (bf16 && !fits(w_off[i], 4 * n[i])))
+                OCM_FAIL(-1, "ocm_x_adam_multi: tensor %d state range exceeds the remote half", i);
+            x.t[j] = AdamTensor{p[i], g[i], n[i], bf16 ? w_off[i] : 0, m_off[i], v_off[i]};
+        }
+        const hipError_t e = adam_remote_multi_launch(x, static_cast<hipStream_t>(stream));
+        if (e != hipSuccess) OCM_FAIL(-1, "ocm_x_adam_multi launch: %s", hipGetErrorString(e));
+    }
+    return 0;
+}
+
 static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64_t w_off, uint64_t m_off,
                        uint64_t v_off, const float hp[7], void *stream, bool bf16) {
     State &s = S();

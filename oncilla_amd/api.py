@@ -175,6 +175,9 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
             "ocm_x_service_stats": (None, [ctypes.POINTER(u64)]),
             "ocm_x_adam": (i32, [vp, vp, vp, u64, u64, u64, ctypes.POINTER(ctypes.c_float), vp]),
+            "ocm_x_adam_multi": (i32, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(u64),
+                                       ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64),
+                                       ctypes.POINTER(ctypes.c_float), i32, vp]),
             "ocm_x_adam_bf16": (i32, [vp, vp, vp, u64, u64, u64, u64, ctypes.POINTER(ctypes.c_float), vp]),
             "ocm_x_set_tuning": (None, [i32, i32, i32]),
             "ocm_x_set_tuning_dir": (i32, [i32, i32, i32, i32]),
@@ -442,6 +445,24 @@ class Allocation:
             raise ValueError(f"unsupported dtypes {p.dtype} / {g.dtype}")
         if rc != 0:
             raise OcmError("ocm_x_adam: " + last_error())
+
+    def adam_multi(self, ps, gs, m_offs, v_offs, hp, w_offs=None, stream=None) -> None:
+        """ocm_x_adam_multi: the fused update of many parameters, 32 per launch. ps / gs are
+        lists of contiguous GPU tensors (all float32, or all bfloat16 with w_offs)."""
+        import torch
+
+        k = len(ps)
+        bf16 = k > 0 and ps[0].dtype == torch.bfloat16
+        if bf16 and w_offs is None:
+            raise ValueError("bf16 parameters need w_offs (fp32 master weights)")
+        arr_v, arr_u = ctypes.c_void_p * k, ctypes.c_uint64 * k
+        hp = tuple(hp) + (0.0,) * (7 - len(hp))
+        rc = self._c.lib.ocm_x_adam_multi(
+            self.handle, k, arr_v(*[t.data_ptr() for t in ps]), arr_v(*[t.data_ptr() for t in gs]),
+            arr_u(*[t.numel() for t in ps]), arr_u(*(w_offs or [0] * k)), arr_u(*m_offs), arr_u(*v_offs),
+            (ctypes.c_float * 7)(*hp), 1 if bf16 else 0, self._stream_handle(stream))
+        if rc != 0:
+            raise OcmError("ocm_x_adam_multi: " + last_error())
 
     def time_onesided(self, op_flag: int, nbytes: int, iters: int, local_offset: int = 0, remote_offset: int = 0) -> float:
         """Seconds per blocking one-sided op, timed inside the native library."""

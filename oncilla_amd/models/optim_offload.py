@@ -140,13 +140,17 @@ class OffloadedAdam:
         b1, b2 = self.betas
         hp = (b1, b2, self.eps, self.weight_decay, self.lr / (1 - b1 ** self.t), 1 / math.sqrt(1 - b2 ** self.t),
               (1 - self.lr * self.weight_decay) if self.decoupled else 0.0)
-        a = self.allocs[0]
+        ps, gs, mo, vo, wo = [], [], [], [], []
         for p, start in zip(self.params, self.starts):
             if p.grad is None:
                 continue
-            g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-            w_off = 4 * (2 * self.padded + start) if self.bf16 else None
-            a.adam(p.data, g, 4 * start, 4 * (self.padded + start), hp, w_off=w_off)
+            ps.append(p.data)
+            gs.append(p.grad if p.grad.is_contiguous() else p.grad.contiguous())
+            mo.append(4 * start)
+            vo.append(4 * (self.padded + start))
+            wo.append(4 * (2 * self.padded + start))
+        # every parameter in ceil(n / 32) launches (descriptors in the kernel arguments)
+        self.allocs[0].adam_multi(ps, gs, mo, vo, hp, w_offs=wo if self.bf16 else None)
 
     def chunk_bytes(self, k: int) -> int:
         """Bytes of chunk k's record: its m half in full, then v up to the chunk's length."""
