@@ -60,12 +60,17 @@ def parse():
 
 def coord_init(world: int):
     """gloo group for coordination only: touches no GPU, so every rank can
-    start its daemon before HIP is initialised in this process."""
+    start its daemon before HIP is initialised in this process. Every
+    collective is bounded (OCM_BENCH_TIMEOUT_S, default 300 s): a rank that
+    hangs makes the others fail with a diagnostic instead of burning the
+    job's time limit."""
     if world <= 1:
         return None
+    from datetime import timedelta
+
     import torch.distributed as dist
 
-    dist.init_process_group("gloo")
+    dist.init_process_group("gloo", timeout=timedelta(seconds=float(os.environ.get("OCM_BENCH_TIMEOUT_S", "300"))))
     return dist
 
 
@@ -76,6 +81,45 @@ def gather_obj(dist, obj, world):
     dist.all_gather_object(out, obj)
     return out
 
+
+class BenchAbort(RuntimeError):
+    """A phase failed on at least one rank; every rank raises it together."""
+
+    def __init__(self, phase: str, errors: dict):
+        super().__init__(f"phase {phase!r} failed on rank(s) {sorted(errors, key=int)}")
+        self.phase = phase
+        self.errors = errors
+
+
+class Phases:
+    """Run each setup/measurement step on every rank, then agree on the outcome.
+
+    A step that raises on one rank is published through the same all-gather the
+    other ranks wait on, so all of them stop together (BenchAbort) instead of
+    waiting in a barrier the failed rank never reaches. Test hook:
+    OCM_BENCH_RAISE="<rank>:<phase>" raises inside that phase on that rank."""
+
+    def __init__(self, dist, world: int, rank: int):
+        self.dist, self.world, self.rank = dist, world, rank
+        self.current = "init"
+        inj = os.environ.get("OCM_BENCH_RAISE", "")
+        self.inject = tuple(inj.split(":", 1)) if ":" in inj else None
+
+    def run(self, name: str, fn):
+        self.current = name
+        val, err = None, None
+        try:
+            if self.inject and int(self.inject[0]) == self.rank and self.inject[1] == name:
+                raise RuntimeError(f"injected failure (OCM_BENCH_RAISE) in phase {name}")
+            val = fn()
+        except Exception as e:  # noqa: BLE001 - published to every rank below
+            err = f"{type(e).__name__}: {e}"[:600]
+            print(f"rank {self.rank}: phase {name} failed: {err}", file=sys.stderr, flush=True)
+        res = gather_obj(self.dist, {"err": err}, self.world)
+        errs = {str(i): r["err"] for i, r in enumerate(res) if r["err"]}
+        if errs:
+            raise BenchAbort(name, errs)
+        return val
 
 
 def _local(fn):
@@ -177,6 +221,54 @@ def optim_extra(client, dist, world: int, local_rank: int, elems: int = 64 << 20
             "state_GiBps_per_rank": round(16 * elems / t / (1 << 30), 2)}
 
 
+def peer_table(client, use_gpu: bool, world: int, rank: int, local_rank: int, nbytes: int) -> dict:
+    """Rank 0 alone, after the timed region: one remote pair on each peer in
+    turn (remote_rank = p, unloaded links), blocking put/get of `nbytes`, and
+    the link type/hops between the two GPUs. The per-link view of the striped
+    all-to-all number (reference: one pair per remote node, test/ocm_test.c:323-425)."""
+    from oncilla_amd import api
+
+    out = {}
+    if rank != 0:
+        return out
+    kind = api.OCM_REMOTE_GPU if use_gpu else api.OCM_REMOTE_RDMA
+    for p in range(world):
+        if p == rank:
+            continue
+
+        def one():
+            a = client.alloc(kind, local_bytes=nbytes, remote_bytes=nbytes, remote_rank=p)
+            try:
+                ext = a.remote_info()["extents"]
+                a.fill(seed=77 + p)
+                a.put(0, 0, nbytes)
+                a.fill(seed=0)
+                a.get(0, 0, nbytes)
+                bad = a.check(seed=77 + p)
+                if bad:
+                    raise RuntimeError(f"{bad} words differ after the round trip to rank {p}")
+                t_put = a.time_onesided(1, nbytes, 3)
+                t_get = a.time_onesided(0, nbytes, 3)
+                row = {"put_GiBps": round(nbytes / t_put / GiB, 2), "get_GiBps": round(nbytes / t_get / GiB, 2),
+                       "owner_rank": ext[0]["owner_rank"], "owner_gpu": ext[0]["owner_gpu"],
+                       "tier": {1: "host", 2: "hbm"}[ext[0]["tier"]]}
+                if use_gpu and ext[0]["owner_gpu"] >= 0:
+                    row["link"] = api.link_info(local_rank, ext[0]["owner_gpu"])
+                return row
+            finally:
+                a.free()
+
+        row, err = _local(one)
+        out[str(p)] = row if row is not None else {"error": err}
+    return out
+
+
+def error_result(world: int, args, phase: str, errors: dict) -> dict:
+    return {"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "uint8", "error": f"phase {phase!r} failed", "phase": phase, "rank_errors": errors}
+
+
 def main() -> int:
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -195,9 +287,6 @@ def main() -> int:
         # Rehearsal mode for a 1-GPU box: every rank (and daemon) on GPU 0, so the
         # N-rank mesh, placement and IPC paths run without N devices.
         local_rank = 0
-    if use_gpu and local_rank >= ndev:
-        print(f"rank {rank}: LOCAL_RANK {local_rank} but only {ndev} GPUs", file=sys.stderr)
-        return 2
     max_bytes = args.max_bytes or ((1 << 30) if use_gpu else (16 << 20))
 
     from oncilla_amd import api
@@ -205,53 +294,68 @@ def main() -> int:
     from oncilla_amd.parallel.mesh import Mesh, free_ports
     from oncilla_amd.utils.paths import is_built
 
-    if not is_built():
-        if rank == 0:
-            from oncilla_amd.utils.build import build
-
-            build()
     dist = coord_init(world)
-    if dist is not None:
-        dist.barrier()
-
-    # ---- daemon mesh: one ocmd per rank / GPU ----
-    # rank 0 picks every daemon port while holding them all bound, so no two
-    # ranks of this node can be handed the same ephemeral port
-    ports = gather_obj(dist, free_ports(world) if rank == 0 else None, world)[0]
-    ns = f"bench{os.environ.get('MASTER_PORT', '0')}_{ports[0]}"
-    workdir = os.path.join("/tmp", f"ocm_{ns}")
-    os.makedirs(workdir, exist_ok=True)
-    gpus = [(local_rank if use_gpu else None) for _ in range(world)]
-    if use_gpu:
-        # every rank's GPU ordinal (single node: LOCAL_RANK == RANK)
-        gpus = gather_obj(dist, local_rank, world)
-    policy = "stripe" if args.pattern == "stripe" else "ring"
-    mesh = Mesh(world, gpus=gpus, ns=ns, policy=policy, workdir=workdir, ports=ports, ranks=[rank])
-    mesh.start(timeout=120)
-    if dist is not None:
-        dist.barrier()
-
-    result = {}
-    client = None
+    ph = Phases(dist, world, rank)
+    mesh = client = None
+    result, rc = {}, 0
     try:
-        client = api.Client(daemon_rank=rank, gpu=(local_rank if use_gpu else None), ns=ns)
-        if not use_gpu:
-            os.environ["OCM_NO_GPU"] = "1"
-        client.init()
+        def setup():
+            if use_gpu and local_rank >= ndev:
+                raise RuntimeError(f"LOCAL_RANK {local_rank} but only {ndev} GPUs visible")
+            if rank == 0 and not is_built():
+                from oncilla_amd.utils.build import build
+
+                build()
+
+        ph.run("setup", setup)
+        # ---- daemon mesh: one ocmd per rank / GPU ----
+        # rank 0 picks every daemon port while holding them all bound, so no two
+        # ranks of this node can be handed the same ephemeral port
+        ports = gather_obj(dist, free_ports(world) if rank == 0 else None, world)[0]
+        ns = f"bench{os.environ.get('MASTER_PORT', '0')}_{ports[0]}"
+        workdir = os.path.join("/tmp", f"ocm_{ns}")
+        os.makedirs(workdir, exist_ok=True)
+        gpus = [(local_rank if use_gpu else None) for _ in range(world)]
+        if use_gpu:
+            # every rank's GPU ordinal (single node: LOCAL_RANK == RANK)
+            gpus = gather_obj(dist, local_rank, world)
+        policy = "stripe" if args.pattern == "stripe" else "ring"
+        # Fault-injection hook for rehearsals: OCM_BENCH_FAULT="<rank>:<OCM_FAULT spec>"
+        # gives that rank's daemon the spec (csrc/src/daemon/mesh.cpp fault injection).
+        rank_env = {}
+        bf = os.environ.get("OCM_BENCH_FAULT", "")
+        if ":" in bf:
+            fr, spec = bf.split(":", 1)
+            rank_env[int(fr)] = {"OCM_FAULT": spec}
+        mesh = Mesh(world, gpus=gpus, ns=ns, policy=policy, workdir=workdir, ports=ports, ranks=[rank],
+                    rank_env=rank_env)
+        ph.run("mesh_start", lambda: mesh.start(timeout=120))
+
+        def attach():
+            c = api.Client(daemon_rank=rank, gpu=(local_rank if use_gpu else None), ns=ns)
+            if not use_gpu:
+                os.environ["OCM_NO_GPU"] = "1"
+            c.init()
+            return c
+
+        client = ph.run("client_init", attach)
         remote_kind = api.OCM_REMOTE_GPU if use_gpu else api.OCM_REMOTE_RDMA
 
         # ---- p50 ocm_alloc latency (remote pair, and the local malloc path) ----
-        lat_remote = wl.alloc_latency(client, remote_kind, args.alloc_samples, local_bytes=64 << 10,
-                                      remote_bytes=1 << 20)
-        lat_local = wl.alloc_latency(client, api.OCM_LOCAL_HOST, args.alloc_samples, local_bytes=1 << 20)
-        leases, _ = _local(lambda: client.stats()["lease_allocs"])
-        if dist is not None:
-            dist.barrier()
+        def latency():
+            lat_remote = wl.alloc_latency(client, remote_kind, args.alloc_samples, local_bytes=64 << 10,
+                                          remote_bytes=1 << 20)
+            lat_local = wl.alloc_latency(client, api.OCM_LOCAL_HOST, args.alloc_samples, local_bytes=1 << 20)
+            leases, _ = _local(lambda: client.stats()["lease_allocs"])
+            return lat_remote, lat_local, leases
+
+        lat_remote, lat_local, leases = ph.run("alloc_latency", latency)
 
         # ---- the sweep pair: 2 x max + 1 bytes each side (reference: 2 GiB + 1) ----
         pair_bytes = 2 * max_bytes + 1
         rflags = {"auto": 0, "loopback": api.OCM_ALLOC_LOOPBACK, "host": api.OCM_ALLOC_HOST_TIER}[args.remote]
-        pair = client.alloc(remote_kind, local_bytes=pair_bytes, remote_bytes=pair_bytes, flags=rflags)
+        pair = ph.run("pair_alloc", lambda: client.alloc(remote_kind, local_bytes=pair_bytes, remote_bytes=pair_bytes,
+                                                         flags=rflags))
         info = pair.remote_info()
 
         # ---- setup (untimed): pick the put/get kernel configuration over the
@@ -259,38 +363,46 @@ def main() -> int:
         # CPU runs (memcpy data path) do it too, so the multi-rank protocol is tested ----
         tuned = None
         if world > 1 and not args.no_autotune:
-            tuned = wl.autotune(pair, min(256 << 20, max_bytes), reps=3,
-                                gather=lambda obj: gather_obj(dist, obj, world))
+            tuned = ph.run("autotune", lambda: wl.autotune(pair, min(256 << 20, max_bytes), reps=3,
+                                                           gather=lambda obj: gather_obj(dist, obj, world)))
 
         # verify: pattern -> put -> clobber -> get -> check
-        pair.fill(seed=1234 + rank, nbytes=max_bytes)
-        pair.put(0, 0, max_bytes)
-        pair.fill(seed=0, nbytes=max_bytes)
-        pair.get(0, 0, max_bytes)
-        bad = pair.check(seed=1234 + rank, nbytes=max_bytes)
-        if bad:
-            raise RuntimeError(f"rank {rank}: {bad} words differ after put/get round trip")
+        def verify():
+            pair.fill(seed=1234 + rank, nbytes=max_bytes)
+            pair.put(0, 0, max_bytes)
+            pair.fill(seed=0, nbytes=max_bytes)
+            pair.get(0, 0, max_bytes)
+            bad = pair.check(seed=1234 + rank, nbytes=max_bytes)
+            if bad:
+                raise RuntimeError(f"{bad} words differ after put/get round trip")
 
+        ph.run("verify", verify)
         sizes = wl.sweep_sizes(args.min_bytes, max_bytes)
-        for _ in range(args.warmup):
-            wl.rw_sweep_step(pair, sizes)
+
+        def warmup():
+            for _ in range(args.warmup):
+                wl.rw_sweep_step(pair, sizes)
+
+        ph.run("warmup", warmup)
 
         def sync():
             if use_gpu:
                 torch.cuda.synchronize(local_rank)
 
+        # ---- timed region: barrier + sync on both sides; the phase's all-gather is the closing barrier ----
         if dist is not None:
             dist.barrier()
         sync()
-        t0 = time.perf_counter()
-        moved = 0
-        for _ in range(args.steps):
-            moved += wl.rw_sweep_step(pair, sizes)
-        sync()
-        t1 = time.perf_counter()
-        if dist is not None:
-            dist.barrier()
-        elapsed = t1 - t0
+
+        def timed():
+            t0 = time.perf_counter()
+            moved = 0
+            for _ in range(args.steps):
+                moved += wl.rw_sweep_step(pair, sizes)
+            sync()
+            return time.perf_counter() - t0, moved
+
+        elapsed, moved = ph.run("timed", timed)
 
         # max over ranks of elapsed, sum of bytes
         stats = gather_obj(dist, {"elapsed": elapsed, "moved": moved, "lat": lat_remote, "lat_local": lat_local,
@@ -300,14 +412,14 @@ def main() -> int:
 
         sweep = {}
         if not args.no_characterize:
-            ch = wl.characterize(pair, sizes)
+            ch = ph.run("characterize", lambda: wl.characterize(pair, sizes))
             chs = gather_obj(dist, ch, world)
             for s in sizes:
                 g = max(c[s]["get_s"] for c in chs)
                 p = max(c[s]["put_s"] for c in chs)
                 sweep[str(s)] = {"get_GiBps": round(world * s / g / GiB, 3), "put_GiBps": round(world * s / p / GiB, 3),
                                  "get_us": round(g * 1e6, 2), "put_us": round(p * 1e6, 2)}
-        # ---- extras for N > 1, after the timed region (never affect the metric) ----
+        # ---- extras, after the timed region (never affect the metric) ----
         # Every rank reaches every collective below even when its local part
         # fails, so a failure is recorded instead of deadlocking the job.
         optim = {}
@@ -316,9 +428,13 @@ def main() -> int:
         baseline = {}
         if use_gpu and world > 1 and not args.no_hw_baseline:
             baseline = hw_baseline_extras(dist, world, rank, local_rank)
-        pair.free()
-        if dist is not None:
-            dist.barrier()  # every rank is done with every owner before daemons stop
+        peers = {}
+        if world > 1:
+            # every rank is done with the sweep pair's owners before rank 0 loads one link at a time
+            gather_obj(dist, None, world)
+            peers = peer_table(client, use_gpu, world, rank, local_rank, min(256 << 20, max_bytes))
+            gather_obj(dist, None, world)
+        ph.run("free", pair.free)
 
         value = total / t_max / GiB
         tiers = sorted({e["tier"] for s in stats for e in s["extents"]})
@@ -362,20 +478,28 @@ def main() -> int:
             result["fused_remote_adam"] = optim
         if baseline:
             result["hw_baseline"] = baseline
+        if peers:
+            result["peers_from_rank0"] = peers
+    except BenchAbort as e:
+        result, rc = error_result(world, args, e.phase, e.errors), 1
+    except Exception as e:  # noqa: BLE001 - a collective timed out or failed: report, never hang
+        result, rc = error_result(world, args, ph.current, {str(rank): f"{type(e).__name__}: {e}"[:600]}), 1
     finally:
         if client is not None:
-            client.close()
-        mesh.stop()
+            _local(client.close)
+        if mesh is not None:
+            _local(mesh.stop)
     if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+        if rc == 0:
+            _local(dist.barrier)
+        _local(dist.destroy_process_group)
     if rank == 0:
         line = json.dumps(result)
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
-    return 0
+    return rc
 
 
 if __name__ == "__main__":

@@ -1,0 +1,33 @@
+// CPU placement next to a GPU.
+//
+// A blocking one-sided op and a control RPC are round trips between the app's
+// thread, the GPU (doorbell / completion words in host memory) and the
+// daemon's thread (mailbox). Their latency depends on where those threads
+// run: on the GPU's socket (its PCIe root) and sharing one L3 complex (CCD), a
+// cache line moves between them in tens of ns instead of hundreds. The daemon
+// of GPU g and the apps that copy on GPU g both restrict themselves to the
+// same CCD of g's NUMA node (chosen by g's ordinal, so the GPUs of one node get
+// different CCDs); OCM_PIN=0 turns it off. No reference counterpart: the
+// reference's daemon and apps ran wherever the scheduler put them.
+#pragma once
+#include <string>
+#include <vector>
+
+namespace ocm {
+
+// NUMA node of a PCI device ("0000:0a:00.0", any case); -1 if unknown.
+int pci_numa_node(const std::string &bus_id);
+
+// Every hardware thread of one L3 complex of `node`: complex `slot` modulo the
+// node's complexes, ordered by their lowest CPU. Empty if sysfs is unreadable.
+std::vector<int> ccd_cpus(int node, int slot);
+
+// Restrict the calling thread to `cpus` intersected with its allowed set.
+// Returns the number of CPUs it may now run on (0: unchanged, nothing in common).
+int pin_thread(const std::vector<int> &cpus);
+
+// pci_numa_node + ccd_cpus + pin_thread unless OCM_PIN=0; returns the CPUs pinned to
+// (empty: not pinned) and logs the choice under OCM_VERBOSE.
+std::vector<int> pin_near_gpu(const std::string &bus_id, int gpu_ordinal, const char *who);
+
+}  // namespace ocm

@@ -223,6 +223,7 @@ private:
     uint64_t n_alloc_ = 0, n_free_ = 0, n_reclaimed_ = 0, n_spilled_ = 0;
     // checkpoint / resume
     uint64_t boot_id_ = 0;               // this process lifetime
+    size_t pinned_cpus_ = 0;             // event loop restricted to this many CPUs near the GPU (0: not pinned)
     uint64_t mesh_token_ = 0;            // HELLO must carry it (hash of namespace + mesh key)
     uint64_t data_token_ = 0;            // network-tier data server: random per boot
     void send_hello(int fd);

@@ -112,32 +112,35 @@ uint32_t xfer_batch_tile_shift(uint32_t n_ext, uint32_t unit_shift);
 hipError_t xfer_batch_launch(const XferBatchArgs &a, const XferTuning &t, hipStream_t stream);
 
 // ---- persistent copy service (low-latency blocking one-sided ops) ----
-// A resident gang of `blocks` workgroups. Workgroup 0 polls a 128-byte request
-// record {args, sum, seq} (ServiceReq). One wave reads the whole record in a
-// single pass; `sum` (a hash of seq and the args) proves the args it read
-// belong to that seq, so torn or reordered writes of the record (the host's
-// write-combining buffer may reorder them) are simply read again.
-// Where the record lives: in the first 128 bytes of the host-pinned
-// ServiceSlot, polled across PCIe (default), or in fine-grained HBM of the
-// service's own GPU that the CPU writes through the PCIe BAR
-// (OCM_SERVICE_DOORBELL=hbm; then one lane polls the seq word in local memory).
-// Measured both ways: profiles/vram_doorbell_r01.json (bare probe: HBM wins),
-// profiles/svc_doorbell_r01.json (library: host wins by 0.4-0.7 us).
-// Requests of at most `solo_tiles` tiles are copied by workgroup 0 alone;
-// larger ones are published to the rest of the gang through a device-memory
-// box (agent-scope release/acquire), every workgroup copies its share of
-// tiles, and the last one to finish (device counter) makes the bytes visible
-// system-wide and publishes `done = seq` in the host-pinned slot.
-// Bounded: workgroup 0 exits on kServiceStop or after `idle_ticks` of
-// s_memrealtime (100 MHz) without work, and takes the gang with it; `exited`
-// records the first seq it did not serve.
+// A resident gang of `blocks` workgroups. Workgroup 0 polls one 128-byte
+// request record {args, gang, sum, seq} in host-pinned memory (ServiceReq),
+// 16 lanes in one load instruction; `sum` (a hash of seq and the other words)
+// proves that a snapshot is whole, so a torn or reordered write of the record
+// (write-combining may reorder the host's stores) is simply read again. The
+// host sizes each request: `gang` = active | target << 16, where `active`
+// workgroups (1 for small requests, up to `blocks`) copy tiles i, i + active, ...
+// and `target` is the running total of gang completions that finishes this
+// request (the device counter only grows, so it is never reset between
+// requests). Workgroup 0 relays a gang request, exactly as read, into the
+// device box with one write-through store; the other workgroups poll that copy
+// and check the same hash. Completion: every taking-part workgroup drains its
+// write-through stores (no release fence) and counts itself in; the one that
+// reaches `target` (or the only one) stores `done = seq` in the host slot.
+// Bounded: workgroup 0 leaves on kServiceStop or after `idle_ticks` of
+// s_memrealtime (100 MHz) without work; on leaving it stores STOP as the relayed
+// seq (the gang leaves on it) and `exited` = the first seq it did not serve.
+// Measured history: profiles/svc_trace_r02.json (a relay that re-hashed and
+// fenced first cost the gang ~2 us), profiles/svc_v3_direct_r02.json (every
+// workgroup polling the host record cost every op 3-4 us), profiles/
+// svc_doorbell_r01.json (a BAR-mapped HBM record was slower than host memory).
 constexpr unsigned long long kServiceStop = ~0ull;
 constexpr int kServiceArgWords = (int)((sizeof(XferArgs) + 7) / 8);
-static_assert(kServiceArgWords <= 14, "service request record holds 14 argument words");
+constexpr int kServiceReqGang = 13;  // record word: active | target << 16
+static_assert(kServiceArgWords <= kServiceReqGang, "service request record holds 13 argument words");
 
 struct alignas(128) ServiceReq {
-    unsigned long long args[14];      // XferArgs, host -> device (words 0..13)
-    unsigned long long sum;           // service_sum(seq, args) (word 14)
+    unsigned long long args[14];      // XferArgs (words 0..12), gang word (13), host -> device
+    unsigned long long sum;           // hash of seq and words 0..13 (word 14)
     unsigned long long seq;           // host -> device, written last (word 15, second cache line)
 };
 static_assert(sizeof(ServiceReq) == 128, "service request layout");
@@ -145,35 +148,45 @@ static_assert(__builtin_offsetof(ServiceReq, seq) == 120 && __builtin_offsetof(S
               "the kernel reads seq/sum as words 15/14");
 
 struct alignas(128) ServiceSlot {
-    ServiceReq req;                   // the request record when it is not in HBM
+    ServiceReq req;                   // the request record
     unsigned long long done;          // device -> host (own cache line)
     unsigned long long exited;        // device -> host: first seq NOT served when it left
-    unsigned long long gpu_ticks;     // device -> host: sum of doorbell-seen -> done ticks (100 MHz)
+    unsigned long long gpu_ticks;     // device -> host: sum of request-seen -> done ticks of workgroup 0 (100 MHz)
     unsigned long long pad[13];
 };
 static_assert(sizeof(ServiceSlot) == 256, "service slot layout");
 
-// Device-memory mailbox of the gang (zeroed before every launch).
+constexpr int kServiceTraceWgs = 64;
+// Device-memory state of the gang (zeroed before every launch).
 struct alignas(128) ServiceBox {
-    unsigned long long seq;           // last published gang request (kServiceStop: leave)
-    unsigned long long active;        // workgroups taking part in it (min(gang, tiles))
-    unsigned long long pad0[14];
-    unsigned long long cnt;           // workgroups finished with the current gang request
+    unsigned long long rec[16];       // relayed request record (ServiceReq words), STOP as seq to leave
+    unsigned long long cnt;           // gang completions, over all requests (only grows)
     unsigned long long pad1[15];
-    unsigned long long args[14];
-    unsigned long long pad2[2];
+    // OCM_SERVICE_PROTO bit 16 (TRACE): per workgroup, GPU clock (100 MHz) of its
+    // last request: seen, copy start, copy drained, counted in / done published.
+    unsigned long long trace[kServiceTraceWgs][4];
 };
 
-// Post one request (args, sum, then seq with release) and flush the CPU's
-// write-combining buffers, so a BAR-mapped record reaches the GPU now.
-void service_post(ServiceReq *req, const XferArgs &a, unsigned long long seq);
+// Workgroups that copy a (normalized) request: 1 when it has at most
+// `solo_tiles` tiles or the gang has one workgroup, else min(tiles, blocks).
+uint32_t service_gang_size(const XferArgs &a, unsigned blocks, unsigned solo_tiles);
+// Post one request (words, sum, then seq with release) and flush the CPU's
+// write-combining buffers. gang = active | target << 16.
+void service_post(ServiceReq *req, const XferArgs &a, unsigned long long gang, unsigned long long seq);
 // Store one word of the record (seq: 0 to re-arm, kServiceStop) and flush.
 void service_store_seq(ServiceReq *req, unsigned long long seq);
 
-// hbm_bell: `req` is in this GPU's HBM (poll its seq word alone, then read the record).
+// Hand-off protocol bits of the service (OCM_SERVICE_PROTO):
+//   WT        copied bytes are loaded sc1 and stored write-through (sc1), and
+//             every wave drains its stores: neither an acquire after the
+//             doorbell nor a system-scope release (buffer_wbl2) before `done`.
+//             Without WT: plain loads and stores, system acquire and release.
+//   TRACE     diagnostics: stamp each workgroup's phases into ServiceBox::trace
+constexpr unsigned kServiceProtoWT = 1u, kServiceProtoTrace = 16u;
+
+// first_seq >= 1: the first request this instance serves.
 hipError_t service_launch(ServiceReq *req, ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
-                          unsigned long long idle_ticks, unsigned blocks, unsigned solo_tiles, bool hbm_bell,
-                          hipStream_t stream);
+                          unsigned long long idle_ticks, unsigned blocks, unsigned proto, hipStream_t stream);
 
 // Deterministic 32-bit word pattern (word i of a buffer) for data verification.
 hipError_t pattern_fill(void *p, uint64_t words, uint64_t first_word, uint32_t seed, hipStream_t stream);

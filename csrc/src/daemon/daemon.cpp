@@ -7,6 +7,8 @@
 // src/mem.c:485-535 (mem_init / mem_new_request / mem_fin, inc/mem.h:29-33).
 #include "ocm/daemon.h"
 
+#include "ocm/affinity.h"
+
 #include <fcntl.h>
 #include <hip/hip_runtime_api.h>
 #include <signal.h>
@@ -147,6 +149,15 @@ int Daemon::init() {
     if (data_->start(cfg_.bind_ip.empty() ? "0.0.0.0" : cfg_.bind_ip) != 0) {
         OCM_WARN("rank %d: network data server unavailable; cross-node placement disabled here", rank_);
         data_.reset();
+    }
+    if (gpu_ >= 0) {
+        // The event loop next to its GPU, on the L3 complex its apps use (ocm/affinity.h);
+        // the data server's threads (started above) keep the full mask.
+        char bus[64] = {0};
+        if (hipDeviceGetPCIBusId(bus, sizeof(bus), gpu_) == hipSuccess)
+            pinned_cpus_ = pin_near_gpu(bus, gpu_, "ocmd").size();
+        else
+            (void)hipGetLastError();
     }
     {
         std::ifstream ur("/dev/urandom", std::ios::binary);

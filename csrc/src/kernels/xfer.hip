@@ -36,59 +36,106 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kWaveSlice = (1 << kTileShift) / kWaves;        // 8 KiB per wave per tile
 constexpr int kChunksPerWave = kWaveSlice / 1024;             // 8 glds (1 KiB each) per wave per tile
 
-template <bool NT>
+// Store flavours of the copy loops:
+//   ST_PLAIN  plain stores (cached in the XCD's L2);
+//   ST_NT     nontemporal stores (streaming; still released by a fence);
+//   ST_WT     write-through (sc1) stores: the bytes leave L2 for memory as they
+//             are stored, so a drain (s_waitcnt vmcnt(0)) of every storing wave
+//             is all a hand-off needs - no buffer_wbl2 release fence
+//             (guide: Guideline 16 R1; MI355X_MICROARCH.md visibility table);
+//             the loads of such a span are sc1 as well.
+enum StoreKind : int { ST_PLAIN = 0, ST_NT = 1, ST_WT = 2 };
+
+__device__ __forceinline__ u32x4 load16(const u32x4 *p) { return __builtin_nontemporal_load(p); }
+
+// Buffer descriptor over [base, base + bytes), built from wave-uniform values
+// (every caller passes a workgroup-uniform span). Buffer accesses are range
+// checked in hardware: a load past the end returns 0 without touching memory
+// and a store past the end is dropped, so a partial tile needs no per-lane
+// branches. (Branches around loads made the compiler put an s_waitcnt vmcnt(0)
+// in front of each one inside the service loop: a partial host-tier tile then
+// paid one PCIe round trip per 4 KiB.)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(const void *base, uint32_t bytes) {
+    const uint64_t b = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, (int)n, 0x00020000);
+}
+
+// cache-policy bits of buffer accesses on gfx950: nt = 2, sc1 = 16
+constexpr int kAuxNT = 2, kAuxSC1 = 16;
+
+template <int ST>
+constexpr int store_aux() {
+    return ST == ST_WT ? kAuxSC1 : ST == ST_NT ? kAuxNT : 0;
+}
+// ST_WT spans are loaded sc1 too: such loads bypass the CU's L1 and read host /
+// peer memory from memory rather than from stale L2 copies (measured:
+// profiles/svc_copy_probe_r02.json), so the persistent service needs no acquire.
+template <int ST>
+constexpr int load_aux() {
+    return ST == ST_WT ? kAuxSC1 : kAuxNT;
+}
+
+template <int ST>
+__device__ __forceinline__ char load_byte(const char *p) {
+    if constexpr (ST == ST_WT)
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1, like the vectors
+    else
+        return *p;
+}
+
+template <int ST>
+__device__ __forceinline__ void store_byte(char *p, char v) {
+    if constexpr (ST == ST_WT)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+    else
+        *p = v;
+}
+
+// Plain / nt store of one vector through a pointer (LDS drain, batch waves).
+template <int ST>
 __device__ __forceinline__ void store16(u32x4 *p, u32x4 v) {
-    if constexpr (NT)
+    if constexpr (ST == ST_NT)
         __builtin_nontemporal_store(v, p);
     else
         *p = v;
 }
 
-__device__ __forceinline__ u32x4 load16(const u32x4 *p) { return __builtin_nontemporal_load(p); }
-
-// Block-cooperative copy of n bytes (n <= one tile is the common case, any n works).
-template <bool NT>
+// Block-cooperative copy of n bytes (n <= one tile is the common case; spans
+// of 2 GiB or more, which no caller makes, take a byte loop).
+template <int ST>
 __device__ __forceinline__ void span_copy(char *__restrict__ dst, const char *__restrict__ src, uint64_t n) {
     const int tid = threadIdx.x;
     uint64_t head = (16u - ((uintptr_t)dst & 15u)) & 15u;
     if (head > n) head = n;
-    if ((uint64_t)tid < head) dst[tid] = src[tid];
+    if ((uint64_t)tid < head) store_byte<ST>(dst + tid, load_byte<ST>(src + tid));
     dst += head;
     src += head;
     n -= head;
-    if (((uintptr_t)src & 15u) == 0) {
-        const uint64_t nv = n >> 4;
-        const u32x4 *s = reinterpret_cast<const u32x4 *>(src);
-        u32x4 *d = reinterpret_cast<u32x4 *>(dst);
-        uint64_t base = 0;
-        for (; base + (uint64_t)kThreads * kUnroll <= nv; base += (uint64_t)kThreads * kUnroll) {
+    if (((uintptr_t)src & 15u) == 0 && n < (1ull << 31)) {
+        const uint32_t nv = (uint32_t)(n >> 4);
+        const __amdgpu_buffer_rsrc_t rs = span_rsrc(src, nv << 4);
+        const __amdgpu_buffer_rsrc_t rd = span_rsrc(dst, nv << 4);
+        // every load of a round in flight before its first store; past-the-end
+        // lanes of the last round are dropped by the range check
+        for (uint32_t base = 0; base < nv; base += kThreads * kUnroll) {
             u32x4 v[kUnroll];
 #pragma unroll
-            for (int k = 0; k < kUnroll; k++) v[k] = load16(s + base + (uint64_t)k * kThreads + tid);
+            for (int k = 0; k < kUnroll; k++)
+                v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((base + k * kThreads + tid) << 4), 0,
+                                                             load_aux<ST>());
 #pragma unroll
-            for (int k = 0; k < kUnroll; k++) store16<NT>(d + base + (uint64_t)k * kThreads + tid, v[k]);
-        }
-        if (base < nv) {
-            // Remainder (< kThreads x kUnroll vectors): every load issued before
-            // the first store, so a partial tile costs one memory round trip,
-            // not one per 4 KiB (a GET of host-tier memory pays PCIe latency each).
-            u32x4 v[kUnroll];
-#pragma unroll
-            for (int k = 0; k < kUnroll; k++) {
-                const uint64_t i = base + (uint64_t)k * kThreads + tid;
-                if (i < nv) v[k] = load16(s + i);
-            }
-#pragma unroll
-            for (int k = 0; k < kUnroll; k++) {
-                const uint64_t i = base + (uint64_t)k * kThreads + tid;
-                if (i < nv) store16<NT>(d + i, v[k]);
-            }
+            for (int k = 0; k < kUnroll; k++)
+                __builtin_amdgcn_raw_buffer_store_b128(v[k], rd, (int)((base + k * kThreads + tid) << 4), 0,
+                                                       store_aux<ST>());
         }
         const uint64_t tail = n & 15u;
-        if ((uint64_t)tid < tail) dst[(nv << 4) + tid] = src[(nv << 4) + tid];
+        if ((uint64_t)tid < tail) store_byte<ST>(dst + ((uint64_t)nv << 4) + tid, load_byte<ST>(src + ((uint64_t)nv << 4) + tid));
     } else {
         // Source and destination disagree mod 16: byte loop (rare; unaligned user offsets).
-        for (uint64_t i = tid; i < n; i += kThreads) dst[i] = src[i];
+        for (uint64_t i = tid; i < n; i += kThreads) store_byte<ST>(dst + i, load_byte<ST>(src + i));
     }
 }
 
@@ -164,7 +211,7 @@ __global__ __launch_bounds__(kThreads) void xfer_reg_kernel(XferArgs a, XferDone
     const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;
     for (uint64_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
         TileSpan s = tile_span(a, ti, first);
-        span_copy<NT>(s.dst, s.src, s.n);
+        span_copy<NT ? ST_NT : ST_PLAIN>(s.dst, s.src, s.n);
     }
     xfer_publish(d);
 }
@@ -194,7 +241,8 @@ __device__ __forceinline__ void drain_tile(char *dst, const char *buf, int wave,
 #pragma unroll
     for (int c = 0; c < kChunksPerWave; c++) v[c] = *reinterpret_cast<const u32x4 *>(l + c * 1024);
 #pragma unroll
-    for (int c = 0; c < kChunksPerWave; c++) store16<NT>(reinterpret_cast<u32x4 *>(g + c * 1024), v[c]);
+    for (int c = 0; c < kChunksPerWave; c++)
+        store16<NT ? ST_NT : ST_PLAIN>(reinterpret_cast<u32x4 *>(g + c * 1024), v[c]);
 }
 
 // Body of the LDS-DMA kernel: this workgroup's tiles ti, ti + grid, ...
@@ -222,7 +270,7 @@ __device__ __forceinline__ void lds_stream(const XferArgs &a, char *lds, int wav
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             drain_tile<NT>(cur.dst, lds + slot * (1 << kTileShift), wave, lane);
         } else {
-            span_copy<NT>(cur.dst, cur.src, cur.n);
+            span_copy<NT ? ST_NT : ST_PLAIN>(cur.dst, cur.src, cur.n);
         }
         if (nt >= ntiles) break;
         ti = nt;
@@ -351,9 +399,9 @@ __device__ __forceinline__ void wave_copy(char *__restrict__ dst, const char *__
 #pragma unroll
             for (int k = 0; k < kBatchUnroll; k++) v[k] = load16(s + i + k * 64);
 #pragma unroll
-            for (int k = 0; k < kBatchUnroll; k++) store16<NT>(d + i + k * 64, v[k]);
+            for (int k = 0; k < kBatchUnroll; k++) store16<NT ? ST_NT : ST_PLAIN>(d + i + k * 64, v[k]);
         }
-        for (; i < nv; i += 64) store16<NT>(d + i, load16(s + i));
+        for (; i < nv; i += 64) store16<NT ? ST_NT : ST_PLAIN>(d + i, load16(s + i));
         const uint64_t tail = n & 15u;
         if ((uint64_t)lane < tail) dst[(nv << 4) + lane] = src[(nv << 4) + lane];
     } else {
@@ -441,6 +489,13 @@ __host__ __device__ __forceinline__ unsigned long long service_mix(unsigned long
     return h ^ (h >> 31);
 }
 
+// Hash of a request record's seq and words 0..kServiceReqGang (args, gang word).
+__host__ __device__ __forceinline__ unsigned long long service_sum(unsigned long long seq, const unsigned long long *w) {
+    unsigned long long h = service_mix(0, seq);
+    for (int i = 0; i <= kServiceReqGang; i++) h = service_mix(h, w[i]);
+    return h;
+}
+
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long w, int lane) {
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)w, lane);
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(w >> 32), lane);
@@ -453,170 +508,161 @@ __device__ __forceinline__ uint64_t service_tiles(const XferArgs &a) {
 }
 
 // Tiles first, first + stride, ... of the request in `sh` (args at sh + 2).
+template <int ST>
 __device__ __forceinline__ void service_copy(const unsigned long long *sh, uint64_t first, uint64_t stride) {
     const XferArgs &a = *reinterpret_cast<const XferArgs *>(sh + 2);  // read in place (no scratch copy)
     const uint64_t ntiles = service_tiles(a);
     const uint64_t base = a.rem_off & ~((1ull << a.tile_shift) - 1);
     for (uint64_t ti = first; ti < ntiles; ti += stride) {
         TileSpan sp = tile_span(a, ti, base);
-        span_copy<false>(sp.dst, sp.src, sp.n);
+        span_copy<ST>(sp.dst, sp.src, sp.n);
     }
 }
 
-// Gang completion: each taking-part workgroup releases its bytes, then counts
-// itself in; the last of `active` publishes `done`.
-__device__ __forceinline__ void service_gang_done(ServiceSlot *slot, ServiceBox *box, unsigned long long s,
-                                                  unsigned long long active) {
-    block_release_system();
+__device__ __forceinline__ void service_stamp(ServiceBox *box, unsigned proto, int k) {
+    if ((proto & kServiceProtoTrace) && threadIdx.x == 0 && blockIdx.x < (unsigned)kServiceTraceWgs)
+        __hip_atomic_store(&box->trace[blockIdx.x][k], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Copy this workgroup's share of the request in `sh` and make it visible
+// system-wide; the workgroup that completes the request publishes `done`.
+__device__ __forceinline__ void service_serve(const unsigned long long *sh, unsigned long long s, ServiceSlot *slot,
+                                              ServiceBox *box, unsigned proto) {
+    const unsigned long long gang = sh[1];
+    const unsigned long long active = gang & 0xFFFFull, target = gang >> 16;
+    if (blockIdx.x >= active) return;  // block-uniform: workgroups past `active` sit this one out
+    service_stamp(box, proto, 1);
+    if (proto & kServiceProtoWT) {
+        service_copy<ST_WT>(sh, blockIdx.x, active);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its sc1 stores
+        __syncthreads();
+    } else {
+        service_copy<ST_PLAIN>(sh, blockIdx.x, active);
+        block_release_system();
+    }
+    service_stamp(box, proto, 2);
     if (threadIdx.x == 0) {
-        const unsigned long long old =
-            __hip_atomic_fetch_add(&box->cnt, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == active - 1) __hip_atomic_store(&slot->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        bool last = active == 1;
+        if (!last) {
+            const unsigned long long old =
+                (proto & kServiceProtoWT)
+                    ? __hip_atomic_fetch_add(&box->cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : __hip_atomic_fetch_add(&box->cnt, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            last = old == target - 1;
+        }
+        if (last) {
+            if (proto & kServiceProtoWT)
+                __hip_atomic_store(&slot->done, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // after the drain
+            else
+                __hip_atomic_store(&slot->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
+    service_stamp(box, proto, 3);
 }
 
+// Workgroup 0 polls the host request record across PCIe; for a gang request it
+// relays the record, as read (the host's hash included), to the gang through
+// device memory with one 16-lane write-through store, before anything else.
+// The gang polls that device copy: 32 workgroups polling the host record
+// directly cost every op 3-4 us (profiles/svc_v3_direct_r02.json), and a relay
+// that re-hashed and fenced first cost the gang ~2 us (profiles/svc_trace_r02.json).
 __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq, ServiceSlot *slot, ServiceBox *box,
                                                            unsigned long long first_seq,
-                                                           unsigned long long idle_ticks, unsigned solo_tiles,
-                                                           unsigned hbm_bell) {
+                                                           unsigned long long idle_ticks, unsigned proto) {
     __shared__ __attribute__((aligned(16))) unsigned long long sh[16];
     const int tid = threadIdx.x;
-    if (blockIdx.x != 0) {
-        // Gang member: wait for workgroup 0 to publish a large request in the box.
-        // Thread 0 takes a consistent snapshot {seq, active, args}: if seq moved
-        // while it read, that request completed without this workgroup (it was
-        // not taking part), so the newer one is taken instead.
-        unsigned long long last = 0;
-        for (;;) {
-            if (tid == 0) {
-                unsigned long long v = 0, act = 0;
-                for (;;) {
-                    v = __hip_atomic_load(&box->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (v == last || v == 0) {
-                        __builtin_amdgcn_s_sleep(4);
-                        continue;
-                    }
-                    if (v == kServiceStop) break;
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // box contents, and no stale cached data
-                    act = __hip_atomic_load(&box->active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (blockIdx.x < act)
-                        for (int i = 0; i < kServiceArgWords; i++)
-                            sh[2 + i] = __hip_atomic_load(&box->args[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the reads above before the re-check
-                    if (__hip_atomic_load(&box->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v) break;
-                }
-                sh[0] = v;
-                sh[1] = act;
-            }
-            __syncthreads();
-            const unsigned long long v = sh[0], active = sh[1];
-            if (v == kServiceStop) break;
-            if (blockIdx.x < active) {  // block-uniform: workgroups past `active` sit this one out
-                service_copy(sh, blockIdx.x, active);
-                service_gang_done(slot, box, v, active);
-            }
-            last = v;
-            __syncthreads();  // sh is rewritten by the next request
-        }
-        return;
-    }
-    unsigned long long expect = first_seq;
+    const bool lead = blockIdx.x == 0;
+    const unsigned long long *req =
+        lead ? reinterpret_cast<const unsigned long long *>(rq) : static_cast<const unsigned long long *>(box->rec);
+    unsigned long long last = first_seq - 1;  // requests carry strictly increasing seqs
     unsigned long long idle_start = __builtin_amdgcn_s_memrealtime();
-    unsigned long long ticks_sum = __hip_atomic_load(&slot->gpu_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const unsigned long long *req = reinterpret_cast<const unsigned long long *>(rq);
+    unsigned long long ticks_sum =
+        lead ? __hip_atomic_load(&slot->gpu_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
     for (;;) {
         if (tid < 64) {
-            // One wave reads the whole request record per poll (lanes 0..15).
-            // A record in this GPU's HBM is polled through its seq word alone
-            // (one lane, cheap local reads) and read whole once seq moved.
+            // One load instruction per poll: lanes 0..15 read the whole record
+            // (args, gang word, sum, seq); a seq whose hash checks out is whole.
             unsigned long long w = 0, s;
             for (;;) {
-                if (hbm_bell) {
-                    unsigned long long q = 0;
-                    if (tid == 0) q = __hip_atomic_load(req + 15, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    q = readlane64(q, 0);
-                    if (q != expect && q != kServiceStop) {
-                        if (__builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks) {
-                            s = kServiceStop;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                        continue;
-                    }
-                }
-                if (tid < 16) w = __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (tid < 16)
+                    w = lead ? __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                             : __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 s = readlane64(w, 15);
                 if (s == kServiceStop) break;
-                if (s == expect) {
+                if (s > last) {
                     unsigned long long h = service_mix(0, s);
 #pragma unroll
-                    for (int i = 0; i < kServiceArgWords; i++) h = service_mix(h, readlane64(w, i));
+                    for (int i = 0; i <= kServiceReqGang; i++) h = service_mix(h, readlane64(w, i));
                     if (h == readlane64(w, 14)) break;
-                    continue;  // seq landed before the args: read the record again
+                    continue;  // seq landed before the rest of the record: read it again
                 }
-                if (__builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks) {
+                if (lead && __builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks) {
                     s = kServiceStop;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(8);  // ~0.2 us between PCIe polls
+                if (lead)
+                    __builtin_amdgcn_s_sleep(8);  // ~0.2 us between PCIe polls
+                else
+                    __builtin_amdgcn_s_sleep(1);
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // order the data loads after the doorbell
-            if (tid < kServiceArgWords) sh[2 + tid] = w;  // args -> sh[2..]
+            if (lead && s != kServiceStop && (readlane64(w, kServiceReqGang) & 0xFFFFull) > 1 && tid < 16)
+                __hip_atomic_store(&box->rec[tid], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // relay, sc1
+            // Data loads are sc1 (ST_WT protocol): they bypass this CU's L1 and are
+            // not served from stale L2 copies of host or peer memory, so no acquire
+            // fence is needed; the plain protocol keeps the system-scope acquire.
+            if (!(proto & kServiceProtoWT)) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (tid <= kServiceReqGang) sh[tid == kServiceReqGang ? 1 : 2 + tid] = w;  // args -> sh[2..], gang -> sh[1]
             if (tid == 0) sh[0] = s;
         }
         __syncthreads();
         const unsigned long long s = sh[0];
         if (s == kServiceStop) break;
         const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
-        const uint64_t ntiles = service_tiles(*reinterpret_cast<const XferArgs *>(sh + 2));
-        if (gridDim.x > 1 && ntiles > solo_tiles) {
-            const unsigned long long active = ntiles < gridDim.x ? ntiles : gridDim.x;
-            if (tid < kServiceArgWords) box->args[tid] = sh[2 + tid];
-            if (tid == 0) {
-                __hip_atomic_store(&box->active, active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&box->cnt, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(&box->seq, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            service_copy(sh, 0, active);
-            service_gang_done(slot, box, s, active);  // gpu_ticks: until workgroup 0's share is out
-        } else {
-            service_copy(sh, 0, 1);
-            // Make the bytes visible to the host, other kernels and DMA (system scope).
-            block_release_system();
-            if (tid == 0) __hip_atomic_store(&slot->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        service_stamp(box, proto, 0);
+        service_serve(sh, s, slot, box, proto);
+        last = s;
         idle_start = __builtin_amdgcn_s_memrealtime();  // every lane: the idle test must stay wave-uniform
-        // Diagnostic, after `done` so it never delays it: a running sum in a
-        // register, published with a plain store (no PCIe atomic round trip).
-        ticks_sum += idle_start - t_seen;
-        if (tid == 0) __hip_atomic_store(&slot->gpu_ticks, ticks_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        expect++;
+        if (lead) {
+            // Diagnostic, after `done` so it never delays it: a running sum in a
+            // register, published with a plain store (no PCIe atomic round trip).
+            ticks_sum += idle_start - t_seen;
+            if (tid == 0) __hip_atomic_store(&slot->gpu_ticks, ticks_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         __syncthreads();  // sh is rewritten by the next poll
     }
-    if (tid == 0) {
-        __hip_atomic_store(&box->seq, kServiceStop, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&slot->exited, expect, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lead && tid == 0) {
+        // Every member leaves on this seq (a STOP in the relayed record).
+        __hip_atomic_store(&box->rec[15], kServiceStop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&slot->exited, last + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
 }  // namespace
 
-void service_post(ServiceReq *req, const XferArgs &a, unsigned long long seq) {
-    unsigned long long w[14] = {};
+uint32_t service_gang_size(const XferArgs &a, unsigned blocks, unsigned solo_tiles) {
+    const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
+    const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - (a.rem_off & ~tile_mask)) >> a.tile_shift;
+    if (blocks <= 1 || ntiles <= solo_tiles) return 1;
+    return (uint32_t)(ntiles < blocks ? ntiles : blocks);
+}
+
+void service_post(ServiceReq *req, const XferArgs &a, unsigned long long gang, unsigned long long seq) {
+    unsigned long long w[kServiceReqGang + 1] = {};
     std::memcpy(w, &a, sizeof(a));
-    unsigned long long h = service_mix(0, seq);
-    for (int i = 0; i < kServiceArgWords; i++) h = service_mix(h, w[i]);
-    // Line 0 (args 0..7) first and fenced, then line 1 (args 8..13, sum, seq):
-    // write-combining may flush a BAR-mapped record's lines in any order, and a
-    // poll that saw seq ahead of its args would fail the hash and cost another
-    // round trip. Host memory keeps x86 store order anyway.
+    w[kServiceReqGang] = gang;
+    const unsigned long long h = service_sum(seq, w);
+    // Line 0 (words 0..7) first and fenced, then line 1 (words 8..13, sum, seq):
+    // a poll that saw seq ahead of the rest fails the hash and reads again.
     for (int i = 0; i < 8; i++) __atomic_store_n(&req->args[i], w[i], __ATOMIC_RELAXED);
     __builtin_ia32_sfence();
-    for (int i = 8; i < 14; i++) __atomic_store_n(&req->args[i], w[i], __ATOMIC_RELAXED);
+    for (int i = 8; i <= kServiceReqGang; i++) __atomic_store_n(&req->args[i], w[i], __ATOMIC_RELAXED);
     __atomic_store_n(&req->sum, h, __ATOMIC_RELAXED);
     __atomic_store_n(&req->seq, seq, __ATOMIC_RELEASE);
-    __builtin_ia32_sfence();  // drain write-combining buffers now
+    __builtin_ia32_sfence();
 }
 
 void service_store_seq(ServiceReq *req, unsigned long long seq) {
@@ -625,13 +671,12 @@ void service_store_seq(ServiceReq *req, unsigned long long seq) {
 }
 
 hipError_t service_launch(ServiceReq *req, ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
-                          unsigned long long idle_ticks, unsigned blocks, unsigned solo_tiles, bool hbm_bell,
-                          hipStream_t stream) {
-    if (!req || !slot || !box || blocks == 0) return hipErrorInvalidValue;
+                          unsigned long long idle_ticks, unsigned blocks, unsigned proto, hipStream_t stream) {
+    if (!req || !slot || !box || blocks == 0 || first_seq == 0) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(box, 0, sizeof(ServiceBox), stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(service_kernel, dim3(blocks), dim3(kThreads), 0, stream, req, slot, box, first_seq, idle_ticks,
-                       solo_tiles, hbm_bell ? 1u : 0u);
+                       proto);
     return hipGetLastError();
 }
 // ---- verification patterns (benchmarks and tests check data without a host round trip) ----

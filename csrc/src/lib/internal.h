@@ -47,6 +47,7 @@ enum Loc { LOC_HOST = 0, LOC_PINNED = 1, LOC_DEVICE = 2 };
 constexpr uint64_t kServiceMaxDefault = 4ull << 20;
 constexpr int kServiceBlocksDefault = 32;
 constexpr int kServiceSoloTilesDefault = 2;
+constexpr unsigned kServiceProtoDefault = kServiceProtoWT;
 // Kernel-published completion of blocking launches (XferDone) up to this size.
 // Measured on HBM pairs (profiles/launch_flag_r01.json): 9.1-13.4 us against
 // 13.0-14.6 us with the runtime event up to 4 MiB; above that the per-workgroup
@@ -157,12 +158,13 @@ struct State {
     OpCounters ctr;
     // persistent copy service (small blocking one-sided ops)
     ServiceSlot *svc = nullptr;
-    ServiceReq *svc_req = nullptr;   // request record: BAR-mapped HBM, or &svc->req
-    bool svc_req_hbm = false;
+    ServiceReq *svc_req = nullptr;   // request record (&svc->req)
+    unsigned long long svc_gang_total = 0;  // gang completions this instance counts to (device counter mirror)
     ServiceBox *svc_box = nullptr;   // device-memory mailbox of the gang
     hipStream_t svc_stream = nullptr;
     unsigned svc_blocks = kServiceBlocksDefault;          // gang size (OCM_SERVICE_BLOCKS)
     unsigned svc_solo_tiles = kServiceSoloTilesDefault;  // requests of <= this many tiles stay on workgroup 0
+    unsigned svc_proto = kServiceProtoDefault;           // hand-off protocol bits (OCM_SERVICE_PROTO)
     bool svc_running = false;
     unsigned long long svc_seq = 0;
     uint64_t svc_ops = 0, svc_ns_post = 0, svc_ns_wait = 0;  // service diagnostics (ocm_x_service_stats)

@@ -14,6 +14,7 @@
 // (src/lib.c:461), NULL deref before check in ocm_free (:357-359), stub
 // copy_in/out (:491-499), swapped GPU->RMA offsets (:654).
 #include "internal.h"
+#include "ocm/affinity.h"
 #include "ocm/optim.h"
 
 using namespace ocm;
@@ -88,6 +89,15 @@ int ocm_init(void) {
             (void)hipGetLastError();
         }
     }
+    if (s.device >= 0) {
+        // This thread next to the GPU, on the L3 complex its daemon uses (ocm/affinity.h).
+        char bus[64] = {0};
+        DeviceGuard guard(s.device);
+        if (hipDeviceGetPCIBusId(bus, sizeof(bus), s.device) == hipSuccess)
+            (void)pin_near_gpu(bus, s.device, "libocm");
+        else
+            (void)hipGetLastError();
+    }
     s.sync_mode = env_int("OCM_SYNC_MODE", 1);
     s.n_lanes = env_int("OCM_ASYNC_LANES", 4);
     if (const char *k = std::getenv("OCM_PINNED_KEEP")) s.pinned_keep = std::strtoull(k, nullptr, 0);
@@ -95,6 +105,7 @@ int ocm_init(void) {
     s.svc_max = sm && *sm ? std::strtoull(sm, nullptr, 0) : kServiceMaxDefault;
     s.svc_blocks = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_BLOCKS", kServiceBlocksDefault), 1024));
     s.svc_solo_tiles = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES", kServiceSoloTilesDefault));
+    s.svc_proto = (unsigned)env_int("OCM_SERVICE_PROTO", (int)kServiceProtoDefault) & 31u;
     s.launch_flags = env_int("OCM_LAUNCH_FLAG", 1) != 0;
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");
     s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
@@ -741,7 +752,21 @@ void ocm_x_service_stats(uint64_t out[5]) {
     out[1] = s.svc_ns_post;
     out[2] = s.svc_ns_wait;
     out[3] = s.svc ? __atomic_load_n(&s.svc->gpu_ticks, __ATOMIC_ACQUIRE) : 0;
-    out[4] = s.svc_req_hbm ? 1 : 0;
+    out[4] = 0;  // doorbell: host memory (the BAR-mapped HBM record was measured slower and dropped)
+}
+
+// Copy-service phase stamps of the last request (OCM_SERVICE_PROTO with the
+// TRACE bit): 4 GPU-clock words per workgroup for the first n workgroups.
+int ocm_x_service_trace(uint64_t *out, int n_wgs) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!s.svc_box || n_wgs < 1 || n_wgs > kServiceTraceWgs) return -1;
+    DeviceGuard g(s.device);
+    if (hipMemcpy(out, s.svc_box->trace, (size_t)n_wgs * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return 0;
 }
 
 // Transfer tuning at runtime (benchmarks): variant 0 auto / 1 reg / 2 lds,

@@ -346,8 +346,13 @@ int alloc_local_half(lib_alloc *a, size_t bytes, Loc want) {
     if (want == LOC_DEVICE && local_pool()) {
         DeviceGuard g(s.device);
         hipError_t e = hipMallocFromPoolAsync(&a->local, bytes, s.pool, s.stream);
-        // The app may touch the buffer from any stream as soon as ocm_alloc returns.
-        if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+        // The app may touch the buffer from any stream as soon as ocm_alloc returns:
+        // the block's earlier user must be done. Blocking ops leave s.stream idle, so
+        // a query (no wait) settles it; otherwise wait for the stream.
+        if (e == hipSuccess) {
+            e = hipStreamQuery(s.stream);
+            if (e == hipErrorNotReady) e = hipStreamSynchronize(s.stream);
+        }
         if (e != hipSuccess) {
             (void)hipGetLastError();
             OCM_FAIL(-1, "pool allocation of %zu bytes for local half: %s", bytes, hipGetErrorString(e));

@@ -131,53 +131,6 @@ int sync_stream() {
 
 // ---- persistent copy service ----
 
-// True when [p, p + n) lies in one CPU mapping with write permission
-// (/proc/self/maps). Device memory the runtime did not map for the CPU is
-// either absent there or a PROT_NONE reservation.
-static bool cpu_writable(const void *p, size_t n) {
-    FILE *f = std::fopen("/proc/self/maps", "r");
-    if (!f) return false;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p), b = a + n;
-    char line[512];
-    bool ok = false;
-    while (std::fgets(line, sizeof(line), f)) {
-        unsigned long lo = 0, hi = 0;
-        char perms[8] = {};
-        if (std::sscanf(line, "%lx-%lx %7s", &lo, &hi, perms) != 3) continue;
-        if (a >= lo && b <= hi) {
-            ok = perms[0] == 'r' && perms[1] == 'w';
-            break;
-        }
-    }
-    std::fclose(f);
-    return ok;
-}
-
-// The copy service's request record: the host-pinned slot (default), or with
-// OCM_SERVICE_DOORBELL=hbm fine-grained HBM of this GPU that the CPU writes
-// through the BAR (if the runtime maps it for the CPU). A bare probe
-// (tools/vram_doorbell_probe.hip) round-trips 1.5 us faster with the HBM
-// record, but inside the library the host record measured 0.4-0.7 us faster
-// per 4 KiB op, same core, interleaved runs (profiles/svc_doorbell_r01.json).
-static void service_pick_doorbell(State &s) {
-    s.svc_req = &s.svc->req;
-    s.svc_req_hbm = false;
-    const char *mode = std::getenv("OCM_SERVICE_DOORBELL");
-    if (!mode || std::strcmp(mode, "hbm") != 0) return;
-    void *p = nullptr;
-    if (hipExtMallocWithFlags(&p, sizeof(ServiceReq), hipDeviceMallocFinegrained) != hipSuccess || !p) {
-        (void)hipGetLastError();
-        return;
-    }
-    if (!cpu_writable(p, sizeof(ServiceReq)) || hipMemset(p, 0, sizeof(ServiceReq)) != hipSuccess) {
-        (void)hipGetLastError();
-        (void)hipFree(p);
-        return;
-    }
-    s.svc_req = static_cast<ServiceReq *>(p);
-    s.svc_req_hbm = true;
-}
-
 int service_start(unsigned long long first_seq) {
     State &s = S();
     DeviceGuard g(s.device);
@@ -190,7 +143,7 @@ int service_start(unsigned long long first_seq) {
             OCM_FAIL(-1, "copy service: no coherent host memory");
         }
         std::memset(s.svc, 0, sizeof(ServiceSlot));
-        service_pick_doorbell(s);
+        s.svc_req = &s.svc->req;
         if (hipMalloc(reinterpret_cast<void **>(&s.svc_box), sizeof(ServiceBox)) != hipSuccess) {
             (void)hipGetLastError();
             s.svc_box = nullptr;
@@ -205,9 +158,9 @@ int service_start(unsigned long long first_seq) {
     }
     __atomic_store_n(&s.svc->exited, 0ull, __ATOMIC_RELEASE);
     service_store_seq(s.svc_req, 0ull);  // clear a STOP left by a parked instance
-    if (service_launch(s.svc_req, s.svc, s.svc_box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_solo_tiles, s.svc_req_hbm,
-                       s.svc_stream) !=
-        hipSuccess) {
+    s.svc_gang_total = 0;  // the launch zeroes the device counter
+    if (service_launch(s.svc_req, s.svc, s.svc_box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_proto,
+                       s.svc_stream) != hipSuccess) {
         (void)hipGetLastError();
         s.svc_max = 0;
         OCM_FAIL(-1, "copy service launch failed");
@@ -237,9 +190,7 @@ void service_stop() {
         s.svc_running = false;
     }
     (void)hipStreamDestroy(s.svc_stream);
-    if (s.svc_req_hbm) (void)hipFree(s.svc_req);
     s.svc_req = nullptr;
-    s.svc_req_hbm = false;
     (void)hipHostFree(s.svc);
     if (s.svc_box) (void)hipFree(s.svc_box);
     s.svc = nullptr;
@@ -253,8 +204,19 @@ int service_xfer(XferArgs x) {
     if (xfer_normalize(x) != hipSuccess) OCM_FAIL(-1, "invalid transfer");
     const unsigned long long seq = ++s.svc_seq;
     if (!s.svc_running && service_start(seq) != 0) return -1;
+    // The host sizes the gang and the completion count every workgroup agrees on.
+    const unsigned long long active = service_gang_size(x, s.svc_blocks, s.svc_solo_tiles);
+    auto gang_word = [&]() {
+        unsigned long long target = 0;
+        if (active > 1) {
+            s.svc_gang_total += active;
+            target = s.svc_gang_total;
+        }
+        return active | (target << 16);
+    };
+    unsigned long long gang = gang_word();
     const uint64_t t0 = now_ns();
-    service_post(s.svc_req, x, seq);
+    service_post(s.svc_req, x, gang, seq);
     const uint64_t t_posted = now_ns();
     for (unsigned spins = 1;; spins++) {
         if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) {
@@ -273,7 +235,8 @@ int service_xfer(XferArgs x) {
                 s.svc_running = false;
                 if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
                 if (service_start(seq) != 0) return -1;
-                service_post(s.svc_req, x, seq);  // start cleared the doorbell: re-post
+                gang = gang_word();              // counted afresh by the new instance
+                service_post(s.svc_req, x, gang, seq);  // start cleared the doorbell: re-post
             }
             if (now_ns() - t0 > 10ull * 1000000000ull) OCM_FAIL(-1, "copy service did not complete a transfer in 10 s");
         }

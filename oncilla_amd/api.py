@@ -174,6 +174,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
             "ocm_x_service_stats": (None, [ctypes.POINTER(u64)]),
+            "ocm_x_service_trace": (i32, [ctypes.POINTER(u64), i32]),
             "ocm_x_adam": (i32, [vp, vp, vp, u64, u64, u64, ctypes.POINTER(ctypes.c_float), vp]),
             "ocm_x_adam_multi": (i32, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(u64),
                                        ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64),
@@ -311,6 +312,21 @@ def service_stats() -> dict:
     n = int(out[0])
     return {"ops": n, "post_us": out[1] / n / 1e3 if n else None, "wait_us": out[2] / n / 1e3 if n else None,
             "gpu_us": out[3] / 100.0 / n if n else None, "doorbell": "hbm" if out[4] else "host"}
+
+
+def service_trace(n_wgs: int = 32) -> list:
+    """Copy-service phase stamps of the last request, per workgroup (needs the TRACE bit,
+    16, in OCM_SERVICE_PROTO): microseconds of [seen, copy start, drained, counted/done]
+    relative to workgroup 0's doorbell-seen stamp; None for a workgroup that never stamped."""
+    out = (ctypes.c_uint64 * (4 * n_wgs))()
+    if load().ocm_x_service_trace(out, n_wgs) != 0:
+        raise OcmError("ocm_x_service_trace: no copy service running")
+    t0 = out[0]
+    rows = []
+    for w in range(n_wgs):
+        r = out[4 * w:4 * w + 4]
+        rows.append(None if r[0] == 0 else [round((x - t0) / 100.0, 2) if x else None for x in r])
+    return rows
 
 
 def layout() -> dict:

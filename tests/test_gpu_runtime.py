@@ -423,15 +423,13 @@ def test_host_tier_prefers_the_gpus_numa_node(mesh_factory):
         a.free()
 
 
-@pytest.mark.parametrize("doorbell", ["host", "hbm"])
-def test_copy_service_doorbell_placement(mesh_factory, monkeypatch, doorbell):
-    """Small blocking ops with the service's request record in host memory
-    (default) or in BAR-mapped HBM (opt-in): data verified, and the library's
-    service diagnostics count every op and say where the record lives."""
-    if doorbell == "hbm":
-        monkeypatch.setenv("OCM_SERVICE_DOORBELL", "hbm")
-    else:
-        monkeypatch.delenv("OCM_SERVICE_DOORBELL", raising=False)
+@pytest.mark.parametrize("proto", ["1", "0"])
+def test_copy_service_protocols(mesh_factory, monkeypatch, proto):
+    """Small blocking ops through the service with the write-through hand-off
+    (default, OCM_SERVICE_PROTO=1) and the fenced one (0), unaligned sizes and
+    offsets included: data verified, and the library's service diagnostics
+    count every op."""
+    monkeypatch.setenv("OCM_SERVICE_PROTO", proto)
     m = mesh_factory(2, gpus=[0, 0])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         n = 1 << 20
@@ -445,7 +443,7 @@ def test_copy_service_doorbell_placement(mesh_factory, monkeypatch, doorbell):
             assert a.check(seed=40 + i, offset=off, nbytes=size - size % 4, first_word=off // 4) == 0, (size, off)
         st = api.service_stats()
         assert st["ops"] - before == 8, st
-        assert st["doorbell"] == doorbell, st
+        assert st["doorbell"] == "host", st
         assert st["gpu_us"] is not None and 0 < st["gpu_us"] < 1000, st
         a.free()
 

@@ -1,0 +1,81 @@
+"""The resident copy service under adversarial reuse (MI355X).
+
+The service runs in one persistent kernel and, with the default write-through
+protocol, issues no acquire fence per request: its loads are sc1 (they bypass
+the CU's L1 and are not served from stale L2 copies of host or peer memory) and
+its stores are sc1 + drained. These tests try to make it read stale bytes:
+torch kernels on every XCD rewrite both halves of a pair between one-sided
+ops, read them in between (warming caches with old data), and the remote half
+is rewritten behind the library's back through its direct mapping. Every word
+is checked on the device. Sizes cover the solo path (one workgroup) and the
+gang (up to 32 workgroups).
+"""
+import time
+
+import pytest
+import torch
+
+from oncilla_amd import api
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [4096, 12288, 65536 + 4096, 256 << 10, (1 << 20) + 512]
+
+
+def _pairs(c):
+    n = 4 << 20
+    return [("hbm", c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_LOOPBACK)),
+            ("host", c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_HOST_TIER))]
+
+
+@pytest.mark.parametrize("rounds", [24])
+def test_service_never_reads_stale_bytes(mesh_factory, rounds):
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        for tier, a in _pairs(c):
+            loc = a.local_tensor(torch.int32)
+            rem = a.remote_tensor(torch.int32)
+            g = torch.Generator(device="cuda:0")
+            for r in range(rounds):
+                for n in SIZES:
+                    words = n // 4
+                    off = 4096 if r % 2 else 0  # aligned and tile-straddling offsets
+                    w0 = off // 4
+                    g.manual_seed(1000 * r + n)
+                    want = torch.randint(-2**31, 2**31 - 1, (words,), device="cuda:0", dtype=torch.int32, generator=g)
+                    # PUT: the local half is rewritten by a torch kernel after a read of the old bytes
+                    _ = loc[w0:w0 + words].sum()
+                    loc[w0:w0 + words].copy_(want)
+                    torch.cuda.synchronize()
+                    a.put(off, off, n)
+                    got = rem[w0:w0 + words].clone()
+                    torch.cuda.synchronize()
+                    assert torch.equal(got, want), f"{tier} put {n} B round {r}: remote half stale"
+                    # GET: the remote half is rewritten behind the library (its direct mapping)
+                    want2 = torch.bitwise_not(want)
+                    rem[w0:w0 + words].copy_(want2)
+                    loc[w0:w0 + words].zero_()
+                    torch.cuda.synchronize()
+                    a.get(off, off, n)
+                    assert torch.equal(loc[w0:w0 + words], want2), f"{tier} get {n} B round {r}: local half stale"
+            a.free()
+
+
+def test_service_restarts_after_idle_exit(mesh_factory):
+    # The service leaves after 2 ms without work (workgroup 0 stores STOP for the
+    # gang); the next op relaunches it. Alternate gang-sized and solo ops across exits.
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 1 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_LOOPBACK)
+        for i in range(12):
+            size = n if i % 2 else 8192
+            a.fill(seed=50 + i, nbytes=size)
+            a.put(0, 0, size)
+            a.fill(seed=0, nbytes=size)
+            a.get(0, 0, size)
+            assert a.check(seed=50 + i, nbytes=size) == 0, f"op pair {i}"
+            time.sleep(0.005)
+        ops = api.service_stats()["ops"]
+        assert ops >= 24
+        a.free()

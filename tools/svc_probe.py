@@ -23,13 +23,17 @@ sys.path.insert(0, REPO)
 
 SIZES = [4096 << i for i in range(15)]  # 4 KiB .. 64 MiB
 CONFIGS = {"launch": {"OCM_SERVICE_MAX": "0"}, "launch_event": {"OCM_SERVICE_MAX": "0", "OCM_LAUNCH_FLAG": "0"}}
-# library defaults; the same with the request record in BAR-mapped HBM instead of host memory;
-# roctx ranges forced on
+# library defaults; roctx ranges forced on; a one-workgroup service
 CONFIGS["default"] = {}
-CONFIGS["default_hbmbell"] = {"OCM_SERVICE_DOORBELL": "hbm"}
 CONFIGS["default_roctx"] = {"OCM_TRACE": "1"}
 CONFIGS["g1"] = {"OCM_SERVICE_BLOCKS": "1"}
-CONFIGS["g1_hbmbell"] = {"OCM_SERVICE_BLOCKS": "1", "OCM_SERVICE_DOORBELL": "hbm"}
+# copy-service hand-off protocols (OCM_SERVICE_PROTO bits: 1 write-through data (sc1 loads and
+# stores, drained, no fences) vs 0 fenced; 16 adds per-workgroup phase stamps, reported as trace_*)
+CONFIGS["proto0"] = {"OCM_SERVICE_PROTO": "0"}
+CONFIGS["trace"] = {"OCM_SERVICE_PROTO": "17"}
+# requests of <= N tiles stay on workgroup 0
+for n in (0, 1, 2, 4, 8):
+    CONFIGS[f"solo{n}"] = {"OCM_SERVICE_SOLO_TILES": str(n)}
 for g in (1, 16, 32, 64, 128, 256):
     CONFIGS[f"svc_g{g}"] = {"OCM_SERVICE_MAX": str(64 << 20), "OCM_SERVICE_BLOCKS": str(g)}
 
@@ -63,19 +67,24 @@ def child(tier: str, cpu: int | None = None) -> None:
                 put = min(a.time_onesided(1, s, it) for _ in range(3))
                 get = min(a.time_onesided(0, s, it) for _ in range(3))
                 out[str(s)] = {"put_us": round(put * 1e6, 2), "get_us": round(get * 1e6, 2)}
-            # where a 4 KiB blocking put spends its time (library diagnostics, deltas over 2000 ops)
-            b0 = api.service_stats()
-            t = a.time_onesided(1, 4096, 2000)
-            b1 = api.service_stats()
-            if b1["ops"] > b0["ops"]:
-                k = b1["ops"] - b0["ops"]
+            # where a blocking op spends its time (library diagnostics, deltas over N ops):
+            # host post, host wait, GPU doorbell-seen -> done
+            for op, s in ((1, 4096), (0, 4096), (0, 16384), (1, 16384), (0, 65536), (0, 262144), (1, 262144),
+                          (0, 1 << 20), (1, 1 << 20)):
+                b0 = api.service_stats()
+                t = a.time_onesided(op, s, 500, 4096, 4096)
+                b1 = api.service_stats()
+                if b1["ops"] > b0["ops"]:
+                    k = b1["ops"] - b0["ops"]
 
-                def mean(key):
-                    return round((b1[key] * b1["ops"] - (b0[key] or 0) * b0["ops"]) / k, 3)
+                    def mean(key):
+                        return round((b1[key] * b1["ops"] - (b0[key] or 0) * b0["ops"]) / k, 3)
 
-                out["breakdown_4k_put"] = {"call_us": round(t * 1e6, 3), "post_us": mean("post_us"),
-                                           "wait_us": mean("wait_us"), "gpu_us": mean("gpu_us"),
-                                           "doorbell": b1["doorbell"]}
+                    out[f"breakdown_{s // 1024}k_{'put' if op else 'get'}"] = {
+                        "call_us": round(t * 1e6, 3), "post_us": mean("post_us"), "wait_us": mean("wait_us"),
+                        "gpu_us": mean("gpu_us"), "doorbell": b1["doorbell"]}
+                    if int(os.environ.get("OCM_SERVICE_PROTO", "0")) & 16:
+                        out[f"trace_{s // 1024}k_{'put' if op else 'get'}"] = [r for r in api.service_trace(32) if r]
             a.free()
     print(json.dumps(out))
 
