@@ -7,7 +7,7 @@
 // cache line moves between them in tens of ns instead of hundreds. The daemon
 // of GPU g and the apps that copy on GPU g both restrict themselves to the
 // same CCD of g's NUMA node (chosen by g's ordinal, so the GPUs of one node get
-// different CCDs); OCM_PIN=0 turns it off. No reference counterpart: the
+// different CCDs), the daemon to a core of its own; OCM_PIN=0 turns it off. No reference counterpart: the
 // reference's daemon and apps ran wherever the scheduler put them.
 #pragma once
 #include <string>
@@ -26,8 +26,14 @@ std::vector<int> ccd_cpus(int node, int slot);
 // Returns the number of CPUs it may now run on (0: unchanged, nothing in common).
 int pin_thread(const std::vector<int> &cpus);
 
-// pci_numa_node + ccd_cpus + pin_thread unless OCM_PIN=0; returns the CPUs pinned to
-// (empty: not pinned) and logs the choice under OCM_VERBOSE.
-std::vector<int> pin_near_gpu(const std::string &bus_id, int gpu_ordinal, const char *who);
+// Hardware threads sharing `cpu`'s core (itself included).
+std::vector<int> core_siblings(int cpu);
+
+// Unless OCM_PIN=0: the event loop of daemon `daemon_rank` on one core of the
+// GPU's L3 complex (one hardware thread; core = rank modulo the complex's
+// cores), an app thread of that daemon on the complex's other cores.
+// Returns the CPUs pinned to (empty: not pinned); logs the choice under OCM_VERBOSE.
+enum class PinRole { Daemon, App };
+std::vector<int> pin_near_gpu(const std::string &bus_id, int gpu_ordinal, PinRole role, int daemon_rank);
 
 }  // namespace ocm

@@ -92,15 +92,46 @@ int pin_thread(const std::vector<int> &cpus) {
     return n;
 }
 
-std::vector<int> pin_near_gpu(const std::string &bus_id, int gpu_ordinal, const char *who) {
+std::vector<int> core_siblings(int cpu) {
+    std::string list;
+    if (!read_line("/sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/topology/thread_siblings_list", &list))
+        return {cpu};
+    return parse_cpulist(list);
+}
+
+std::vector<int> pin_near_gpu(const std::string &bus_id, int gpu_ordinal, PinRole role, int daemon_rank) {
     const char *e = std::getenv("OCM_PIN");
     if (e && std::strcmp(e, "0") == 0) return {};
+    const bool whole_ccd = e && std::strcmp(e, "ccd") == 0;  // everyone on the whole complex
     const int node = pci_numa_node(bus_id);
-    std::vector<int> cpus = ccd_cpus(node, gpu_ordinal);
-    const int n = cpus.empty() ? 0 : pin_thread(cpus);
+    std::vector<int> ccd = ccd_cpus(node, gpu_ordinal);
+    if (ccd.empty()) return {};
+    // Physical cores of the complex (the first hardware thread of each).
+    std::vector<int> cores;
+    for (int c : ccd) {
+        const std::vector<int> sib = core_siblings(c);
+        if (!sib.empty() && *std::min_element(sib.begin(), sib.end()) == c) cores.push_back(c);
+    }
+    if (cores.empty()) cores = ccd;
+    // The daemon's event loop gets a core of the complex to itself (one hardware
+    // thread; several daemons of one GPU take successive cores by rank); its apps
+    // get every other core, so none shares a core or its SMT sibling with it.
+    const int dcore = cores[(size_t)(daemon_rank < 0 ? 0 : daemon_rank) % cores.size()];
+    const std::vector<int> dsib = core_siblings(dcore);
+    std::vector<int> cpus;
+    if (whole_ccd) {
+        cpus = ccd;
+    } else if (role == PinRole::Daemon) {
+        cpus.push_back(dcore);
+    } else {
+        for (int c : ccd)
+            if (std::find(dsib.begin(), dsib.end(), c) == dsib.end()) cpus.push_back(c);
+        if (cpus.empty()) cpus = ccd;
+    }
+    const int n = pin_thread(cpus);
     if (n == 0) return {};
-    OCM_LOG("%s: pinned to %d CPUs of the L3 complex at CPU %d (NUMA node %d of GPU %s)", who, n, cpus.front(), node,
-            bus_id.c_str());
+    OCM_LOG("%s: pinned to %d CPU(s) from %d, L3 complex at CPU %d (NUMA node %d of GPU %s), daemon core %d",
+            role == PinRole::Daemon ? "ocmd" : "libocm", n, cpus.front(), ccd.front(), node, bus_id.c_str(), dcore);
     return cpus;
 }
 

@@ -155,7 +155,7 @@ int Daemon::init() {
         // the data server's threads (started above) keep the full mask.
         char bus[64] = {0};
         if (hipDeviceGetPCIBusId(bus, sizeof(bus), gpu_) == hipSuccess)
-            pinned_cpus_ = pin_near_gpu(bus, gpu_, "ocmd").size();
+            pinned_cpus_ = pin_near_gpu(bus, gpu_, PinRole::Daemon, rank_).size();
         else
             (void)hipGetLastError();
     }

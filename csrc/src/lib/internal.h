@@ -190,6 +190,12 @@ struct State {
     uint64_t launch_flag_max = kLaunchFlagMaxDefault;  // OCM_LAUNCH_FLAG_MAX
     bool pool_tried = false;
     uint64_t pool_keep = 8ull << 30;       // bytes kept reserved across frees
+    // Freed pool blocks kept for an exact-size reuse (OCM_LOCAL_CACHE bytes, 0 = off):
+    // a reuse needs no HIP call at all, where a pool allocation right after a
+    // stream-ordered free must wait for that free on the stream.
+    std::multimap<size_t, void *> dev_cache;
+    uint64_t dev_cache_bytes = 0;
+    uint64_t dev_cache_cap = 1ull << 30;
     hipEvent_t done = nullptr;
     int rpc_timeout_ms = 60000;
     uint64_t rpc_spin_ns = 50000;          // OCM_RPC_SPIN_US: poll for a reply this long before sleeping
@@ -257,6 +263,7 @@ private:
 
 // ---- local halves (runtime.cpp)
 Loc pointer_loc(const void *p);
+void release_dev_cache();
 hipMemPool_t local_pool();
 int free_local_half(lib_alloc *a);
 int alloc_local_half(lib_alloc *a, size_t bytes, Loc want);

@@ -94,13 +94,14 @@ int ocm_init(void) {
         char bus[64] = {0};
         DeviceGuard guard(s.device);
         if (hipDeviceGetPCIBusId(bus, sizeof(bus), s.device) == hipSuccess)
-            (void)pin_near_gpu(bus, s.device, "libocm");
+            (void)pin_near_gpu(bus, s.device, PinRole::App, s.daemon_rank);
         else
             (void)hipGetLastError();
     }
     s.sync_mode = env_int("OCM_SYNC_MODE", 1);
     s.n_lanes = env_int("OCM_ASYNC_LANES", 4);
     if (const char *k = std::getenv("OCM_PINNED_KEEP")) s.pinned_keep = std::strtoull(k, nullptr, 0);
+    if (const char *k = std::getenv("OCM_LOCAL_CACHE")) s.dev_cache_cap = std::strtoull(k, nullptr, 0);
     const char *sm = std::getenv("OCM_SERVICE_MAX");
     s.svc_max = sm && *sm ? std::strtoull(sm, nullptr, 0) : kServiceMaxDefault;
     s.svc_blocks = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_BLOCKS", kServiceBlocksDefault), 1024));
@@ -153,6 +154,7 @@ int ocm_tini(void) {
         s.lane_cnt = nullptr;
         s.lane_flag_seq.clear();
     }
+    release_dev_cache();
     if (s.stream) {
         DeviceGuard g(s.device);
         (void)hipStreamSynchronize(s.stream);

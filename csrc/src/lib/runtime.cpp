@@ -319,9 +319,17 @@ int free_local_half(lib_alloc *a) {
     State &s = S();
     if (!a->local) return 0;
     if (a->pooled) {
-        DeviceGuard g(s.device);
-        // Ordered after every transfer queued on s.stream; the block returns to the pool.
-        if (hipFreeAsync(a->local, s.stream) != hipSuccess) (void)hipGetLastError();
+        // The library's own ops on the block are done (ocm_free waited for them):
+        // keep it for an exact-size reuse, or return it to the pool, ordered after
+        // every transfer queued on s.stream.
+        const uint64_t kMaxCachedBlock = 256ull << 20;
+        if (a->local_bytes <= kMaxCachedBlock && s.dev_cache_bytes + a->local_bytes <= s.dev_cache_cap) {
+            s.dev_cache.emplace(a->local_bytes, a->local);
+            s.dev_cache_bytes += a->local_bytes;
+        } else {
+            DeviceGuard g(s.device);
+            if (hipFreeAsync(a->local, s.stream) != hipSuccess) (void)hipGetLastError();
+        }
         a->pooled = false;
     } else if (a->loc == LOC_DEVICE) {
         DeviceGuard g(s.device);
@@ -338,12 +346,33 @@ int free_local_half(lib_alloc *a) {
     return 0;
 }
 
+// Return every cached block to the pool (ocm_tini, before the pool goes).
+void release_dev_cache() {
+    State &s = S();
+    if (s.dev_cache.empty()) return;
+    DeviceGuard g(s.device);
+    for (auto &kv : s.dev_cache)
+        if (hipFreeAsync(kv.second, s.stream) != hipSuccess) (void)hipGetLastError();
+    s.dev_cache.clear();
+    s.dev_cache_bytes = 0;
+    (void)hipStreamSynchronize(s.stream);
+}
+
 int alloc_local_half(lib_alloc *a, size_t bytes, Loc want) {
     State &s = S();
     a->local_bytes = bytes;
     if (bytes == 0) return 0;
     if (want != LOC_HOST && s.device < 0) want = LOC_HOST;
     if (want == LOC_DEVICE && local_pool()) {
+        auto hit = s.dev_cache.find(bytes);
+        if (hit != s.dev_cache.end()) {
+            a->local = hit->second;
+            s.dev_cache_bytes -= bytes;
+            s.dev_cache.erase(hit);
+            a->pooled = true;
+            a->loc = want;
+            return 0;
+        }
         DeviceGuard g(s.device);
         hipError_t e = hipMallocFromPoolAsync(&a->local, bytes, s.pool, s.stream);
         // The app may touch the buffer from any stream as soon as ocm_alloc returns:
