@@ -311,7 +311,9 @@ def main() -> int:
         # ---- daemon mesh: one ocmd per rank / GPU ----
         # rank 0 picks every daemon port while holding them all bound, so no two
         # ranks of this node can be handed the same ephemeral port
-        ports = gather_obj(dist, free_ports(world) if rank == 0 else None, world)[0]
+        import secrets
+
+        ports, mesh_key = gather_obj(dist, (free_ports(world), secrets.token_hex(16)) if rank == 0 else None, world)[0]
         ns = f"bench{os.environ.get('MASTER_PORT', '0')}_{ports[0]}"
         workdir = os.path.join("/tmp", f"ocm_{ns}")
         os.makedirs(workdir, exist_ok=True)
@@ -328,7 +330,7 @@ def main() -> int:
             fr, spec = bf.split(":", 1)
             rank_env[int(fr)] = {"OCM_FAULT": spec}
         mesh = Mesh(world, gpus=gpus, ns=ns, policy=policy, workdir=workdir, ports=ports, ranks=[rank],
-                    rank_env=rank_env)
+                    rank_env=rank_env, key=mesh_key)
         ph.run("mesh_start", lambda: mesh.start(timeout=120))
 
         def attach():

@@ -129,6 +129,7 @@ private:
         uint16_t flags = 0;
         uint16_t n_extents = 1;
         uint64_t stripe_unit = 0;
+        uint64_t grant = 0;        // network tier: the data-server capability of this extent
     };
 
     int init();
@@ -169,6 +170,7 @@ private:
     void r0_place_fail(Msg &m);
     void owner_do_alloc(Msg &m);
     void owner_do_free(Msg &m);
+    int free_owned(const OwnedExtent &oe);
     void origin_do_alloc_resp(Msg &m);
     void origin_do_free_resp(Msg &m);
     void finish_alloc(Pending &p);

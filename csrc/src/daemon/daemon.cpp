@@ -165,6 +165,26 @@ int Daemon::init() {
         if (!boot_id_) boot_id_ = ((uint64_t)getpid() << 32) ^ (uint64_t)now_ms();
     }
     {
+        const std::string bind = cfg_.bind_ip.empty() ? "0.0.0.0" : cfg_.bind_ip;
+        const bool loopback = bind.compare(0, 4, "127.") == 0 || bind == "::1" || bind == "localhost";
+        if (cfg_.mesh_key.empty() && n_ == 1) {
+            // No peer has to agree on it: a random secret keeps the port closed.
+            uint64_t k = 0;
+            std::ifstream ur("/dev/urandom", std::ios::binary);
+            ur.read(reinterpret_cast<char *>(&k), sizeof(k));
+            char hex[17];
+            std::snprintf(hex, sizeof(hex), "%016llx", (unsigned long long)(k ^ boot_id_));
+            cfg_.mesh_key = hex;
+        } else if (cfg_.mesh_key.empty() && !loopback) {
+            const char *insecure = std::getenv("OCM_MESH_INSECURE");
+            if (!insecure || std::strcmp(insecure, "1") != 0) {
+                OCM_ERR("rank %d: the mesh port binds %s but OCM_MESH_KEY is not set: anyone reaching it could "
+                        "free or allocate memory. Set the same OCM_MESH_KEY on every daemon (or OCM_MESH_INSECURE=1 "
+                        "on a trusted network)", rank_, bind.c_str());
+                return -1;
+            }
+            OCM_WARN("rank %d: UNAUTHENTICATED mesh on %s (OCM_MESH_INSECURE=1, no OCM_MESH_KEY)", rank_, bind.c_str());
+        }
         // FNV-1a over namespace + shared key: strangers on the mesh port cannot join.
         uint64_t h = 1469598103934665603ull;
         for (char ch : ns_ + '\x1f' + cfg_.mesh_key) h = (h ^ (uint8_t)ch) * 1099511628211ull;

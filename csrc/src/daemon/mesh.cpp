@@ -288,6 +288,7 @@ void Daemon::owner_do_alloc(Msg &m) {
         return;
     }
     rg.owner_rank = rank_;
+    uint64_t grant = 0;
     if (rg.flags & REGION_NET) {
         if (!data_) {
             arena_->free(rg.slab_id, rg.offset);
@@ -299,13 +300,26 @@ void Daemon::owner_do_alloc(Msg &m) {
             send_rank(0, f);
             return;
         }
-        // Other node: the app streams through our data server instead of mapping the slab.
-        std::memset(rg.handle, 0, sizeof(rg.handle));
-        std::snprintf(reinterpret_cast<char *>(rg.handle), sizeof(rg.handle), "net:%s:%d:%llx",
-                      nf_.nodes[rank_].ip.c_str(), data_->port(), (unsigned long long)data_token_);
+        // Other node: the app streams through our data server instead of mapping the
+        // slab, with a capability for this extent alone.
+        grant = data_->grant(rg.slab_id, rg.offset, rg.bytes);
+        if (!format_net_handle(rg.handle, nf_.nodes[rank_].ip, data_->port(), data_token_, grant)) {
+            OCM_ERR("rank %d: net handle for %s does not fit %zu bytes", rank_, nf_.nodes[rank_].ip.c_str(),
+                    kHandleBytes);
+            data_->revoke(grant);
+            arena_->free(rg.slab_id, rg.offset);
+            Msg f = m;
+            f.type = MSG_PLACE_FAIL;
+            f.status = MSG_REQUEST;
+            f.err = ENAMETOOLONG;
+            f.u.region.owner_rank = rank_;
+            send_rank(0, f);
+            return;
+        }
         rg.flags = (uint16_t)(rg.flags & ~REGION_DEDICATED);
     }
     OwnedExtent oe;
+    oe.grant = grant;
     oe.slab_id = rg.slab_id;
     oe.offset = rg.offset;
     oe.tier = rg.tier;
@@ -324,12 +338,19 @@ void Daemon::owner_do_alloc(Msg &m) {
     send_rank(m.rank, r);
 }
 
+// Give an owned extent back to the arena. A network-tier extent first loses its
+// grant; when a data-server request is still copying it, that request frees it.
+int Daemon::free_owned(const OwnedExtent &oe) {
+    if (oe.grant && data_ && !data_->revoke(oe.grant)) return 0;
+    return arena_->free(oe.slab_id, oe.offset);
+}
+
 void Daemon::owner_do_free(Msg &m) {
     const Region &rg = m.u.region;
     auto it = owned_.find({rg.alloc_id, (int)rg.extent_idx});
     int err = ENOENT;
     if (it != owned_.end()) {
-        err = arena_->free(it->second.slab_id, it->second.offset);
+        err = free_owned(it->second);
         owned_.erase(it);
     }
     Msg r = m;
@@ -630,7 +651,7 @@ void Daemon::peer_lost(int rank) {
     for (auto &kv : owned_)
         if (kv.second.orig_rank == rank) orphan.push_back(kv.first);
     for (auto &k : orphan) {
-        arena_->free(owned_[k].slab_id, owned_[k].offset);
+        free_owned(owned_[k]);
         owned_.erase(k);
         n_reclaimed_++;
     }

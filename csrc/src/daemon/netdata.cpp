@@ -9,6 +9,7 @@
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
+#include <random>
 
 #include "ocm/arena.h"
 #include "ocm/log.h"
@@ -44,19 +45,6 @@ inline void hb_release([[maybe_unused]] void *tok) {
 #endif
 }
 }  // namespace
-
-bool parse_net_handle(const uint8_t *handle, std::string *ip, int *port, uint64_t *token) {
-    char buf[65] = {0};
-    std::memcpy(buf, handle, 64);
-    char host[64] = {0};
-    int p = 0;
-    unsigned long long t = 0;
-    if (std::sscanf(buf, "net:%63[^:]:%d:%llx", host, &p, &t) != 3 || p <= 0) return false;
-    *ip = host;
-    *port = p;
-    *token = t;
-    return true;
-}
 
 DataServer::DataServer(Arena *arena, int gpu, uint64_t token) : arena_(arena), gpu_(gpu), token_(token) {}
 
@@ -124,6 +112,71 @@ void DataServer::reap() {
     }
 }
 
+uint64_t DataServer::grant(uint32_t slab_id, uint64_t offset, uint64_t bytes) {
+    static thread_local std::mt19937_64 rng(std::random_device{}() ^ ((uint64_t)std::random_device{}() << 32));
+    std::lock_guard<std::mutex> lk(mu_);
+    uint64_t g = 0;
+    while (g == 0 || grants_.count(g)) g = rng();
+    Grant &e = grants_[g];
+    e.slab_id = slab_id;
+    e.offset = offset;
+    e.bytes = bytes;
+    return g;
+}
+
+bool DataServer::revoke(uint64_t g) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = grants_.find(g);
+    if (it == grants_.end()) return true;
+    if (it->second.busy > 0) {
+        it->second.revoked = true;  // release() frees the extent
+        return false;
+    }
+    grants_.erase(it);
+    return true;
+}
+
+size_t DataServer::grants() const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return grants_.size();
+}
+
+bool DataServer::acquire(const NetReq &q, void **mem, uint32_t *tier, int *err) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = grants_.find(q.grant);
+    if (it == grants_.end() || it->second.revoked) {
+        *err = EACCES;
+        return false;
+    }
+    Grant &g = it->second;
+    if (q.offset > g.bytes || q.len > g.bytes - q.offset) {
+        *err = EFAULT;
+        return false;
+    }
+    // The extent cannot be freed while busy > 0, so its slab stays mapped.
+    if (!arena_->locate(g.slab_id, g.offset + q.offset, q.len, mem, tier)) {
+        *err = EFAULT;
+        return false;
+    }
+    g.busy++;
+    return true;
+}
+
+void DataServer::release(uint64_t g) {
+    uint32_t slab = 0;
+    uint64_t off = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = grants_.find(g);
+        if (it == grants_.end()) return;
+        if (--it->second.busy > 0 || !it->second.revoked) return;
+        slab = it->second.slab_id;
+        off = it->second.offset;
+        grants_.erase(it);
+    }
+    arena_->free(slab, off);  // the owner freed it while we were copying
+}
+
 void DataServer::serve(int fd) {
     void *stage = nullptr;
     if (gpu_ >= 0) {
@@ -141,16 +194,19 @@ void DataServer::serve(int fd) {
     while (authed && !stop_ && recv_all(fd, &q, sizeof(q)) == 1) {
         NetResp r{kNetMagic, 0, q.len};
         if (q.magic != kNetMagic) break;
-        hb_acquire(&token_);
-        void *mem = nullptr;
-        uint32_t tier = 0;
         if (q.op == NET_PING) {
             r.len = 0;
             if (send_all(fd, &r, sizeof(r)) != 1) break;
             continue;
         }
-        if (!arena_->locate(q.slab_id, q.offset, q.len, &mem, &tier)) r.err = EFAULT;
-        if (tier == TIER_GPU && !stage) r.err = r.err ? r.err : ENOMEM;
+        if (q.op != NET_PUT && q.op != NET_GET) break;
+        hb_acquire(&token_);
+        void *mem = nullptr;
+        uint32_t tier = 0;
+        int err = 0;
+        const bool held = acquire(q, &mem, &tier, &err);
+        if (!held) r.err = err;
+        if (held && tier == TIER_GPU && !stage) r.err = ENOMEM;
         bool ok = true;
         if (q.op == NET_PUT) {
             for (uint64_t done = 0; ok && done < q.len;) {
@@ -167,10 +223,11 @@ void DataServer::serve(int fd) {
                 done += n;
             }
             hb_release(&token_);
+            if (held) release(q.grant);
             if (!ok || send_all(fd, &r, sizeof(r)) != 1) break;
-        } else if (q.op == NET_GET) {
+        } else {
             if (r.err) r.len = 0;
-            if (send_all(fd, &r, sizeof(r)) != 1) break;
+            ok = send_all(fd, &r, sizeof(r)) == 1;
             for (uint64_t done = 0; ok && !r.err && done < q.len;) {
                 const size_t n = (size_t)std::min<uint64_t>(kNetChunk, q.len - done);
                 if (tier == TIER_HOST) {
@@ -182,9 +239,8 @@ void DataServer::serve(int fd) {
                 done += n;
             }
             hb_release(&token_);
+            if (held) release(q.grant);
             if (!ok) break;
-        } else {
-            break;
         }
     }
     if (stage) (void)hipHostFree(stage);

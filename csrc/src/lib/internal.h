@@ -69,6 +69,7 @@ struct Extent {
     bool net = false;      // owner on another node: streamed through its data server
     std::string ep;        // "ip:port" of that data server
     uint64_t net_token = 0;  // presented first on each connection to it
+    uint64_t net_grant = 0;  // this extent's capability, named by every request
 };
 
 

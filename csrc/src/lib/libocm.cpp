@@ -13,6 +13,8 @@
 // Reference defects deliberately not reproduced: inverted ocm_is_remote
 // (src/lib.c:461), NULL deref before check in ocm_free (:357-359), stub
 // copy_in/out (:491-499), swapped GPU->RMA offsets (:654).
+#include <cmath>
+
 #include "internal.h"
 #include "ocm/affinity.h"
 #include "ocm/optim.h"
@@ -578,6 +580,13 @@ int ocm_remote_info(ocm_alloc_t a, struct ocm_remote_info *info) {
     return a->remote ? 0 : -1;
 }
 
+// Raw 64-byte handle of extent i (tests: the network tier's capability checks).
+int ocm_x_extent_handle(ocm_alloc_t a, int i, uint8_t *out) {
+    if (!a || !out || i < 0 || (size_t)i >= a->ext.size()) return -1;
+    std::memcpy(out, a->ext[(size_t)i].r.handle, kHandleBytes);
+    return 0;
+}
+
 void *ocm_remotebuf(ocm_alloc_t a) {
     if (!a || a->ext.size() != 1 || a->ext[0].net) return nullptr;
     return S().device >= 0 ? a->ext[0].dptr : a->ext[0].hptr;
@@ -680,9 +689,17 @@ int ocm_x_adam_multi(ocm_alloc_t a, int count, void *const *p, const void *const
     x.c.wd = hp[3];
     x.c.step_size = hp[4];
     x.c.inv_sqrt_bc2 = hp[5];
-    x.c.decoupled = hp[6] != 0.f ? 1u : 0u;
+    x.c.decoupled = std::isnan(hp[6]) ? 0u : 1u;  // NaN: L2 Adam; else AdamW's weight multiplier
     x.c.decay = hp[6];
     x.c.bf16 = bf16 ? 1u : 0u;
+    // Every tensor is checked before the first launch: a bad one never leaves
+    // some parameters a step ahead of the others.
+    for (int i = 0; i < count; i++) {
+        if (!p[i] || !g[i]) OCM_FAIL(-1, "ocm_x_adam_multi: tensor %d has no data", i);
+        if (n[i] > (UINT64_MAX >> 3) || !fits(m_off[i], 4 * n[i]) || !fits(v_off[i], 4 * n[i]) ||
+            (bf16 && !fits(w_off[i], 4 * n[i])))
+            OCM_FAIL(-1, "ocm_x_adam_multi: tensor %d state range exceeds the remote half", i);
+    }
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (wait_alloc(a) != 0) return -1;
     DeviceGuard dg(s.device);
@@ -690,9 +707,6 @@ int ocm_x_adam_multi(ocm_alloc_t a, int count, void *const *p, const void *const
         x.count = (uint32_t)std::min(count - k0, kAdamMaxTensors);
         for (uint32_t j = 0; j < x.count; j++) {
             const int i = k0 + (int)j;
-            if (n[i] > (UINT64_MAX >> 3) || !fits(m_off[i], 4 * n[i]) || !fits(v_off[i], 4 * n[i]) ||
-                (bf16 && !fits(w_off[i], 4 * n[i])))
-                OCM_FAIL(-1, "ocm_x_adam_multi: tensor %d state range exceeds the remote half", i);
             x.t[j] = AdamTensor{p[i], g[i], n[i], bf16 ? w_off[i] : 0, m_off[i], v_off[i]};
         }
         const hipError_t e = adam_remote_multi_launch(x, static_cast<hipStream_t>(stream));
@@ -735,7 +749,7 @@ static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64
     x.wd = hp[3];
     x.step_size = hp[4];
     x.inv_sqrt_bc2 = hp[5];
-    x.decoupled = hp[6] != 0.f ? 1u : 0u;
+    x.decoupled = std::isnan(hp[6]) ? 0u : 1u;
     x.decay = hp[6];
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (wait_alloc(a) != 0) return -1;  // queued async ops on this allocation come first

@@ -56,7 +56,7 @@ void net_close(NetConn &c) {
 // calling thread or a helper thread: touches only `c` and the caller's buffers.
 int net_part(NetConn &c, const Extent &e, bool put, char *lin, bool dev, int device, uint64_t ext_off,
              uint64_t len) {
-    NetReq q{kNetMagic, put ? (uint32_t)NET_PUT : (uint32_t)NET_GET, e.r.slab_id, e.r.tier, e.r.offset + ext_off, len};
+    NetReq q{kNetMagic, put ? (uint32_t)NET_PUT : (uint32_t)NET_GET, e.net_grant, ext_off, len};
     if (send_all(c.fd, &q, sizeof(q)) != 1) return -1;
     DeviceGuard g(dev ? device : -1);
     NetResp r;

@@ -84,17 +84,15 @@ int import_extent(Extent &e) {
     State &s = S();
     const Region &r = e.r;
     if (r.flags & REGION_NET) {
-        char buf[65] = {0};
-        std::memcpy(buf, r.handle, 64);
-        char host[64] = {0};
+        std::string host;
         int port = 0;
-        unsigned long long tok = 0;
-        if (std::sscanf(buf, "net:%63[^:]:%d:%llx", host, &port, &tok) != 3 || port <= 0)
-            OCM_FAIL(-1, "bad network-tier handle");
+        uint64_t tok = 0, grant = 0;
+        if (!parse_net_handle(r.handle, &host, &port, &tok, &grant)) OCM_FAIL(-1, "bad network-tier handle");
         e.net = true;
         e.dev_ok = false;
-        e.ep = std::string(host) + ":" + std::to_string(port);
+        e.ep = host + ":" + std::to_string(port);
         e.net_token = tok;
+        e.net_grant = grant;
         return 0;
     }
     SlabKey key{r.owner_rank, r.tier, r.slab_id};

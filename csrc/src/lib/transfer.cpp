@@ -367,6 +367,13 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     } else {
         service_park();
         segments(a, rem_off, len, segs);
+        // Pieces between a host-resident local half and the host tier are copied
+        // by this thread right away: first let the work they must follow finish
+        // (an ocm_stream_wait dependency and earlier async ops, both queued on st).
+        bool cpu_piece = false;
+        for (auto &g : segs) cpu_piece |= lloc != LOC_DEVICE && a->ext[g.ext].r.tier != TIER_GPU;
+        if (cpu_piece && (err = hipStreamSynchronize(st)) != hipSuccess)
+            OCM_FAIL(-1, "ordering a host copy after queued work: %s", hipGetErrorString(err));
         for (auto &g : segs) {
             const Extent &e = a->ext[g.ext];
             char *r = (lloc == LOC_DEVICE || e.r.tier == TIER_GPU) ? e.dptr : e.hptr;

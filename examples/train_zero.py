@@ -61,12 +61,15 @@ def main():
         return out
 
     # one ocmd per rank, one mesh (rank 0 picks the ports)
-    ports = gather(free_ports(world) if rank == 0 else None)[0]
+    import secrets
+
+    ports, key = gather((free_ports(world), secrets.token_hex(16)) if rank == 0 else None)[0]
     ns = f"zero{os.environ.get('MASTER_PORT', '0')}_{ports[0]}"
     workdir = os.path.join("/tmp", f"ocm_{ns}")
     os.makedirs(workdir, exist_ok=True)
     gpus = gather(gpu) if gpu is not None else [None] * world
-    mesh = Mesh(world, gpus=gpus, ns=ns, policy="stripe", workdir=workdir, ports=ports, ranks=[rank]).start(timeout=120)
+    mesh = Mesh(world, gpus=gpus, ns=ns, policy="stripe", workdir=workdir, ports=ports, ranks=[rank],
+                key=key).start(timeout=120)
     dist.barrier()
     ok = False
     try:

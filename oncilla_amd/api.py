@@ -184,6 +184,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_set_tuning_dir": (i32, [i32, i32, i32, i32]),
             "ocm_x_batch": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, ctypes.POINTER(u64), i32, i32]),
             "ocm_x_link_info": (i32, [i32, i32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
+            "ocm_x_extent_handle": (i32, [vp, i32, ctypes.c_char_p]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(lib, name)
@@ -191,6 +192,16 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             fn.argtypes = args
         _lib = lib
         return lib
+
+
+def _adam_hp(hp) -> tuple:
+    """(b1, b2, eps, weight_decay, step_size, 1/sqrt(bias_correction2)[, decay]) -> 7 floats.
+    decay is AdamW's weight multiplier 1 - lr * weight_decay; NaN (the default) selects
+    L2-regularised Adam."""
+    hp = tuple(float(x) for x in hp)
+    if len(hp) not in (6, 7):
+        raise ValueError("Adam hyper-parameters: 6 values (Adam) or 7 (AdamW decay multiplier last)")
+    return hp if len(hp) == 7 else hp + (float("nan"),)
 
 
 def last_error() -> str:
@@ -388,6 +399,13 @@ class Allocation:
             ],
         }
 
+    def extent_handle(self, i: int = 0) -> bytes:
+        """Raw 64-byte export handle of extent i (IPC handle, host-tier path or net: capability)."""
+        buf = ctypes.create_string_buffer(64)
+        if self._c.lib.ocm_x_extent_handle(self.handle, i, buf) != 0:
+            raise OcmError("ocm_x_extent_handle: no such extent")
+        return buf.raw
+
     # --- data movement ---
     def onesided(self, op_flag: int, local_offset: int, remote_offset: int, nbytes: int, async_: bool = False) -> None:
         p = OcmParams(local_offset, remote_offset, 0, 0, nbytes, op_flag)
@@ -448,7 +466,7 @@ class Allocation:
         Queued on `stream` (default: torch's current stream)."""
         import torch
 
-        hp = tuple(hp) + (0.0,) * (7 - len(hp))
+        hp = _adam_hp(hp)
         h = (ctypes.c_float * 7)(*hp)
         pp, gp, st = ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(g.data_ptr()), self._stream_handle(stream)
         if p.dtype == torch.bfloat16:
@@ -472,7 +490,7 @@ class Allocation:
         if bf16 and w_offs is None:
             raise ValueError("bf16 parameters need w_offs (fp32 master weights)")
         arr_v, arr_u = ctypes.c_void_p * k, ctypes.c_uint64 * k
-        hp = tuple(hp) + (0.0,) * (7 - len(hp))
+        hp = _adam_hp(hp)
         rc = self._c.lib.ocm_x_adam_multi(
             self.handle, k, arr_v(*[t.data_ptr() for t in ps]), arr_v(*[t.data_ptr() for t in gs]),
             arr_u(*[t.numel() for t in ps]), arr_u(*(w_offs or [0] * k)), arr_u(*m_offs), arr_u(*v_offs),

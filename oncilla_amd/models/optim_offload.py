@@ -58,8 +58,6 @@ class OffloadedAdam:
                 raise ValueError("OffloadedAdam takes contiguous float32 or bfloat16 parameters")
         if not self.bf16 and any(p.dtype != torch.float32 for p in self.params):
             raise ValueError("mixed float32 / bfloat16 parameter lists are not supported")
-        if self.bf16 and mode == "staged":
-            raise ValueError("bfloat16 parameters use mode='fused' (fp32 master weights in remote memory)")
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.decoupled = decoupled  # AdamW (torch.optim.AdamW): decay the weights, not the gradient
         self.t = 0
@@ -72,6 +70,10 @@ class OffloadedAdam:
         self.mode = ("fused" if on_gpu else "staged") if mode == "auto" else mode
         if self.mode not in ("fused", "staged"):
             raise ValueError(f"mode {mode!r}")
+        if self.bf16 and self.mode == "staged":
+            # the staged path has no fp32 master weights: small updates would round away in bf16
+            raise ValueError("bfloat16 parameters need mode='fused' on a GPU client (fp32 master weights "
+                             "in remote memory)")
         if self.mode == "fused":
             if not on_gpu:
                 raise ValueError("mode='fused' needs a GPU client")
@@ -139,7 +141,7 @@ class OffloadedAdam:
     def _step_fused(self) -> None:
         b1, b2 = self.betas
         hp = (b1, b2, self.eps, self.weight_decay, self.lr / (1 - b1 ** self.t), 1 / math.sqrt(1 - b2 ** self.t),
-              (1 - self.lr * self.weight_decay) if self.decoupled else 0.0)
+              (1 - self.lr * self.weight_decay) if self.decoupled else math.nan)  # NaN: L2 Adam
         ps, gs, mo, vo, wo = [], [], [], [], []
         for p, start in zip(self.params, self.starts):
             if p.grad is None:

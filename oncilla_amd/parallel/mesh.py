@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import json
 import os
+import secrets
 import signal
 import socket
 import subprocess
@@ -70,7 +71,8 @@ class Mesh:
     def __init__(self, n: int, gpus: Optional[Sequence[Optional[int]]] = None, ns: Optional[str] = None,
                  policy: str = "ring", extra_args: Sequence[str] = (), env: Optional[dict] = None,
                  workdir: Optional[str] = None, ports: Optional[Sequence[int]] = None, ranks: Optional[Sequence[int]] = None,
-                 rank_env: Optional[dict] = None, bin_dir: Optional[str] = None, watch: bool = True):
+                 rank_env: Optional[dict] = None, bin_dir: Optional[str] = None, watch: bool = True,
+                 key: Optional[str] = None):
         self.n = n
         self.gpus = list(gpus) if gpus is not None else [None] * n
         self.ns = ns or f"m{uuid.uuid4().hex[:10]}"
@@ -85,6 +87,9 @@ class Mesh:
         self.ranks = list(ranks) if ranks is not None else list(range(n))  # which ranks THIS process launches
         self.nodefile = os.path.join(self.workdir, "nodefile")
         self.daemons: list[Daemon] = []
+        # Mesh authentication secret (OCM_MESH_KEY): random per mesh unless the
+        # caller shares one (ranks launched by different processes must agree).
+        self.key = key or self.env.get("OCM_MESH_KEY") or os.environ.get("OCM_MESH_KEY") or secrets.token_hex(16)
 
     def client_env(self, rank: int = 0) -> dict:
         env = dict(os.environ)
@@ -109,6 +114,7 @@ class Mesh:
         env.update(self.env)
         env.update(self.rank_env.get(r, {}))
         env["OCM_NS"] = self.ns
+        env["OCM_MESH_KEY"] = self.key
         with open(log, "a") as lf:
             proc = subprocess.Popen(args, stdout=lf, stderr=subprocess.STDOUT, env=env, start_new_session=True)
         return Daemon(r, proc, ready, log)

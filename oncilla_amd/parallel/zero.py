@@ -28,6 +28,10 @@ def flatten_params(params: Iterable, device=None):
     import torch
 
     params = [p for p in params if p.requires_grad]
+    bad = sorted({str(p.dtype) for p in params if p.dtype != torch.float32})
+    if bad:
+        # re-pointing p.data at an fp32 buffer would silently change the model's dtype
+        raise TypeError(f"flatten_params takes float32 parameters only (got {', '.join(bad)})")
     total = sum(p.numel() for p in params)
     device = device or params[0].device
     flat = torch.empty(total, dtype=torch.float32, device=device)

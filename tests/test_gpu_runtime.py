@@ -479,3 +479,30 @@ def test_autotune_installs_a_per_direction_choice(mesh_factory):
         finally:
             api.set_tuning()
             a.free()
+
+
+def test_stream_wait_orders_host_tier_memcpy(mesh_factory):
+    """ocm_stream_wait must hold back a put whose pieces the CPU copies (pinned
+    local half <-> host tier): the GPU write into the local half queued on
+    another stream lands first (the memcpy ignored the dependency)."""
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 8 << 20
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_HOST_TIER)
+        assert a.remote_info()["extents"][0]["tier"] == api.OCM_TIER_HOST
+        loc = a.local_tensor()
+        assert loc.device.type == "cpu" and loc.is_pinned()
+        loc.zero_()
+        src = torch.full((n,), 7, dtype=torch.uint8, device="cuda:0")
+        st = torch.cuda.Stream(device=0)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(200_000_000)  # keep the stream busy for a while
+            loc.copy_(src, non_blocking=True)  # D2H into the pinned local half, after the spin
+        a.stream_wait(st)
+        a.put(0, 0, n)
+        st.synchronize()
+        loc.zero_()
+        a.get(0, 0, n)
+        assert int((loc != 7).sum()) == 0
+        a.free()

@@ -135,3 +135,21 @@ def test_reference_style_daemon_launch(tmp_path, native, tool):
     finally:
         d.terminate()
         d.wait(timeout=10)
+
+
+def test_mesh_on_open_address_needs_a_key(tmp_path, native):
+    """A multi-daemon mesh whose port binds a non-loopback address refuses to start
+    without OCM_MESH_KEY (its HELLO token would be a guessable constant), unless the
+    operator opts out with OCM_MESH_INSECURE=1."""
+    import subprocess
+
+    from oncilla_amd.parallel.mesh import free_ports, write_nodefile
+
+    ports = free_ports(2)
+    nf = write_nodefile(str(tmp_path / "nodefile"), ports)
+    env = dict(os.environ, OCM_NS=f"keyless{ports[0]}", OCM_NO_GPU="1")
+    env.pop("OCM_MESH_KEY", None)
+    env.pop("OCM_MESH_INSECURE", None)
+    r = subprocess.run([f"{native}/ocmd", nf, "--rank", "1", "--gpu", "none", "--bind", "0.0.0.0"], env=env,
+                       capture_output=True, text=True, timeout=30)
+    assert r.returncode != 0 and "OCM_MESH_KEY" in (r.stdout + r.stderr)

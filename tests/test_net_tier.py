@@ -103,3 +103,105 @@ def test_parallel_streams_odd_split(mesh_factory, monkeypatch, streams):
             a.get(loff, roff, size)
             assert a.check(seed=50 + i, offset=loff, nbytes=size - size % 4, first_word=loff // 4) == 0, size
         a.free()
+
+
+# ---- data-server capabilities (per-extent grants) ----
+
+def _net_endpoint(handle: bytes):
+    """'net:<ip>:<port>:<conn token>:<grant>' -> (ip, port, token, grant)."""
+    tag, ip, port, tok, grant = handle.rstrip(b"\0").decode().split(":")
+    assert tag == "net"
+    return ip, int(port), int(tok, 16), int(grant, 16)
+
+
+def _raw_conn(ip, port, tok):
+    import socket
+    import struct
+
+    s = socket.create_connection((ip, port), timeout=20)
+    s.sendall(struct.pack("<Q", tok))
+    return s
+
+
+def _recv_exact(s, n):
+    buf = bytearray()
+    while len(buf) < n:
+        chunk = s.recv(min(n - len(buf), 1 << 20))
+        assert chunk, "data server closed the connection"
+        buf += chunk
+    return bytes(buf)
+
+
+def _raw_get_header(s, grant, off, n):
+    import struct
+
+    s.sendall(struct.pack("<IIQQQ", 0x4F434E44, 2, grant, off, n))
+    magic, err, ln = struct.unpack("<IiQ", _recv_exact(s, 16))
+    assert magic == 0x4F434E44
+    return err, ln
+
+
+def test_net_grant_bounds_each_request_by_its_extent(mesh_factory):
+    """A request names its extent's grant and stays inside that extent: the
+    slab around it, other extents and forged grants are refused (ADVICE r1:
+    one token used to open every allocation on the owner)."""
+    import ctypes
+    import errno
+
+    m = mesh_factory(2, rank_env=hosts("nodeA", "nodeB"))
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        n = 1 << 20
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=n, remote_bytes=n)
+        b = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=n, remote_bytes=n)
+        a.fill(seed=11)
+        a.put(0, 0, n)
+        ip, port, tok, ga = _net_endpoint(a.extent_handle(0))
+        gb = _net_endpoint(b.extent_handle(0))[3]
+        assert ga != gb and ga and gb
+        s = _raw_conn(ip, port, tok)
+        try:
+            err, ln = _raw_get_header(s, ga, 4096, 8192)
+            assert err == 0 and ln == 8192
+            assert _recv_exact(s, 8192) == ctypes.string_at(a.local_ptr + 4096, 8192)
+            assert _raw_get_header(s, ga, n - 8, 16)[0] == errno.EFAULT  # runs past the extent
+            assert _raw_get_header(s, ga, 0, n + 1)[0] == errno.EFAULT
+            assert _raw_get_header(s, ga ^ (1 << 17), 0, 8)[0] == errno.EACCES  # forged grant
+            b.free()
+            assert _raw_get_header(s, gb, 0, 8)[0] == errno.EACCES  # revoked at free
+        finally:
+            s.close()
+        a.free()
+
+
+def test_net_free_during_inflight_get_defers_release(mesh_factory):
+    """Freeing an extent while a data-server GET still streams it must not pull
+    the memory from under the copy: the last request releases it."""
+    import ctypes
+    import errno
+    import time
+
+    m = mesh_factory(2, rank_env=hosts("nodeA", "nodeB"))
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        n = 32 << 20
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=n, remote_bytes=n)
+        a.fill(seed=21)
+        a.put(0, 0, n)
+        want = ctypes.string_at(a.local_ptr, n)
+        ip, port, tok, g = _net_endpoint(a.extent_handle(0))
+        s = _raw_conn(ip, port, tok)
+        try:
+            err, ln = _raw_get_header(s, g, 0, n)
+            assert err == 0 and ln == n
+            head = _recv_exact(s, 1 << 20)  # the server is now blocked sending the rest
+            a.free()
+            time.sleep(0.2)
+            assert c.stats(1)["host_used"] >= n  # still held by the in-flight GET
+            got = head + _recv_exact(s, n - len(head))
+            assert got == want
+            deadline = time.time() + 10
+            while c.stats(1)["host_used"] and time.time() < deadline:
+                time.sleep(0.02)
+            assert c.stats(1)["host_used"] == 0  # released by the request that finished
+            assert _raw_get_header(s, g, 0, 8)[0] == errno.EACCES
+        finally:
+            s.close()

@@ -141,3 +141,75 @@ def test_fused_adam_bf16_params_with_remote_fp32_master(mesh_factory):
                 torch.testing.assert_close(vv, opt_ref.state[r]["exp_avg_sq"].cpu(), rtol=1e-4, atol=1e-6)
         finally:
             opt.close()
+
+
+@pytest.mark.gpu
+def test_fused_adamw_many_tensors_and_missing_grads(mesh_factory):
+    """More than one launch's worth of parameters (32 descriptors per launch),
+    large and tiny tensors mixed, some without a gradient (skipped, like torch),
+    and AdamW with lr * weight_decay == 1 (decay multiplier 0: the weights are
+    fully decayed, which an in-band 0 = 'no AdamW' flag used to turn into L2 Adam)."""
+    m = mesh_factory(2, gpus=[0, 0])
+    g = torch.Generator().manual_seed(9)
+    shapes = [(1 << 16,) if i % 7 == 0 else (int(torch.randint(1, 300, (1,), generator=g)),) for i in range(45)]
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        for lr, wd in ((1e-2, 0.05), (0.5, 2.0)):
+            ref = [torch.randn(s, generator=g).to("cuda:0").requires_grad_() for s in shapes]
+            mine = [p.detach().clone().requires_grad_() for p in ref]
+            opt_ref = torch.optim.AdamW(ref, lr=lr, weight_decay=wd)
+            opt = OffloadedAdamW(mine, c, lr=lr, weight_decay=wd, mode="fused")
+            try:
+                for s in range(3):
+                    gg = torch.Generator().manual_seed(200 + s)
+                    for i, (a, b) in enumerate(zip(ref, mine)):
+                        if i % 5 == 3:
+                            a.grad = b.grad = None
+                            continue
+                        a.grad = torch.randn(a.shape, generator=gg).to("cuda:0")
+                        b.grad = a.grad.clone()
+                    opt_ref.step()
+                    opt.step()
+                opt.synchronize()
+                for a, b in zip(ref, mine):
+                    torch.testing.assert_close(b.detach().cpu(), a.detach().cpu(), rtol=1e-5, atol=1e-6)
+            finally:
+                opt.close()
+
+
+@pytest.mark.gpu
+def test_fused_adam_rejects_bad_tensor_before_any_launch(mesh_factory):
+    """A state range outside the remote half anywhere in the list fails the whole
+    call before the first launch: no parameter moves."""
+    m = mesh_factory(2, gpus=[0, 0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=64 * 40 * 8)
+        ps = [torch.zeros(64, device="cuda:0") for _ in range(40)]
+        gs = [torch.ones(64, device="cuda:0") for _ in range(40)]
+        mo = [4 * 64 * i for i in range(40)]
+        vo = [4 * 64 * (40 + i) for i in range(40)]
+        vo[37] = 64 * 40 * 8  # past the end, in the second launch's chunk
+        hp = (0.9, 0.999, 1e-8, 0.0, 1e-3, 1.0, float("nan"))
+        with pytest.raises(api.OcmError):
+            a.adam_multi(ps, gs, mo, vo, hp)
+        torch.cuda.synchronize()
+        assert all(int(p.count_nonzero()) == 0 for p in ps)
+        a.free()
+
+
+def test_staged_mode_refuses_bf16_after_auto_resolution(mesh_factory, monkeypatch):
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    m = mesh_factory(1)
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        p = torch.zeros(16, dtype=torch.bfloat16, requires_grad=True)
+        with pytest.raises(ValueError, match="fused"):
+            OffloadedAdam([p], c)  # mode='auto' resolves to staged on a CPU client
+
+
+def test_flatten_params_keeps_dtypes_honest():
+    from oncilla_amd.parallel.zero import flatten_params
+
+    with pytest.raises(TypeError):
+        flatten_params([torch.zeros(4, dtype=torch.bfloat16, requires_grad=True)])
+    p = torch.ones(3, requires_grad=True)
+    flat, layout = flatten_params([p])
+    assert p.dtype == torch.float32 and flat.numel() == 3 and layout[0][1:] == (0, 3)
