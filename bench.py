@@ -491,16 +491,17 @@ def main() -> int:
             _local(client.close)
         if mesh is not None:
             _local(mesh.stop)
-    if dist is not None:
-        if rc == 0:
-            _local(dist.barrier)
-        _local(dist.destroy_process_group)
     if rank == 0:
         line = json.dumps(result)
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    if dist is not None:
+        # Rank 0 has printed: only now may a failed rank exit (torchrun tears every
+        # worker down as soon as one exits non-zero). Bounded by the group timeout.
+        _local(dist.barrier)
+        _local(dist.destroy_process_group)
     return rc
 
 

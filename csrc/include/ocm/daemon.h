@@ -228,6 +228,8 @@ private:
     size_t pinned_cpus_ = 0;             // event loop restricted to this many CPUs near the GPU (0: not pinned)
     uint64_t mesh_token_ = 0;            // HELLO must carry it (hash of namespace + mesh key)
     uint64_t data_token_ = 0;            // network-tier data server: random per boot
+    NodeLinks links_{};                  // xGMI link table of our GPU (sent to rank0 after ADD_NODE)
+    void probe_links();
     void send_hello(int fd);
     bool resumed_ = false;               // rank0 restored its directory from state_file
     uint64_t saved_version_ = 0;

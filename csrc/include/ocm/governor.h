@@ -37,6 +37,7 @@ struct NodeState {
     uint64_t host_capacity = 0, host_reserved = 0;
     std::string host;
     uint64_t boot_id = 0;      // identifies one ocmd process lifetime (resume: same id = memory survived)
+    std::vector<uint8_t> hops; // by GPU ordinal on its host: xGMI hops from this node's GPU (MSG_NODE_LINKS)
 };
 
 struct PlacedExtent {
@@ -76,6 +77,12 @@ public:
     // directory thought it owned.
     void add_node(const NodeConfig &cfg, uint64_t boot_id = 0);
     void mark_dead(int rank);
+    // A node's xGMI table (MSG_NODE_LINKS): same-host peers are then tried
+    // nearest first (ring order among equals), so ring / least_loaded / stripe
+    // prefer 1-hop GPUs. Without tables every peer is equally near.
+    void set_links(const NodeLinks &l);
+    // xGMI hops from rank a's GPU to rank b's GPU; kHopsUnknown when not on one host / unknown.
+    int hops(int a, int b) const;
     const NodeState &node(int rank) const { return nodes_.at(rank); }
     int num_nodes() const { return static_cast<int>(nodes_.size()); }
     int num_alive() const;

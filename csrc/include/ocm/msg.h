@@ -42,6 +42,7 @@ enum MsgType : uint32_t {
     MSG_TICK_WAKE,        // any -> all (TCP): join tick number u.req.bytes
     MSG_OWNED,            // daemon -> rank0 after ADD_NODE: one extent it holds (u.region, pid = app)
     MSG_OWNED_DONE,       // daemon -> rank0: end of that report
+    MSG_NODE_LINKS,       // daemon -> rank0 after ADD_NODE: xGMI link type / hops from its GPU (u.links)
     MSG_MAX
 };
 
@@ -101,13 +102,31 @@ struct NodeConfig {
     uint64_t host_capacity;
     uint64_t gpu_used;
     uint64_t host_used;
-    uint32_t num_nodes;
-    uint32_t num_apps;
+    uint16_t num_nodes;
+    uint16_t num_apps;
+    uint8_t xgmi_peers;    // GPUs on the node this daemon's GPU reaches over xGMI
+    uint8_t min_hops, max_hops;  // over those links (0 when none)
+    uint8_t pad0;
     uint32_t n_alloc, n_free, n_reclaimed, n_spilled, n_slabs;
     uint32_t ticks;        // allgather ticks of the control transport (0 on TCP)
     uint32_t n_leases;     // capacity leases this daemon holds on peers
     uint32_t lease_allocs; // allocations served from them (no mesh round trip)
 };
+
+// Topology of one daemon's GPU (hipExtGetLinkTypeAndHopCount to every other
+// GPU ordinal on its node), fed to rank0's placement (nearest peer first).
+constexpr int kMaxLinkGpus = 32;
+constexpr uint8_t kHopsUnknown = 0xFF;
+struct NodeLinks {
+    int32_t rank;
+    int32_t gpu;           // -1: CPU-only daemon (no table)
+    uint32_t n;            // entries used (GPU ordinals 0..n-1)
+    uint32_t pad;
+    uint8_t hops[kMaxLinkGpus];  // kHopsUnknown: no link / self
+    uint8_t type[kMaxLinkGpus];  // hipExtLinkType* value
+};
+
+static_assert(sizeof(NodeLinks) <= 128, "NodeLinks fits the message union");
 
 struct Msg {
     uint32_t type;     // MsgType
@@ -121,6 +140,7 @@ struct Msg {
         AllocReq req;
         Region region;
         NodeConfig node;
+        NodeLinks links;
         uint8_t raw[128];
     } u;
 };

@@ -49,6 +49,11 @@ public:
     virtual ~Collective() = default;
     // recv = concat over ranks of every rank's `bytes`-byte send buffer. 0 ok.
     virtual int allgather(const void *send, void *recv, size_t bytes) = 0;
+    // Persistent slots (optional): when send_slot() returns a buffer, the caller
+    // may fill it in place and pass it as `send`; recv_slots() then holds the
+    // gathered slots after allgather() with recv == recv_slots().
+    virtual void *send_slot(size_t) { return nullptr; }
+    virtual const void *recv_slots() const { return nullptr; }
     virtual void abort() {}
     virtual const char *name() const = 0;
 };

@@ -129,7 +129,9 @@ struct ocm_daemon_stats {
     uint64_t ctrl_ticks;   /* allgather ticks of the RCCL/socket control transport (0 on TCP) */
     uint64_t n_leases;     /* capacity leases held on peers */
     uint64_t lease_allocs; /* allocations carved from them without a mesh round trip */
-    uint64_t reserved[1];
+    uint32_t xgmi_peers;   /* GPUs on the node this daemon's GPU reaches over xGMI */
+    uint16_t min_hops;     /* xGMI hop count over those links (0 when none) */
+    uint16_t max_hops;
 };
 
 ocm_alloc_t ocm_alloc_ex(ocm_alloc_param_t alloc_param, const struct ocm_alloc_ex_params *ex);

@@ -214,6 +214,20 @@ int Governor::restore(const std::string &text, std::string *err) {
     return (int)table_.size();
 }
 
+void Governor::set_links(const NodeLinks &l) {
+    if (l.rank < 0 || l.rank >= (int)nodes_.size()) return;
+    const uint32_t n = std::min<uint32_t>(l.n, (uint32_t)kMaxLinkGpus);
+    nodes_[l.rank].hops.assign(l.hops, l.hops + n);
+    version_++;
+}
+
+int Governor::hops(int a, int b) const {
+    if (a < 0 || b < 0 || a >= (int)nodes_.size() || b >= (int)nodes_.size()) return kHopsUnknown;
+    const NodeState &x = nodes_[a], &y = nodes_[b];
+    if (x.host != y.host || x.gpu < 0 || y.gpu < 0 || y.gpu >= (int)x.hops.size()) return kHopsUnknown;
+    return x.hops[(size_t)y.gpu];
+}
+
 void Governor::mark_dead(int rank) {
     if (rank >= 0 && rank < (int)nodes_.size()) nodes_[rank].alive = false;
     version_++;
@@ -265,6 +279,8 @@ std::vector<int> Governor::candidates(const PlaceRequest &r) const {
         int k = (r.orig_rank + d) % n;
         if (nodes_[k].alive && nodes_[k].joined && nodes_[k].host == home) out.push_back(k);
     }
+    // Nearest GPUs first (xGMI hop count from the origin's GPU), ring order among equals.
+    std::stable_sort(out.begin(), out.end(), [&](int a, int b) { return hops(r.orig_rank, a) < hops(r.orig_rank, b); });
     return out;
 }
 

@@ -73,6 +73,7 @@ const char *msg_type_str(uint32_t t) {
     case MSG_TICK_WAKE: return "MSG_TICK_WAKE";
     case MSG_OWNED: return "MSG_OWNED";
     case MSG_OWNED_DONE: return "MSG_OWNED_DONE";
+    case MSG_NODE_LINKS: return "MSG_NODE_LINKS";
     default: return "INVALID MSG TYPE";
     }
 }

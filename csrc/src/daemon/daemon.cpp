@@ -67,8 +67,15 @@ NodeConfig Daemon::my_config() const {
     c.host_capacity = arena_ ? arena_->capacity(TIER_HOST) : 0;
     c.gpu_used = arena_ ? arena_->used(TIER_GPU) : 0;
     c.host_used = arena_ ? arena_->used(TIER_HOST) : 0;
-    c.num_nodes = (uint32_t)n_;
-    c.num_apps = (uint32_t)apps_.size();
+    c.num_nodes = (uint16_t)n_;
+    c.num_apps = (uint16_t)std::min<size_t>(apps_.size(), 65535);
+    for (uint32_t p = 0; p < links_.n && p < (uint32_t)kMaxLinkGpus; p++) {
+        const uint8_t h = links_.hops[p];
+        if ((int)p == gpu_ || h == kHopsUnknown) continue;
+        c.xgmi_peers++;
+        c.min_hops = c.min_hops ? std::min(c.min_hops, h) : h;
+        c.max_hops = std::max(c.max_hops, h);
+    }
     c.n_alloc = (uint32_t)n_alloc_;
     c.n_free = (uint32_t)n_free_;
     c.n_reclaimed = (uint32_t)n_reclaimed_;
@@ -272,6 +279,7 @@ int Daemon::init() {
         ep_add(fd, EPOLLIN, tag(T_CONN, (uint64_t)fd));
         conns_[fd] = std::move(c);
     }
+    probe_links();
     // Join: report our configuration to rank0 (reference notify_rank0, src/main.c:143-160).
     join_rank0();
     OCM_INFO("ocmd rank %d/%d up: gpu %d (%d visible, host tier on NUMA node %d), hbm capacity %.1f GiB, host tier %.1f GiB, policy %s, ns %s",

@@ -65,6 +65,12 @@ void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
     case MSG_OWNED:
         if (rank_ == 0 && gov_) gov_->confirm_extent(m.src_rank, m.u.region, m.pid);
         break;
+    case MSG_NODE_LINKS:
+        if (rank_ == 0 && gov_) {
+            m.u.links.rank = m.rank;
+            gov_->set_links(m.u.links);
+        }
+        break;
     case MSG_OWNED_DONE:
         if (rank_ == 0 && gov_) {
             int dropped = gov_->end_reconcile(m.src_rank);

@@ -46,6 +46,15 @@ void Daemon::join_rank0() {
     add.seq = boot_id_;
     add.u.node = my_config();
     send_rank(0, add);
+    if (links_.gpu >= 0) {
+        Msg l;
+        std::memset(&l, 0, sizeof(l));
+        l.type = MSG_NODE_LINKS;
+        l.status = MSG_REQUEST;
+        l.rank = rank_;
+        l.u.links = links_;
+        send_rank(0, l);
+    }
     // What we hold (empty on first boot): lets a restarted rank0 rebuild its directory.
     for (auto &kv : owned_) {
         const OwnedExtent &oe = kv.second;
@@ -76,6 +85,34 @@ void Daemon::join_rank0() {
     done.rank = rank_;
     done.seq = owned_.size();
     send_rank(0, done);
+}
+
+// hipExtGetLinkTypeAndHopCount from our GPU to every other ordinal on the node.
+// OCM_LINK_HOPS="h0,h1,..." overrides the hop counts (tests: synthetic topologies).
+void Daemon::probe_links() {
+    std::memset(&links_, 0, sizeof(links_));
+    links_.rank = rank_;
+    links_.gpu = gpu_;
+    std::memset(links_.hops, kHopsUnknown, sizeof(links_.hops));
+    if (gpu_ < 0) return;
+    links_.n = (uint32_t)std::min(num_gpu_, kMaxLinkGpus);
+    for (int p = 0; p < (int)links_.n; p++) {
+        if (p == gpu_) continue;
+        uint32_t type = 0, hops = 0;
+        if (hipExtGetLinkTypeAndHopCount(gpu_, p, &type, &hops) == hipSuccess && hops < kHopsUnknown) {
+            links_.hops[p] = (uint8_t)hops;
+            links_.type[p] = (uint8_t)type;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
+    if (const char *o = std::getenv("OCM_LINK_HOPS")) {
+        std::stringstream ss(o);
+        std::string tok;
+        for (int p = 0; p < kMaxLinkGpus && std::getline(ss, tok, ','); p++)
+            if (!tok.empty()) links_.hops[p] = (uint8_t)std::min(254, std::atoi(tok.c_str()));
+        links_.n = (uint32_t)kMaxLinkGpus;
+    }
 }
 
 void Daemon::try_rejoin_rank0() {

@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 
 #include "ocm/log.h"
@@ -20,9 +21,20 @@ namespace {
 
 // ---------------------------------------------------------------- RCCL
 
+// Each tick is ONE replay of a captured ncclAllGather over persistent slots:
+// the send slot and the gathered slots live in pinned, device-mapped host
+// memory, so the tick thread writes its records straight into the send slot
+// and reads the peers' records straight out of the receive slots (no H2D /
+// D2H copies, no per-tick allocation), and the collective is launched as a
+// HIP graph (one launch, no RCCL enqueue work per tick). Completion is a
+// spin on the stream, bounded by abort requests and RCCL async errors.
+// OCM_TICK_GRAPH=0 launches ncclAllGather directly; OCM_TICK_MAPPED=0 keeps
+// the slots in HBM with explicit copies (the round-1 path, for A/B).
 class RcclCollective : public Collective {
 public:
     ~RcclCollective() override {
+        if (exec_) (void)hipGraphExecDestroy(exec_);
+        if (graph_) (void)hipGraphDestroy(graph_);
         if (comm_) {
             if (aborted_)
                 (void)ncclCommAbort(comm_);
@@ -30,14 +42,23 @@ public:
                 (void)ncclCommDestroy(comm_);
         }
         if (stream_) (void)hipStreamDestroy(stream_);
-        if (dsend_) (void)hipFree(dsend_);
-        if (drecv_) (void)hipFree(drecv_);
-        if (hsend_) (void)hipHostFree(hsend_);
-        if (hrecv_) (void)hipHostFree(hrecv_);
+        if (mapped_) {
+            if (hsend_) (void)hipHostFree(hsend_);
+            if (hrecv_) (void)hipHostFree(hrecv_);
+        } else {
+            if (dsend_) (void)hipFree(dsend_);
+            if (drecv_) (void)hipFree(drecv_);
+            if (hsend_) (void)hipHostFree(hsend_);
+            if (hrecv_) (void)hipHostFree(hrecv_);
+        }
     }
     int init(int gpu, int rank, int n, const uint8_t *id, std::string *err) {
         gpu_ = gpu;
         n_ = n;
+        const char *g = std::getenv("OCM_TICK_GRAPH");
+        const char *m = std::getenv("OCM_TICK_MAPPED");
+        use_graph_ = !(g && std::strcmp(g, "0") == 0);
+        mapped_ = !(m && std::strcmp(m, "0") == 0);
         if (hipSetDevice(gpu) != hipSuccess || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
             *err = "rccl: no stream on gpu " + std::to_string(gpu);
             return -1;
@@ -64,25 +85,26 @@ public:
         return 0;
     }
     void request_abort() { abort_req_ = true; }
+    void *send_slot(size_t bytes) override {
+        if (bytes != cap_ && setup(bytes) != 0) return nullptr;
+        return hsend_;
+    }
+    const void *recv_slots() const override { return hrecv_; }
     int allgather(const void *send, void *recv, size_t bytes) override {
         if (aborted_) return -1;
         (void)hipSetDevice(gpu_);
-        if (bytes != cap_) {
-            if (dsend_) (void)hipFree(dsend_);
-            if (drecv_) (void)hipFree(drecv_);
-            if (hsend_) (void)hipHostFree(hsend_);
-            if (hrecv_) (void)hipHostFree(hrecv_);
-            if (hipMalloc(&dsend_, bytes) != hipSuccess || hipMalloc(&drecv_, bytes * n_) != hipSuccess ||
-                hipHostMalloc(&hsend_, bytes) != hipSuccess || hipHostMalloc(&hrecv_, bytes * n_) != hipSuccess)
-                return -1;
-            cap_ = bytes;
+        if (bytes != cap_ && setup(bytes) != 0) return -1;
+        if (send != hsend_) std::memcpy(hsend_, send, bytes);
+        if (!mapped_ && hipMemcpyAsync(dsend_, hsend_, bytes, hipMemcpyHostToDevice, stream_) != hipSuccess) return -1;
+        if (exec_) {
+            if (hipGraphLaunch(exec_, stream_) != hipSuccess) return -1;
+        } else if (ncclAllGather(dsend_, drecv_, bytes, ncclUint8, comm_, stream_) != ncclSuccess) {
+            return -1;
         }
-        std::memcpy(hsend_, send, bytes);
-        if (hipMemcpyAsync(dsend_, hsend_, bytes, hipMemcpyHostToDevice, stream_) != hipSuccess) return -1;
-        if (ncclAllGather(dsend_, drecv_, bytes, ncclUint8, comm_, stream_) != ncclSuccess) return -1;
-        if (hipMemcpyAsync(hrecv_, drecv_, bytes * n_, hipMemcpyDeviceToHost, stream_) != hipSuccess) return -1;
+        if (!mapped_ && hipMemcpyAsync(hrecv_, drecv_, bytes * n_, hipMemcpyDeviceToHost, stream_) != hipSuccess)
+            return -1;
         // Wait without blocking forever: a dead peer never joins the collective.
-        for (;;) {
+        for (unsigned spins = 1;; spins++) {
             hipError_t q = hipStreamQuery(stream_);
             if (q == hipSuccess) break;
             if (q != hipErrorNotReady) return -1;
@@ -90,22 +112,63 @@ public:
                 aborted_ = true;
                 return -1;
             }
-            ncclResult_t async = ncclSuccess;
-            if (ncclCommGetAsyncError(comm_, &async) == ncclSuccess && async != ncclSuccess && async != ncclInProgress)
-                return -1;
+            if ((spins & 63) == 0) {
+                ncclResult_t async = ncclSuccess;
+                if (ncclCommGetAsyncError(comm_, &async) == ncclSuccess && async != ncclSuccess &&
+                    async != ncclInProgress)
+                    return -1;
+            }
         }
-        std::memcpy(recv, hrecv_, bytes * n_);
+        if (recv != hrecv_) std::memcpy(recv, hrecv_, bytes * n_);
         return 0;
     }
     void abort() override { abort_req_ = true; }
     const char *name() const override { return "rccl"; }
 
 private:
+    int setup(size_t bytes) {
+        if (cap_) return -1;  // the slot size is fixed for the transport's life
+        if (mapped_) {
+            const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable;
+            if (hipHostMalloc(&hsend_, bytes, fl) != hipSuccess || hipHostMalloc(&hrecv_, bytes * n_, fl) != hipSuccess ||
+                hipHostGetDevicePointer(&dsend_, hsend_, 0) != hipSuccess ||
+                hipHostGetDevicePointer(&drecv_, hrecv_, 0) != hipSuccess) {
+                (void)hipGetLastError();
+                return -1;
+            }
+        } else if (hipMalloc(&dsend_, bytes) != hipSuccess || hipMalloc(&drecv_, bytes * n_) != hipSuccess ||
+                   hipHostMalloc(&hsend_, bytes) != hipSuccess || hipHostMalloc(&hrecv_, bytes * n_) != hipSuccess) {
+            (void)hipGetLastError();
+            return -1;
+        }
+        std::memset(hsend_, 0, bytes);
+        std::memset(hrecv_, 0, bytes * n_);
+        cap_ = bytes;
+        if (use_graph_) {
+            // Capture once; every rank captures the same single collective, so replays stay matched.
+            hipGraph_t g = nullptr;
+            bool ok = hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal) == hipSuccess;
+            const bool queued = ok && ncclAllGather(dsend_, drecv_, bytes, ncclUint8, comm_, stream_) == ncclSuccess;
+            ok = ok && hipStreamEndCapture(stream_, &g) == hipSuccess && queued;
+            ok = ok && hipGraphInstantiate(&exec_, g, nullptr, nullptr, 0) == hipSuccess;
+            if (g) graph_ = g;
+            if (!ok) {
+                (void)hipGetLastError();
+                if (exec_) (void)hipGraphExecDestroy(exec_);
+                exec_ = nullptr;
+                OCM_WARN("rccl tick: graph capture of the allgather failed; launching it directly");
+            }
+        }
+        return 0;
+    }
     int gpu_ = 0, n_ = 1;
     ncclComm_t comm_ = nullptr;
     hipStream_t stream_ = nullptr;
     void *dsend_ = nullptr, *drecv_ = nullptr, *hsend_ = nullptr, *hrecv_ = nullptr;
     size_t cap_ = 0;
+    bool use_graph_ = true, mapped_ = true;
+    hipGraph_t graph_ = nullptr;
+    hipGraphExec_t exec_ = nullptr;
     std::atomic<bool> abort_req_{false};
     bool aborted_ = false;
 };
@@ -310,6 +373,7 @@ void TickTransport::run() {
     constexpr int kBusyTicks = 64;
     int busy_left = 0;
     TickSlot mine;
+    const TickSlot *send = &mine;
     std::string err;
     std::unique_ptr<Collective> c = factory_(&err, &stop_);
     auto signal = [this] {
@@ -339,12 +403,16 @@ void TickTransport::run() {
                 if (stop_) break;
                 if (!out_.empty() && wake_upto_.load() < ticks_.load() + 1) announce_ = true;  // we start the burst
             }
-            std::memset(&mine, 0, sizeof(mine));
-            while (!out_.empty() && mine.count < (uint32_t)kTickMsgs) {
-                mine.rec[mine.count++] = out_.front();
+            // Fill the collective's own send slot when it has one (no extra copy).
+            TickSlot *slot = static_cast<TickSlot *>(coll_->send_slot(sizeof(TickSlot)));
+            if (!slot) slot = &mine;
+            slot->count = 0;
+            while (!out_.empty() && slot->count < (uint32_t)kTickMsgs) {
+                slot->rec[slot->count++] = out_.front();
                 out_.pop_front();
             }
-            mine.busy = out_.empty() ? 0 : 1;
+            slot->busy = out_.empty() ? 0 : 1;
+            send = slot;
         }
         if (announce_.load()) {
             // Let the event loop nudge the peers for this tick before we block in it.
@@ -352,7 +420,8 @@ void TickTransport::run() {
             ssize_t w = write(efd_, &one, sizeof(one));
             (void)w;
         }
-        if (coll_->allgather(&mine, recv_.data(), sizeof(TickSlot)) != 0) {
+        const TickSlot *got = static_cast<const TickSlot *>(coll_->recv_slots());
+        if (coll_->allgather(send, got ? const_cast<TickSlot *>(got) : recv_.data(), sizeof(TickSlot)) != 0) {
             if (!stop_) OCM_WARN("rank %d: %s tick transport failed; falling back to TCP", rank_, coll_->name());
             failed_ = true;
             uint64_t one = 1;
@@ -366,7 +435,7 @@ void TickTransport::run() {
         {
             std::lock_guard<std::mutex> lk(mu_);
             for (int k = 0; k < n_; k++) {
-                const TickSlot &s = recv_[(size_t)k];
+                const TickSlot &s = (got ? got : recv_.data())[k];
                 if (s.count || s.busy) traffic = true;
                 for (uint32_t i = 0; i < s.count && i < (uint32_t)kTickMsgs; i++)
                     if (s.rec[i].dest == rank_) {

@@ -167,6 +167,7 @@ struct State {
     unsigned svc_solo_tiles = kServiceSoloTilesDefault;  // requests of <= this many tiles stay on workgroup 0
     unsigned svc_proto = kServiceProtoDefault;           // hand-off protocol bits (OCM_SERVICE_PROTO)
     bool svc_running = false;
+    bool svc_park_kernel = false;  // park the service during kernel transfers above svc_max (OCM_SERVICE_PARK_KERNEL)
     unsigned long long svc_seq = 0;
     uint64_t svc_ops = 0, svc_ns_post = 0, svc_ns_wait = 0;  // service diagnostics (ocm_x_service_stats)
     uint64_t svc_max = kServiceMaxDefault;

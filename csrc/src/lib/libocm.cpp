@@ -110,6 +110,7 @@ int ocm_init(void) {
     s.svc_solo_tiles = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES", kServiceSoloTilesDefault));
     s.svc_proto = (unsigned)env_int("OCM_SERVICE_PROTO", (int)kServiceProtoDefault) & 31u;
     s.launch_flags = env_int("OCM_LAUNCH_FLAG", 1) != 0;
+    s.svc_park_kernel = env_int("OCM_SERVICE_PARK_KERNEL", 0) != 0;
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");
     s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
     s.tuning = xfer_tuning_from_env();
@@ -619,6 +620,9 @@ int ocm_stats(int rank, struct ocm_daemon_stats *out) {
     out->ctrl_ticks = c.ticks;
     out->n_leases = c.n_leases;
     out->lease_allocs = c.lease_allocs;
+    out->xgmi_peers = c.xgmi_peers;
+    out->min_hops = c.min_hops;
+    out->max_hops = c.max_hops;
     return 0;
 }
 

@@ -333,6 +333,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     hipStream_t st = async ? lane_stream(a) : s.stream;
     if (honor_dep(a, st, false) != 0) return -1;
     if (use_kernel) {
+        if (s.svc_park_kernel && len > s.svc_max) service_park();  // A/B: no resident poller during the copy
         XferArgs x;
         std::memset(&x, 0, sizeof(x));
         x.lin = lin;

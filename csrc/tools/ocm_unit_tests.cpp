@@ -306,12 +306,65 @@ static void t_arena_host() {
     CHECK(ar.free(r2.slab_id, r2.offset) == 0);
 }
 
+// xGMI topology: rank0 places on the nearest peer GPU (hops from the origin's
+// GPU), ring order among equals; stripes take the nearest peers first.
+static void t_governor_topology() {
+    const uint64_t G = 1ull << 30;
+    auto links = [](int rank, std::vector<int> h) {
+        NodeLinks l;
+        std::memset(&l, 0, sizeof(l));
+        l.rank = rank;
+        l.gpu = rank;
+        l.n = (uint32_t)h.size();
+        std::memset(l.hops, kHopsUnknown, sizeof(l.hops));
+        for (size_t i = 0; i < h.size(); i++) l.hops[i] = h[i] < 0 ? kHopsUnknown : (uint8_t)h[i];
+        return l;
+    };
+    {  // ring from rank 0: (0+1) % 4 would be rank 1 (2 hops); rank 2 is 1 hop away
+        Governor gov(4, Policy::Ring, 1 << 20);
+        for (int r = 0; r < 4; r++) gov.add_node(cfg(r, 8 * G, G));
+        gov.set_links(links(0, {-1, 2, 1, 2}));
+        CHECK(gov.hops(0, 2) == 1 && gov.hops(0, 1) == 2 && gov.hops(1, 0) == kHopsUnknown);
+        PlaceRequest pr;
+        pr.orig_rank = 0;
+        pr.bytes = G;
+        Placement p = gov.place(pr);
+        CHECK(p.err == 0 && p.extents[0].owner == 2);
+        pr.orig_rank = 1;  // no table for rank 1: reference ring order
+        CHECK(gov.place(pr).extents[0].owner == 2);
+    }
+    {  // least loaded: equal free capacity -> the 1-hop peer; more free space still wins
+        Governor gov(4, Policy::LeastLoaded, 1 << 20);
+        for (int r = 0; r < 4; r++) gov.add_node(cfg(r, 8 * G, G));
+        gov.set_links(links(0, {-1, 3, 3, 1}));
+        PlaceRequest pr;
+        pr.orig_rank = 0;
+        pr.bytes = G;
+        CHECK(gov.place(pr).extents[0].owner == 3);
+        CHECK(gov.place(pr).extents[0].owner == 1);  // rank 3 now has less free HBM
+    }
+    {  // stripe width 2 takes the two nearest peers
+        Governor gov(5, Policy::Stripe, 1 << 20);
+        for (int r = 0; r < 5; r++) gov.add_node(cfg(r, 8 * G, G));
+        gov.set_links(links(0, {-1, 2, 2, 1, 1}));
+        PlaceRequest pr;
+        pr.orig_rank = 0;
+        pr.bytes = 8 << 20;
+        pr.stripe_width = 2;
+        Placement p = gov.place(pr);
+        std::set<int> owners;
+        for (auto &e : p.extents) owners.insert(e.owner);
+        CHECK(p.err == 0 && owners == std::set<int>({3, 4}));
+    }
+}
+
 int main() {
     struct T {
         const char *name;
         std::function<void()> fn;
     } tests[] = {{"layout", t_layout},           {"nodefile", t_nodefile}, {"range_alloc", t_range_alloc},
                  {"governor", t_governor},       {"governor_hosts", t_governor_hosts},
+                 {"governor_topology", t_governor_topology},
                  {"governor_checkpoint", t_governor_checkpoint},
                  {"stripe_geometry", t_stripe_geometry},
                  {"arena_host", t_arena_host}};

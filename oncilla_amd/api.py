@@ -108,12 +108,13 @@ class OcmDaemonStats(ctypes.Structure):
         ("ctrl_ticks", ctypes.c_uint64),
         ("n_leases", ctypes.c_uint64),
         ("lease_allocs", ctypes.c_uint64),
-        ("reserved", ctypes.c_uint64 * 1),
+        ("xgmi_peers", ctypes.c_uint32),
+        ("min_hops", ctypes.c_uint16),
+        ("max_hops", ctypes.c_uint16),
     ]
 
     def as_dict(self) -> dict:
-        return {name: (getattr(self, name) if name != "reserved" else None) for name, _ in self._fields_
-                if name != "reserved"}
+        return {name: getattr(self, name) for name, _ in self._fields_}
 
 
 class OcmError(RuntimeError):

@@ -91,3 +91,25 @@ def test_autotune_picks_fastest_by_slowest_rank(native, monkeypatch):
     # 2 gathers per (candidate, direction) + 1 for the rank count
     assert len(calls) == 2 * 2 * len(cands) + 1
     assert cur[0] == cands[r["get"]] and cur[1] == cands[r["put"]]
+
+
+@pytest.mark.parametrize("inject", [("OCM_BENCH_RAISE", "5:verify"), ("OCM_BENCH_FAULT", "3:crash_after_allocs=0")])
+def test_bench_eight_ranks_fail_fast(native, inject):
+    """A failure on one of 8 ranks (a raised phase, or its daemon dying at the
+    first DO_ALLOC) ends every rank within the bound: non-zero exit, and rank 0
+    prints one JSON line naming the phase and the failing ranks' messages."""
+    import time
+
+    env = dict(os.environ, OCM_BENCH_TIMEOUT_S="90", **{inject[0]: inject[1]})
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(29561 + len(inject[1])),
+                        os.path.join(REPO, "bench.py"), "--gpus", "8", "--device", "cpu", "--steps", "1", "--warmup",
+                        "1", "--max-bytes", str(1 << 20), "--alloc-samples", "10"], capture_output=True, text=True,
+                       timeout=280, cwd="/tmp", env=env)
+    assert time.time() - t0 < 270
+    assert r.returncode != 0
+    res = _last_json(r.stdout)
+    assert res["value"] is None and res["error"] and res["rank_errors"], res
+    if inject[0] == "OCM_BENCH_RAISE":
+        assert res["phase"] == "verify" and list(res["rank_errors"]) == ["5"]

@@ -1,5 +1,6 @@
 """Control-plane transport cost: remote ocm_alloc p50 with the records on TCP
-(self queue) vs an RCCL ncclAllGather tick (1-rank communicator, OCM_TICK_SELF)
+(self queue) vs an RCCL ncclAllGather tick (1-rank communicator, OCM_TICK_SELF;
+variants: graph replay over mapped slots, direct launches, round-1 copies)
 vs the socket-ring collective, on one GPU. Leases off so every allocation
 takes the full REQ_ALLOC -> DO_ALLOC -> reply path.
 
@@ -18,8 +19,8 @@ from oncilla_amd.models import workloads as wl  # noqa: E402
 from oncilla_amd.parallel import Mesh  # noqa: E402
 
 
-def run(ctrl, tick_self):
-    env = {"OCM_LEASE_BYTES": "0"}
+def run(ctrl, tick_self, **extra_env):
+    env = {"OCM_LEASE_BYTES": "0", **extra_env}
     if tick_self:
         env["OCM_TICK_SELF"] = "1"
     with Mesh(1, gpus=[0], extra_args=["--ctrl", ctrl], env=env) as m:
@@ -37,7 +38,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    out = {"tcp": run("tcp", False), "rccl_tick": run("rccl", True), "socket_tick": run("socket", True)}
+    out = {"tcp": run("tcp", False),
+           "rccl_tick": run("rccl", True),  # persistent mapped slots + graph-replayed allgather
+           "rccl_tick_nograph": run("rccl", True, OCM_TICK_GRAPH="0"),
+           "rccl_tick_r01_path": run("rccl", True, OCM_TICK_GRAPH="0", OCM_TICK_MAPPED="0"),
+           "socket_tick": run("socket", True)}
     print(json.dumps(out, indent=1))
     if a.out:
         with open(a.out, "w") as f:
