@@ -54,6 +54,8 @@ def parse():
                     help="N>1: skip the setup-time kernel autotune over the xGMI links (library defaults)")
     ap.add_argument("--no-hw-baseline", action="store_true", help="skip the N>1 runtime peer-copy extras")
     ap.add_argument("--no-optim-extra", action="store_true", help="skip the fused remote-Adam extra")
+    ap.add_argument("--no-ctrl-extra", action="store_true",
+                    help="N>1: skip the control-plane extra (alloc p50 with the records on TCP vs RCCL ticks)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -260,6 +262,58 @@ def peer_table(client, use_gpu: bool, world: int, rank: int, local_rank: int, nb
 
         row, err = _local(one)
         out[str(p)] = row if row is not None else {"error": err}
+    return out
+
+
+def ctrl_extra(dist, world: int, rank: int, local_rank: int, use_gpu: bool, samples: int = 100) -> dict:
+    """N>1, after the timed region, with the sweep's mesh gone: a fresh mesh per
+    control transport (records between daemons on persistent TCP links, then
+    on tick collectives: RCCL over xGMI on GPUs, the socket ring on CPU),
+    leases off so every allocation takes REQ_ALLOC -> DO_ALLOC -> reply
+    through the transport; every rank measures remote ocm_alloc p50 at once."""
+    import secrets
+
+    from oncilla_amd import api
+    from oncilla_amd.models import workloads as wl
+    from oncilla_amd.parallel.mesh import Mesh, free_ports
+
+    out = {}
+    kind = api.OCM_REMOTE_GPU if use_gpu else api.OCM_REMOTE_RDMA
+    for ctrl in ("tcp", "rccl" if use_gpu else "socket"):
+        ports, key = gather_obj(dist, (free_ports(world), secrets.token_hex(16)) if rank == 0 else None, world)[0]
+        ns = f"ctrl{ctrl}_{ports[0]}"
+        gpus = [local_rank if use_gpu else None for _ in range(world)]
+        if use_gpu:
+            gpus = gather_obj(dist, local_rank, world)
+        mesh = Mesh(world, gpus=gpus, ns=ns, policy="ring", ports=ports, ranks=[rank], key=key,
+                    workdir=os.path.join("/tmp", f"ocm_{ns}"), extra_args=["--ctrl", ctrl],
+                    env={"OCM_LEASE_BYTES": "0"})
+        os.makedirs(mesh.workdir, exist_ok=True)
+        up, err = _local(lambda: mesh.start(timeout=60))
+        res = gather_obj(dist, {"err": err}, world)
+        r, err = None, next((x["err"] for x in res if x["err"]), None)
+        if err is None:
+            def run():
+                with api.Client(daemon_rank=rank, gpu=(local_rank if use_gpu else None), ns=ns) as c:
+                    if ctrl != "tcp":  # the transport comes up right after the mesh is complete
+                        deadline = time.time() + 10
+                        while c.stats(rank)["ctrl_ticks"] == 0 and time.time() < deadline:
+                            c.alloc(kind, local_bytes=4096, remote_bytes=1 << 20).free()
+                    lat = wl.alloc_latency(c, kind, samples, local_bytes=4096, remote_bytes=1 << 20)
+                    lat["ticks"] = c.stats(rank)["ctrl_ticks"]
+                    return lat
+
+            r, err = _local(run)
+        res = gather_obj(dist, {"r": r, "err": err}, world)
+        _local(mesh.stop)
+        errs = [x["err"] for x in res if x["err"]]
+        if errs:
+            out[ctrl] = {"error": errs[0]}
+            continue
+        out[ctrl] = {"alloc_p50_us": round(max(x["r"]["alloc_p50_us"] for x in res), 2),
+                     "alloc_p99_us": round(max(x["r"]["alloc_p99_us"] for x in res), 2),
+                     "free_p50_us": round(max(x["r"]["free_p50_us"] for x in res), 2),
+                     "ticks_rank0": res[0]["r"]["ticks"], "samples_per_rank": samples}
     return out
 
 
@@ -482,6 +536,13 @@ def main() -> int:
             result["hw_baseline"] = baseline
         if peers:
             result["peers_from_rank0"] = peers
+        if world > 1 and not args.no_ctrl_extra:
+            # needs this process's library detached from the sweep's mesh first
+            _local(client.close)
+            client = None
+            _local(mesh.stop)
+            mesh = None
+            result["control_plane"] = ctrl_extra(dist, world, rank, local_rank, use_gpu)
     except BenchAbort as e:
         result, rc = error_result(world, args, e.phase, e.errors), 1
     except Exception as e:  # noqa: BLE001 - a collective timed out or failed: report, never hang

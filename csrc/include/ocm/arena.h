@@ -62,6 +62,8 @@ public:
     // Thread-safe bounds check for the network data server: [offset, +len)
     // inside slab `slab_id`; returns its address and tier.
     bool locate(uint32_t slab_id, uint64_t offset, uint64_t len, void **p, uint32_t *tier) const;
+    // A dup of host-tier slab `slab_id`'s memfd (the caller closes it), -1 if none.
+    int dup_slab_fd(uint32_t slab_id) const;
 
 private:
     Slab *new_slab(uint32_t tier, uint64_t bytes, bool dedicated, int *err);

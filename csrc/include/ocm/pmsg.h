@@ -39,6 +39,11 @@ int mbox_peer_uid(int fd);  // SO_PEERCRED uid, -1 on error
 // block, -1 error or peer closed.
 int mbox_send(int fd, const void *msg, size_t size, int timeout_ms);
 int mbox_recv(int fd, void *msg, size_t size, int timeout_ms);
+// The same with one file descriptor attached (SCM_RIGHTS): the capability
+// transfer of a host-tier slab (memfd) from its owner daemon to an app.
+// mbox_recv_fd sets *passed to the received fd, or -1 when none came.
+int mbox_send_fd(int fd, const void *msg, size_t size, int pass_fd, int timeout_ms);
+int mbox_recv_fd(int fd, void *msg, size_t size, int *passed, int timeout_ms);
 
 // Client-side channel to one daemon (what libocm uses).
 class Channel {

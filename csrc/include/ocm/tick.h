@@ -9,6 +9,13 @@
 // posts into an idle mesh nudges its peers awake (a 1-byte doorbell on the
 // existing mesh sockets) and everybody ticks back-to-back while traffic lasts.
 //
+// Ticks can be pipelined: up to depth() ticks queued on the GPU at once (a
+// launch-and-wait costs ~12-16 us on MI355X, a queued collective ~3.5 us,
+// profiles/rccl_tick_floor_r02.json). Whether tick k is issued is decided from
+// the gathered contents of ticks that every rank has already completed, so all
+// ranks issue the same sequence. Measured, a queued record then waits behind
+// empty ticks, so the RCCL default depth is 1 (OCM_TICK_DEPTH).
+//
 // The collective is pluggable: RcclCollective (ncclAllGather on the daemon's
 // MI355X) in production, SocketCollective (ring allgather over abstract unix
 // sockets) so the tick protocol itself is exercised multi-rank on CPU. Any
@@ -47,26 +54,28 @@ static_assert(sizeof(TickRecord) == 168, "tick record layout");
 class Collective {
 public:
     virtual ~Collective() = default;
-    // recv = concat over ranks of every rank's `bytes`-byte send buffer. 0 ok.
-    virtual int allgather(const void *send, void *recv, size_t bytes) = 0;
-    // Persistent slots (optional): when send_slot() returns a buffer, the caller
-    // may fill it in place and pass it as `send`; recv_slots() then holds the
-    // gathered slots after allgather() with recv == recv_slots().
-    virtual void *send_slot(size_t) { return nullptr; }
-    virtual const void *recv_slots() const { return nullptr; }
+    // Ring of depth() tick slots: fill send_slot(i), start(i) gathers every
+    // rank's slot i into recv_slots(i) (rank-major), test(i) reports it done.
+    // Ticks on different slots may be in flight together (stream-ordered).
+    virtual int depth() const { return 1; }
+    virtual void *send_slot(int i) = 0;
+    virtual const void *recv_slots(int i) = 0;
+    virtual int start(int i) = 0;   // 0 ok
+    virtual int test(int i) = 0;    // 1 done, 0 in flight, -1 failed
     virtual void abort() {}
     virtual const char *name() const = 0;
 };
 
 // Collective constructors block until every rank joined; `cancel` aborts them.
 // RCCL over xGMI. `id` is the ncclUniqueId (128 bytes) chosen by rank0.
-std::unique_ptr<Collective> make_rccl_collective(int gpu, int rank, int nranks, const uint8_t *id, std::string *err,
-                                                 const std::atomic<bool> *cancel);
+// `slot_bytes`: size of one rank's slot (sizeof(TickSlot)).
+std::unique_ptr<Collective> make_rccl_collective(int gpu, int rank, int nranks, const uint8_t *id, size_t slot_bytes,
+                                                 std::string *err, const std::atomic<bool> *cancel);
 // Fill a fresh ncclUniqueId (rank0). Returns 0 on success.
 int rccl_unique_id(uint8_t out[128], std::string *err);
 // Ring allgather over abstract unix sockets (same host), for CPU meshes/tests.
-std::unique_ptr<Collective> make_socket_collective(const std::string &ns, int rank, int nranks, std::string *err,
-                                                   const std::atomic<bool> *cancel);
+std::unique_ptr<Collective> make_socket_collective(const std::string &ns, int rank, int nranks, size_t slot_bytes,
+                                                   std::string *err, const std::atomic<bool> *cancel);
 
 using CollectiveFactory = std::function<std::unique_ptr<Collective>(std::string *err, const std::atomic<bool> *cancel)>;
 
@@ -109,9 +118,8 @@ private:
     std::deque<TickRecord> out_;
     std::vector<Msg> in_;
     std::atomic<bool> stop_{false}, failed_{false}, announce_{false}, up_{false};
-    std::atomic<uint64_t> ticks_{0}, wake_upto_{0};
+    std::atomic<uint64_t> ticks_{0}, wake_upto_{0}, announce_tick_{0};
     int efd_ = -1;
-    std::vector<TickSlot> recv_;
 };
 
 }  // namespace ocm

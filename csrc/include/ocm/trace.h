@@ -15,6 +15,8 @@ struct OpCounters {
     uint64_t ns_put = 0, ns_get = 0, ns_alloc = 0, ns_free = 0;
     uint64_t n_batch = 0, n_batch_ops = 0, bytes_batch = 0, ns_batch = 0;
     uint64_t n_batch_launches = 0;  // batch kernels launched outside plans (batches, remote->remote copies)
+    uint64_t n_slab_fd = 0;         // host-tier slabs imported through an fd from their owner (SCM_RIGHTS)
+    uint64_t n_slab_path = 0;       // ... through the /proc/<pid>/fd path fallback
 };
 
 bool trace_enabled();  // OCM_TRACE=0 disables the roctx ranges

@@ -74,6 +74,7 @@ const char *msg_type_str(uint32_t t) {
     case MSG_OWNED: return "MSG_OWNED";
     case MSG_OWNED_DONE: return "MSG_OWNED_DONE";
     case MSG_NODE_LINKS: return "MSG_NODE_LINKS";
+    case MSG_SLAB_FD: return "MSG_SLAB_FD";
     default: return "INVALID MSG TYPE";
     }
 }

@@ -162,6 +162,81 @@ int mbox_recv(int fd, void *msg, size_t size, int timeout_ms) {
     }
 }
 
+int mbox_send_fd(int fd, const void *msg, size_t size, int pass_fd, int timeout_ms) {
+    if (fd < 0) OCM_FAIL(-1, "send on closed mailbox");
+    struct iovec iov = {const_cast<void *>(msg), size};
+    union {
+        char buf[CMSG_SPACE(sizeof(int))];
+        struct cmsghdr align;
+    } ctl;
+    std::memset(&ctl, 0, sizeof(ctl));
+    struct msghdr mh;
+    std::memset(&mh, 0, sizeof(mh));
+    mh.msg_iov = &iov;
+    mh.msg_iovlen = 1;
+    if (pass_fd >= 0) {
+        mh.msg_control = ctl.buf;
+        mh.msg_controllen = sizeof(ctl.buf);
+        struct cmsghdr *c = CMSG_FIRSTHDR(&mh);
+        c->cmsg_level = SOL_SOCKET;
+        c->cmsg_type = SCM_RIGHTS;
+        c->cmsg_len = CMSG_LEN(sizeof(int));
+        std::memcpy(CMSG_DATA(c), &pass_fd, sizeof(int));
+    }
+    for (;;) {
+        ssize_t n = sendmsg(fd, &mh, MSG_NOSIGNAL);
+        if (n == (ssize_t)size) return 1;
+        if (n >= 0) OCM_FAIL(-1, "short mailbox send (%zd)", n);
+        if (errno == EINTR) continue;
+        if (errno == EAGAIN || errno == EWOULDBLOCK) {
+            if (timeout_ms == 0) return 0;
+            int w = wait_fd(fd, POLLOUT, timeout_ms);
+            if (w <= 0) return w;
+            continue;
+        }
+        OCM_FAIL(-1, "mailbox send: %s", strerror(errno));
+    }
+}
+
+int mbox_recv_fd(int fd, void *msg, size_t size, int *passed, int timeout_ms) {
+    *passed = -1;
+    if (fd < 0) OCM_FAIL(-1, "recv on closed mailbox");
+    for (;;) {
+        struct iovec iov = {msg, size};
+        union {
+            char buf[CMSG_SPACE(sizeof(int))];
+            struct cmsghdr align;
+        } ctl;
+        struct msghdr mh;
+        std::memset(&mh, 0, sizeof(mh));
+        mh.msg_iov = &iov;
+        mh.msg_iovlen = 1;
+        mh.msg_control = ctl.buf;
+        mh.msg_controllen = sizeof(ctl.buf);
+        ssize_t n = recvmsg(fd, &mh, MSG_CMSG_CLOEXEC);
+        if (n > 0) {
+            for (struct cmsghdr *c = CMSG_FIRSTHDR(&mh); c; c = CMSG_NXTHDR(&mh, c))
+                if (c->cmsg_level == SOL_SOCKET && c->cmsg_type == SCM_RIGHTS && c->cmsg_len >= CMSG_LEN(sizeof(int)))
+                    std::memcpy(passed, CMSG_DATA(c), sizeof(int));
+        }
+        if (n == (ssize_t)size) return 1;
+        if (*passed >= 0) {
+            ::close(*passed);
+            *passed = -1;
+        }
+        if (n == 0) OCM_FAIL(-1, "mailbox peer closed");
+        if (n > 0) OCM_FAIL(-1, "short mailbox record (%zd bytes)", n);
+        if (errno == EINTR) continue;
+        if (errno == EAGAIN || errno == EWOULDBLOCK) {
+            if (timeout_ms == 0) return 0;
+            int w = wait_fd(fd, POLLIN, timeout_ms);
+            if (w <= 0) return w;
+            continue;
+        }
+        OCM_FAIL(-1, "mailbox recv: %s", strerror(errno));
+    }
+}
+
 int Channel::connect(const std::string &name, int timeout_ms) {
     close();
     fd_ = mbox_connect(name, timeout_ms);

@@ -5,6 +5,7 @@
 // there, src/rdma_server.c:40-236), including the leak it fixes (src/alloc.c:171).
 #include "ocm/arena.h"
 
+#include <fcntl.h>
 #include <hip/hip_runtime_api.h>
 #include <sys/mman.h>
 #include <sys/syscall.h>
@@ -69,6 +70,13 @@ bool Arena::locate(uint32_t slab_id, uint64_t offset, uint64_t len, void **p, ui
     *p = static_cast<char *>(s.base) + offset;
     *tier = s.tier;
     return true;
+}
+
+int Arena::dup_slab_fd(uint32_t slab_id) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = slabs_.find(slab_id);
+    if (it == slabs_.end() || it->second->tier != TIER_HOST || it->second->memfd < 0) return -1;
+    return fcntl(it->second->memfd, F_DUPFD_CLOEXEC, 0);
 }
 
 uint64_t Arena::capacity(uint32_t tier) const {

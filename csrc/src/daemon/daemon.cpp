@@ -13,6 +13,7 @@
 #include <hip/hip_runtime_api.h>
 #include <signal.h>
 #include <sys/epoll.h>
+#include <sys/prctl.h>
 #include <sys/signalfd.h>
 #include <sys/syscall.h>
 #include <time.h>
@@ -89,6 +90,11 @@ NodeConfig Daemon::my_config() const {
 
 int Daemon::init() {
     std::string err;
+    if (const char *nd = std::getenv("OCM_NONDUMPABLE"); nd && std::strcmp(nd, "1") == 0) {
+        // Hardening: no ptrace / core dumps, and /proc/<pid>/fd becomes root-only.
+        // Apps still map host-tier slabs: they receive the memfds (MSG_SLAB_FD).
+        if (prctl(PR_SET_DUMPABLE, 0, 0, 0, 0) != 0) OCM_WARN("prctl(PR_SET_DUMPABLE): %s", strerror(errno));
+    }
     if (parse_nodefile(cfg_.nodefile, &nf_, &err) != 0) {
         OCM_ERR("%s", err.c_str());
         return -1;
@@ -498,6 +504,17 @@ void Daemon::on_app_conn(int fd, uint32_t events) {
         if (m.type == MSG_CONNECT) {
             it->second.app_pid = m.pid;
             app_connect(m, fd);
+            continue;
+        }
+        if (m.type == MSG_SLAB_FD) {
+            // Capability transfer of a host-tier slab to an app of our uid (checked at
+            // accept): the memfd itself, so no /proc path (ptrace rules, hidepid) is needed.
+            Msg r = m;
+            r.status = MSG_RESPONSE;
+            const int sfd = arena_ ? arena_->dup_slab_fd(m.u.region.slab_id) : -1;
+            r.err = sfd >= 0 ? 0 : ENOENT;
+            if (mbox_send_fd(fd, &r, kMsgBytes, sfd, 1000) != 1) OCM_WARN("rank %d: slab fd reply to pid %d failed", rank_, (int)m.pid);
+            if (sfd >= 0) close(sfd);
             continue;
         }
         handle_app_msg(m);

@@ -710,13 +710,13 @@ void Daemon::start_tick(const uint8_t *id) {
         std::vector<uint8_t> uid(id, id + 128);
         const int gpu = gpu_, rank = rank_, n = n_;
         f = [uid, gpu, rank, n](std::string *err, const std::atomic<bool> *cancel) {
-            return make_rccl_collective(gpu, rank, n, uid.data(), err, cancel);
+            return make_rccl_collective(gpu, rank, n, uid.data(), sizeof(TickSlot), err, cancel);
         };
     } else {
         const std::string ns = ns_;
         const int rank = rank_, n = n_;
         f = [ns, rank, n](std::string *err, const std::atomic<bool> *cancel) {
-            return make_socket_collective(ns, rank, n, err, cancel);
+            return make_socket_collective(ns, rank, n, sizeof(TickSlot), err, cancel);
         };
     }
     tick_ = std::make_unique<TickTransport>(rank_, n_, f);

@@ -8,6 +8,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
@@ -21,47 +22,67 @@ namespace {
 
 // ---------------------------------------------------------------- RCCL
 
-// Each tick is ONE replay of a captured ncclAllGather over persistent slots:
-// the send slot and the gathered slots live in pinned, device-mapped host
-// memory, so the tick thread writes its records straight into the send slot
-// and reads the peers' records straight out of the receive slots (no H2D /
-// D2H copies, no per-tick allocation), and the collective is launched as a
-// HIP graph (one launch, no RCCL enqueue work per tick). Completion is a
-// spin on the stream, bounded by abort requests and RCCL async errors.
-// OCM_TICK_GRAPH=0 launches ncclAllGather directly; OCM_TICK_MAPPED=0 keeps
-// the slots in HBM with explicit copies (the round-1 path, for A/B).
+// RCCL over xGMI: a ring of depth() slot pairs in pinned, device-mapped host
+// memory (OCM_TICK_MAPPED=0: HBM slots with H2D/D2H copies queued around the
+// collective), one ncclAllGather per tick queued on one stream, an event per
+// slot for completion. The tick thread writes its records straight into the
+// send slot before queueing the tick and reads the peers' records straight
+// out of the receive slots once the slot's event has fired.
+// OCM_TICK_DEPTH (default 1) ticks may be queued at once.
 class RcclCollective : public Collective {
 public:
     ~RcclCollective() override {
-        if (exec_) (void)hipGraphExecDestroy(exec_);
-        if (graph_) (void)hipGraphDestroy(graph_);
         if (comm_) {
             if (aborted_)
                 (void)ncclCommAbort(comm_);
             else
                 (void)ncclCommDestroy(comm_);
         }
-        if (stream_) (void)hipStreamDestroy(stream_);
-        if (mapped_) {
-            if (hsend_) (void)hipHostFree(hsend_);
-            if (hrecv_) (void)hipHostFree(hrecv_);
-        } else {
-            if (dsend_) (void)hipFree(dsend_);
-            if (drecv_) (void)hipFree(drecv_);
-            if (hsend_) (void)hipHostFree(hsend_);
-            if (hrecv_) (void)hipHostFree(hrecv_);
+        for (auto &sl : ring_) {
+            if (sl.ev) (void)hipEventDestroy(sl.ev);
+            if (sl.hsend) (void)hipHostFree(sl.hsend);
+            if (sl.hrecv) (void)hipHostFree(sl.hrecv);
+            if (!mapped_) {
+                if (sl.dsend) (void)hipFree(sl.dsend);
+                if (sl.drecv) (void)hipFree(sl.drecv);
+            }
         }
+        if (stream_) (void)hipStreamDestroy(stream_);
     }
-    int init(int gpu, int rank, int n, const uint8_t *id, std::string *err) {
+    int init(int gpu, int rank, int n, const uint8_t *id, size_t bytes, std::string *err) {
         gpu_ = gpu;
         n_ = n;
-        const char *g = std::getenv("OCM_TICK_GRAPH");
+        bytes_ = bytes;
         const char *m = std::getenv("OCM_TICK_MAPPED");
-        use_graph_ = !(g && std::strcmp(g, "0") == 0);
         mapped_ = !(m && std::strcmp(m, "0") == 0);
+        const char *d = std::getenv("OCM_TICK_DEPTH");
+        // Depth 1 by default: measured on MI355X, queueing ticks ahead makes a
+        // record wait behind empty ones (profiles/ctrl_probe_r02b.json).
+        const int depth = std::max(1, std::min(d && *d ? std::atoi(d) : 1, 64));
         if (hipSetDevice(gpu) != hipSuccess || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
             *err = "rccl: no stream on gpu " + std::to_string(gpu);
             return -1;
+        }
+        ring_.resize((size_t)depth);
+        for (auto &sl : ring_) {
+            bool ok = hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) == hipSuccess;
+            if (mapped_) {
+                const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable;
+                ok = ok && hipHostMalloc(&sl.hsend, bytes, fl) == hipSuccess &&
+                     hipHostMalloc(&sl.hrecv, bytes * (size_t)n, fl) == hipSuccess &&
+                     hipHostGetDevicePointer(&sl.dsend, sl.hsend, 0) == hipSuccess &&
+                     hipHostGetDevicePointer(&sl.drecv, sl.hrecv, 0) == hipSuccess;
+            } else {
+                ok = ok && hipMalloc(&sl.dsend, bytes) == hipSuccess && hipMalloc(&sl.drecv, bytes * (size_t)n) == hipSuccess &&
+                     hipHostMalloc(&sl.hsend, bytes) == hipSuccess && hipHostMalloc(&sl.hrecv, bytes * (size_t)n) == hipSuccess;
+            }
+            if (!ok) {
+                (void)hipGetLastError();
+                *err = "rccl: no memory for the tick slots";
+                return -1;
+            }
+            std::memset(sl.hsend, 0, bytes);
+            std::memset(sl.hrecv, 0, bytes * (size_t)n);
         }
         ncclUniqueId uid;
         std::memcpy(&uid, id, sizeof(uid));
@@ -85,96 +106,58 @@ public:
         return 0;
     }
     void request_abort() { abort_req_ = true; }
-    void *send_slot(size_t bytes) override {
-        if (bytes != cap_ && setup(bytes) != 0) return nullptr;
-        return hsend_;
-    }
-    const void *recv_slots() const override { return hrecv_; }
-    int allgather(const void *send, void *recv, size_t bytes) override {
+    int depth() const override { return (int)ring_.size(); }
+    void *send_slot(int i) override { return ring_[(size_t)i].hsend; }
+    const void *recv_slots(int i) override { return ring_[(size_t)i].hrecv; }
+    int start(int i) override {
         if (aborted_) return -1;
+        Slot &sl = ring_[(size_t)i];
         (void)hipSetDevice(gpu_);
-        if (bytes != cap_ && setup(bytes) != 0) return -1;
-        if (send != hsend_) std::memcpy(hsend_, send, bytes);
-        if (!mapped_ && hipMemcpyAsync(dsend_, hsend_, bytes, hipMemcpyHostToDevice, stream_) != hipSuccess) return -1;
-        if (exec_) {
-            if (hipGraphLaunch(exec_, stream_) != hipSuccess) return -1;
-        } else if (ncclAllGather(dsend_, drecv_, bytes, ncclUint8, comm_, stream_) != ncclSuccess) {
+        if (!mapped_ && hipMemcpyAsync(sl.dsend, sl.hsend, bytes_, hipMemcpyHostToDevice, stream_) != hipSuccess) return -1;
+        if (ncclAllGather(sl.dsend, sl.drecv, bytes_, ncclUint8, comm_, stream_) != ncclSuccess) return -1;
+        if (!mapped_ && hipMemcpyAsync(sl.hrecv, sl.drecv, bytes_ * (size_t)n_, hipMemcpyDeviceToHost, stream_) != hipSuccess)
+            return -1;
+        return hipEventRecord(sl.ev, stream_) == hipSuccess ? 0 : -1;
+    }
+    int test(int i) override {
+        // Bounded by abort requests and RCCL async errors: a dead peer never
+        // joins the collective, so the event would never fire.
+        if (abort_req_.load()) {
+            aborted_ = true;
             return -1;
         }
-        if (!mapped_ && hipMemcpyAsync(hrecv_, drecv_, bytes * n_, hipMemcpyDeviceToHost, stream_) != hipSuccess)
-            return -1;
-        // Wait without blocking forever: a dead peer never joins the collective.
-        for (unsigned spins = 1;; spins++) {
-            hipError_t q = hipStreamQuery(stream_);
-            if (q == hipSuccess) break;
-            if (q != hipErrorNotReady) return -1;
-            if (abort_req_.load()) {
-                aborted_ = true;
+        const hipError_t q = hipEventQuery(ring_[(size_t)i].ev);
+        if (q == hipSuccess) return 1;
+        if (q != hipErrorNotReady) return -1;
+        if ((++polls_ & 63) == 0) {
+            ncclResult_t async = ncclSuccess;
+            if (ncclCommGetAsyncError(comm_, &async) == ncclSuccess && async != ncclSuccess && async != ncclInProgress)
                 return -1;
-            }
-            if ((spins & 63) == 0) {
-                ncclResult_t async = ncclSuccess;
-                if (ncclCommGetAsyncError(comm_, &async) == ncclSuccess && async != ncclSuccess &&
-                    async != ncclInProgress)
-                    return -1;
-            }
         }
-        if (recv != hrecv_) std::memcpy(recv, hrecv_, bytes * n_);
         return 0;
     }
     void abort() override { abort_req_ = true; }
     const char *name() const override { return "rccl"; }
 
 private:
-    int setup(size_t bytes) {
-        if (cap_) return -1;  // the slot size is fixed for the transport's life
-        if (mapped_) {
-            const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable;
-            if (hipHostMalloc(&hsend_, bytes, fl) != hipSuccess || hipHostMalloc(&hrecv_, bytes * n_, fl) != hipSuccess ||
-                hipHostGetDevicePointer(&dsend_, hsend_, 0) != hipSuccess ||
-                hipHostGetDevicePointer(&drecv_, hrecv_, 0) != hipSuccess) {
-                (void)hipGetLastError();
-                return -1;
-            }
-        } else if (hipMalloc(&dsend_, bytes) != hipSuccess || hipMalloc(&drecv_, bytes * n_) != hipSuccess ||
-                   hipHostMalloc(&hsend_, bytes) != hipSuccess || hipHostMalloc(&hrecv_, bytes * n_) != hipSuccess) {
-            (void)hipGetLastError();
-            return -1;
-        }
-        std::memset(hsend_, 0, bytes);
-        std::memset(hrecv_, 0, bytes * n_);
-        cap_ = bytes;
-        if (use_graph_) {
-            // Capture once; every rank captures the same single collective, so replays stay matched.
-            hipGraph_t g = nullptr;
-            bool ok = hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal) == hipSuccess;
-            const bool queued = ok && ncclAllGather(dsend_, drecv_, bytes, ncclUint8, comm_, stream_) == ncclSuccess;
-            ok = ok && hipStreamEndCapture(stream_, &g) == hipSuccess && queued;
-            ok = ok && hipGraphInstantiate(&exec_, g, nullptr, nullptr, 0) == hipSuccess;
-            if (g) graph_ = g;
-            if (!ok) {
-                (void)hipGetLastError();
-                if (exec_) (void)hipGraphExecDestroy(exec_);
-                exec_ = nullptr;
-                OCM_WARN("rccl tick: graph capture of the allgather failed; launching it directly");
-            }
-        }
-        return 0;
-    }
+    struct Slot {
+        void *hsend = nullptr, *hrecv = nullptr, *dsend = nullptr, *drecv = nullptr;
+        hipEvent_t ev = nullptr;
+    };
     int gpu_ = 0, n_ = 1;
+    size_t bytes_ = 0;
+    bool mapped_ = true;
+    unsigned polls_ = 0;
     ncclComm_t comm_ = nullptr;
     hipStream_t stream_ = nullptr;
-    void *dsend_ = nullptr, *drecv_ = nullptr, *hsend_ = nullptr, *hrecv_ = nullptr;
-    size_t cap_ = 0;
-    bool use_graph_ = true, mapped_ = true;
-    hipGraph_t graph_ = nullptr;
-    hipGraphExec_t exec_ = nullptr;
+    std::vector<Slot> ring_;
     std::atomic<bool> abort_req_{false};
     bool aborted_ = false;
 };
 
 // ---------------------------------------------------------------- sockets
 
+// Ring allgather over abstract unix sockets, done inside start() (depth 1).
 class SocketCollective : public Collective {
 public:
     ~SocketCollective() override {
@@ -182,9 +165,12 @@ public:
         if (right_ >= 0) close(right_);
         if (listen_ >= 0) close(listen_);
     }
-    int init(const std::string &ns, int rank, int n, std::string *err) {
+    int init(const std::string &ns, int rank, int n, size_t bytes, std::string *err) {
         rank_ = rank;
         n_ = n;
+        bytes_ = bytes;
+        send_.assign(bytes, 0);
+        recv_.assign(bytes * (size_t)n, 0);
         if (n == 1) return 0;
         listen_ = mbox_listen("ocm_" + ns + "_coll" + std::to_string(rank), 4);
         if (listen_ < 0) {
@@ -203,18 +189,21 @@ public:
         }
         return 0;
     }
-    int allgather(const void *send, void *recv, size_t bytes) override {
-        char *out = static_cast<char *>(recv);
-        std::memcpy(out + (size_t)rank_ * bytes, send, bytes);
+    void *send_slot(int) override { return send_.data(); }
+    const void *recv_slots(int) override { return recv_.data(); }
+    int start(int) override {
+        char *out = recv_.data();
+        std::memcpy(out + (size_t)rank_ * bytes_, send_.data(), bytes_);
         // Ring: at step s send block (rank - s) right, receive block (rank - s - 1) from the left.
         for (int s = 0; s < n_ - 1; s++) {
             const int sb = ((rank_ - s) % n_ + n_) % n_;
             const int rb = ((rank_ - s - 1) % n_ + n_) % n_;
-            if (xfer(right_, out + (size_t)sb * bytes, bytes, true) != 0) return -1;
-            if (xfer(left_, out + (size_t)rb * bytes, bytes, false) != 0) return -1;
+            if (xfer(right_, out + (size_t)sb * bytes_, bytes_, true) != 0) return -1;
+            if (xfer(left_, out + (size_t)rb * bytes_, bytes_, false) != 0) return -1;
         }
         return 0;
     }
+    int test(int) override { return aborted_ ? -1 : 1; }
     void abort() override {
         aborted_ = true;
         if (left_ >= 0) shutdown(left_, SHUT_RDWR);
@@ -242,6 +231,8 @@ private:
         return aborted_ ? -1 : 0;
     }
     int rank_ = 0, n_ = 1, left_ = -1, right_ = -1, listen_ = -1;
+    size_t bytes_ = 0;
+    std::vector<char> send_, recv_;
     std::atomic<bool> aborted_{false};
 };
 
@@ -259,8 +250,8 @@ int rccl_unique_id(uint8_t out[128], std::string *err) {
     return 0;
 }
 
-std::unique_ptr<Collective> make_rccl_collective(int gpu, int rank, int nranks, const uint8_t *id, std::string *err,
-                                                 const std::atomic<bool> *cancel) {
+std::unique_ptr<Collective> make_rccl_collective(int gpu, int rank, int nranks, const uint8_t *id, size_t slot_bytes,
+                                                 std::string *err, const std::atomic<bool> *cancel) {
     auto c = std::make_unique<RcclCollective>();
     std::atomic<bool> done{false};
     std::thread watch;
@@ -273,17 +264,17 @@ std::unique_ptr<Collective> make_rccl_collective(int gpu, int rank, int nranks, 
             }
         });
     }
-    int rc = c->init(gpu, rank, nranks, id, err);
+    int rc = c->init(gpu, rank, nranks, id, slot_bytes, err);
     done = true;
     if (watch.joinable()) watch.join();
     if (rc != 0) return nullptr;
     return c;
 }
 
-std::unique_ptr<Collective> make_socket_collective(const std::string &ns, int rank, int nranks, std::string *err,
-                                                   const std::atomic<bool> *) {
+std::unique_ptr<Collective> make_socket_collective(const std::string &ns, int rank, int nranks, size_t slot_bytes,
+                                                   std::string *err, const std::atomic<bool> *) {
     auto c = std::make_unique<SocketCollective>();
-    if (c->init(ns, rank, nranks, err) != 0) return nullptr;
+    if (c->init(ns, rank, nranks, slot_bytes, err) != 0) return nullptr;
     return c;
 }
 
@@ -292,7 +283,6 @@ std::unique_ptr<Collective> make_socket_collective(const std::string &ns, int ra
 TickTransport::TickTransport(int rank, int nranks, CollectiveFactory factory)
     : rank_(rank), n_(nranks), factory_(std::move(factory)) {
     efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
-    recv_.resize((size_t)n_);
 }
 
 TickTransport::~TickTransport() {
@@ -354,7 +344,7 @@ void TickTransport::wake_at(uint64_t tick) {
 
 bool TickTransport::take_announce(uint64_t *tick) {
     if (!announce_.exchange(false)) return false;
-    *tick = ticks_.load() + 1;
+    *tick = announce_tick_.load();
     return true;
 }
 
@@ -366,14 +356,13 @@ std::vector<TickRecord> TickTransport::take_unsent() {
 }
 
 void TickTransport::run() {
-    // Every rank runs the same state machine over identical allgather
-    // outputs, so all ranks agree on when to tick: after a tick that carried
-    // traffic everybody ticks kBusyTicks more times; an idle rank ticks again
-    // only for its own records or a peer's wake-up for the current tick count.
-    constexpr int kBusyTicks = 64;
-    int busy_left = 0;
-    TickSlot mine;
-    const TickSlot *send = &mine;
+    // Every rank runs the same state machine over identical allgather outputs,
+    // so all ranks issue the same ticks: after completing a tick that carried
+    // traffic, everybody extends its target by kBusyTicks; an idle rank issues
+    // a tick only for its own records (announced to the peers) or a peer's
+    // wake-up. Up to depth() ticks are queued at once; tick k's records are
+    // read from ring slot (k - 1) % depth.
+    constexpr uint64_t kBusyTicks = 64;
     std::string err;
     std::unique_ptr<Collective> c = factory_(&err, &stop_);
     auto signal = [this] {
@@ -391,66 +380,88 @@ void TickTransport::run() {
         std::lock_guard<std::mutex> lk(mu_);
         coll_ = std::move(c);
     }
+    Collective *coll = coll_.get();
+    const uint64_t depth = (uint64_t)std::max(1, coll->depth());
     up_ = true;
     signal();
+    uint64_t issued = 0, done = 0, target = 0;
+    auto fail = [&] {
+        if (!stop_) OCM_WARN("rank %d: %s tick transport failed; falling back to TCP", rank_, coll->name());
+        failed_ = true;
+        signal();
+    };
     while (!stop_) {
         {
             std::unique_lock<std::mutex> lk(mu_);
-            if (busy_left == 0) {
-                cv_.wait(lk, [&] {
-                    return stop_.load() || !out_.empty() || wake_upto_.load() >= ticks_.load() + 1;
-                });
+            if (done == issued && issued >= target) {
+                // Idle: sleep until there is something to send or a peer calls a tick.
+                cv_.wait(lk, [&] { return stop_.load() || !out_.empty() || wake_upto_.load() > target; });
                 if (stop_) break;
-                if (!out_.empty() && wake_upto_.load() < ticks_.load() + 1) announce_ = true;  // we start the burst
+                if (wake_upto_.load() <= target) {
+                    // We start the burst: the peers must join tick issued + 1.
+                    announce_tick_ = issued + 1;
+                    announce_ = true;
+                    target = issued + 1;
+                }
             }
-            // Fill the collective's own send slot when it has one (no extra copy).
-            TickSlot *slot = static_cast<TickSlot *>(coll_->send_slot(sizeof(TickSlot)));
-            if (!slot) slot = &mine;
-            slot->count = 0;
-            while (!out_.empty() && slot->count < (uint32_t)kTickMsgs) {
-                slot->rec[slot->count++] = out_.front();
-                out_.pop_front();
+            target = std::max(target, wake_upto_.load());
+            // Queue ticks up to the target, at most `depth` in flight.
+            while (issued < target && issued - done < depth) {
+                const int i = (int)(issued % depth);
+                TickSlot *slot = static_cast<TickSlot *>(coll->send_slot(i));
+                slot->count = 0;
+                while (!out_.empty() && slot->count < (uint32_t)kTickMsgs) {
+                    slot->rec[slot->count++] = out_.front();
+                    out_.pop_front();
+                }
+                slot->busy = out_.empty() ? 0 : 1;
+                if (announce_.load()) signal();  // let the event loop wake the peers first
+                lk.unlock();
+                const int rc = coll->start(i);
+                lk.lock();
+                if (rc != 0) break;
+                issued++;
             }
-            slot->busy = out_.empty() ? 0 : 1;
-            send = slot;
+            if (issued < target && issued - done < depth) {  // start() failed
+                lk.unlock();
+                fail();
+                break;
+            }
         }
-        if (announce_.load()) {
-            // Let the event loop nudge the peers for this tick before we block in it.
-            uint64_t one = 1;
-            ssize_t w = write(efd_, &one, sizeof(one));
-            (void)w;
+        if (done == issued) continue;
+        const int i = (int)(done % depth);
+        int t = 0;
+        // Spin on the oldest tick without the queue lock (the event loop posts
+        // under it); come back to queue more ticks only when there is room.
+        for (unsigned spins = 0; !stop_; spins++) {
+            t = coll->test(i);
+            if (t != 0) break;
+            if (issued - done < depth && (spins & 15) == 15) break;
         }
-        const TickSlot *got = static_cast<const TickSlot *>(coll_->recv_slots());
-        if (coll_->allgather(send, got ? const_cast<TickSlot *>(got) : recv_.data(), sizeof(TickSlot)) != 0) {
-            if (!stop_) OCM_WARN("rank %d: %s tick transport failed; falling back to TCP", rank_, coll_->name());
-            failed_ = true;
-            uint64_t one = 1;
-            ssize_t w = write(efd_, &one, sizeof(one));
-            (void)w;
+        if (t < 0) {
+            fail();
             break;
         }
-        const uint64_t t = ++ticks_;
+        if (t == 0) continue;
+        const TickSlot *got = static_cast<const TickSlot *>(coll->recv_slots(i));
         bool traffic = false;
         size_t delivered = 0;
         {
             std::lock_guard<std::mutex> lk(mu_);
             for (int k = 0; k < n_; k++) {
-                const TickSlot &s = (got ? got : recv_.data())[k];
-                if (s.count || s.busy) traffic = true;
-                for (uint32_t i = 0; i < s.count && i < (uint32_t)kTickMsgs; i++)
-                    if (s.rec[i].dest == rank_) {
-                        in_.push_back(s.rec[i].msg);
+                const TickSlot &sl = got[k];
+                if (sl.count || sl.busy) traffic = true;
+                for (uint32_t r = 0; r < sl.count && r < (uint32_t)kTickMsgs; r++)
+                    if (sl.rec[r].dest == rank_) {
+                        in_.push_back(sl.rec[r].msg);
                         delivered++;
                     }
             }
         }
-        busy_left = traffic ? kBusyTicks : (busy_left > 0 ? busy_left - 1 : 0);
-        (void)t;
-        if (delivered) {
-            uint64_t one = 1;
-            ssize_t w = write(efd_, &one, sizeof(one));
-            (void)w;
-        }
+        done++;
+        ticks_ = done;
+        if (traffic) target = std::max(target, done + kBusyTicks);
+        if (delivered) signal();
     }
 }
 

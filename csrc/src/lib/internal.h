@@ -174,6 +174,7 @@ struct State {
     unsigned long long svc_idle_ticks = 200000ull;  // 2 ms at 100 MHz: live only during bursts of small ops
     // network tier
     std::map<std::string, NetConn> net_conns;  // "ip:port#stream" -> connection
+    std::map<int, int> fd_chans;               // owner rank -> mailbox connection for slab fds (MSG_SLAB_FD)
     int net_streams = 4;                       // OCM_NET_STREAMS: parallel connections per owner
     uint64_t net_split_min = 1ull << 20;       // OCM_NET_SPLIT_MIN: smallest part worth its own stream
     // Local GPU halves: stream-ordered pool (no device-wide sync in free, freed
@@ -236,6 +237,8 @@ inline int log2_exact(uint64_t v) {
 
 // ---- import cache (runtime.cpp)
 int import_extent(Extent &e);
+int slab_fd_from_owner(int owner, uint32_t slab_id);
+void close_fd_chans();
 void release_extent(const Extent &e, bool force);
 
 // ---- pinned host arena for local halves (runtime.cpp)

@@ -142,6 +142,7 @@ int ocm_tini(void) {
     s.imports.clear();
     service_stop();
     net_close_all();
+    close_fd_chans();
     for (auto st : s.lanes) {
         DeviceGuard g(s.device);
         (void)hipStreamSynchronize(st);
@@ -634,11 +635,12 @@ const char *ocm_last_error(void) { return last_error(); }
 // ---------------- internal hooks for tests and benchmarks (not part of the ABI) ----------------
 
 // Per-process operation counters (see ocm/trace.h): 17 x uint64.
-void ocm_x_counters(uint64_t out[17]) {
+void ocm_x_counters(uint64_t out[19]) {
     const OpCounters &c = S().ctr;
-    const uint64_t v[17] = {c.n_put,  c.n_get,    c.bytes_put, c.bytes_get,   c.n_alloc,     c.n_free,
+    const uint64_t v[19] = {c.n_put,  c.n_get,    c.bytes_put, c.bytes_get,   c.n_alloc,     c.n_free,
                             c.n_copy, c.bytes_copy, c.ns_put,  c.ns_get,      c.ns_alloc,    c.ns_free,
-                            c.n_batch, c.n_batch_ops, c.bytes_batch, c.ns_batch, c.n_batch_launches};
+                            c.n_batch, c.n_batch_ops, c.bytes_batch, c.ns_batch, c.n_batch_launches,
+                            c.n_slab_fd, c.n_slab_path};
     std::memcpy(out, v, sizeof(v));
 }
 
@@ -647,7 +649,7 @@ void ocm_x_counters(uint64_t out[17]) {
 // exp_avg / exp_avg_sq of element 0 sit at byte offsets m_off / v_off of the
 // remote half. hp = {b1, b2, eps, weight_decay, step_size, 1/sqrt(bias_correction2),
 // adamw_decay}: adamw_decay = 1 - lr * weight_decay selects AdamW (decoupled decay;
-// weight_decay then unused), 0 selects Adam with the L2 term.
+// weight_decay then unused), NaN selects Adam with the L2 term.
 // Queued on `stream` (e.g. torch's current stream); no host wait.
 static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64_t w_off, uint64_t m_off,
                        uint64_t v_off, const float hp[7], void *stream, bool bf16);

@@ -80,6 +80,39 @@ bool is_pair(enum ocm_kind k) { return k == OCM_REMOTE_GPU || k == OCM_REMOTE_RD
 
 // ---------------------------------------------------------------- import cache
 
+// Ask the owner daemon for host-tier slab `slab_id`'s memfd over its mailbox
+// (a side connection per owner, kept open). -1 when it cannot be had.
+int slab_fd_from_owner(int owner, uint32_t slab_id) {
+    State &s = S();
+    auto it = s.fd_chans.find(owner);
+    if (it == s.fd_chans.end()) {
+        const int fd = mbox_connect(daemon_mailbox_name(owner, s.ns), 2000);
+        if (fd < 0) return -1;
+        it = s.fd_chans.emplace(owner, fd).first;
+    }
+    Msg q = new_msg(MSG_SLAB_FD);
+    q.seq = ++s.seq;
+    q.u.region.owner_rank = owner;
+    q.u.region.slab_id = slab_id;
+    q.u.region.tier = TIER_HOST;
+    Msg r;
+    int got = -1;
+    if (mbox_send(it->second, &q, kMsgBytes, 5000) != 1 || mbox_recv_fd(it->second, &r, kMsgBytes, &got, 5000) != 1 ||
+        r.seq != q.seq || r.type != MSG_SLAB_FD || r.err) {
+        if (got >= 0) close(got);
+        close(it->second);
+        s.fd_chans.erase(it);  // the stream may be out of step: reconnect next time
+        return -1;
+    }
+    return got;
+}
+
+void close_fd_chans() {
+    State &s = S();
+    for (auto &kv : s.fd_chans) close(kv.second);
+    s.fd_chans.clear();
+}
+
 int import_extent(Extent &e) {
     State &s = S();
     const Region &r = e.r;
@@ -122,11 +155,20 @@ int import_extent(Extent &e) {
             if (err != hipSuccess) OCM_FAIL(-1, "hipIpcOpenMemHandle(owner %d slab %u): %s", r.owner_rank, r.slab_id, hipGetErrorString(err));
             m.dbase = static_cast<char *>(p);
         } else {
-            char path[kHandleBytes + 1];
-            std::memcpy(path, r.handle, kHandleBytes);
-            path[kHandleBytes] = 0;
-            int fd = open(path, O_RDWR | O_CLOEXEC);
-            if (fd < 0) OCM_FAIL(-1, "open host-tier slab %s: %s", path, strerror(errno));
+            // The owner hands us the slab's memfd (SCM_RIGHTS); the /proc path in
+            // the handle is the fallback (it needs ptrace access to the owner).
+            int fd = slab_fd_from_owner(r.owner_rank, r.slab_id);
+            if (fd >= 0) {
+                s.ctr.n_slab_fd++;
+            } else {
+                char path[kHandleBytes + 1];
+                std::memcpy(path, r.handle, kHandleBytes);
+                path[kHandleBytes] = 0;
+                fd = open(path, O_RDWR | O_CLOEXEC);
+                if (fd < 0) OCM_FAIL(-1, "host-tier slab %u of rank %d: no fd from its owner, and open(%s): %s", r.slab_id,
+                                     r.owner_rank, path, strerror(errno));
+                s.ctr.n_slab_path++;
+            }
             void *p = mmap(nullptr, r.slab_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
             close(fd);
             if (p == MAP_FAILED) OCM_FAIL(-1, "mmap host-tier slab: %s", strerror(errno));

@@ -41,6 +41,10 @@ def test_bench_multi_rank(native, n):
     # the setup-time autotune ran its all-rank protocol and agreed on one pick per direction
     assert res["autotune"]["ranks"] == n and res["autotune"]["get"] in res["autotune"]["GiBps"], res["autotune"]
     assert len(res["alloc_p50_us_per_rank"]) == n
+    # control-plane extra: the same allocation path on TCP links and on socket-collective ticks
+    cp = res["control_plane"]
+    assert cp["tcp"]["alloc_p50_us"] > 0 and cp["tcp"]["ticks_rank0"] == 0, cp
+    assert cp["socket"]["alloc_p50_us"] > 0 and cp["socket"]["ticks_rank0"] > 0, cp
 
 
 def test_bench_extras_helpers_run(native):

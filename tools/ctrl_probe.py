@@ -1,6 +1,6 @@
 """Control-plane transport cost: remote ocm_alloc p50 with the records on TCP
 (self queue) vs an RCCL ncclAllGather tick (1-rank communicator, OCM_TICK_SELF;
-variants: graph replay over mapped slots, direct launches, round-1 copies)
+variants: pipeline depth 4 / 1, slots in mapped host memory / HBM with copies)
 vs the socket-ring collective, on one GPU. Leases off so every allocation
 takes the full REQ_ALLOC -> DO_ALLOC -> reply path.
 
@@ -39,9 +39,9 @@ def main():
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     out = {"tcp": run("tcp", False),
-           "rccl_tick": run("rccl", True),  # persistent mapped slots + graph-replayed allgather
-           "rccl_tick_nograph": run("rccl", True, OCM_TICK_GRAPH="0"),
-           "rccl_tick_r01_path": run("rccl", True, OCM_TICK_GRAPH="0", OCM_TICK_MAPPED="0"),
+           "rccl_tick": run("rccl", True),  # one tick in flight, mapped slots
+           "rccl_tick_depth2": run("rccl", True, OCM_TICK_DEPTH="2"),
+           "rccl_tick_hbm_slots": run("rccl", True, OCM_TICK_MAPPED="0"),
            "socket_tick": run("socket", True)}
     print(json.dumps(out, indent=1))
     if a.out:
