@@ -32,6 +32,8 @@
 #include <thread>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "ocm/msg.h"
 
 namespace ocm {
@@ -47,9 +49,27 @@ struct TickRecord {
 struct TickSlot {
     uint32_t count;    // records used in this slot
     uint32_t busy;     // sender still has queued records (keep ticking)
+    uint64_t first;    // device-sealed slots: ring index of rec[0] (the sender's progress)
     TickRecord rec[kTickMsgs];
 };
 static_assert(sizeof(TickRecord) == 168, "tick record layout");
+
+// Outbox of a device-sealed collective: pinned, device-mapped host memory the
+// tick transport appends records to (then releases `published`). A small
+// kernel queued in front of each collective ("seal", csrc/src/kernels/tick.hip)
+// moves up to kTickMsgs unsent records into that tick's send slot WHEN THE
+// TICK RUNS, so a record posted while ticks are queued rides the next tick to
+// execute instead of waiting behind them.
+constexpr uint32_t kTickRing = 256;  // power of two
+struct TickRing {
+    uint64_t published;               // records appended so far (host, release)
+    uint64_t pad[15];
+    TickRecord rec[kTickRing];        // record j lives at rec[j % kTickRing]
+};
+
+// Queue the seal of one tick on `stream`: *consumed (device memory, only this
+// stream touches it) -> slot->first, up to kTickMsgs records of `ring` -> slot.
+hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, hipStream_t stream);
 
 class Collective {
 public:
@@ -58,6 +78,9 @@ public:
     // rank's slot i into recv_slots(i) (rank-major), test(i) reports it done.
     // Ticks on different slots may be in flight together (stream-ordered).
     virtual int depth() const { return 1; }
+    // Device-sealed collectives expose their outbox ring; the transport then
+    // appends records there instead of filling send slots (host-filled: null).
+    virtual TickRing *ring() { return nullptr; }
     virtual void *send_slot(int i) = 0;
     virtual const void *recv_slots(int i) = 0;
     virtual int start(int i) = 0;   // 0 ok
@@ -119,6 +142,10 @@ private:
     std::vector<Msg> in_;
     std::atomic<bool> stop_{false}, failed_{false}, announce_{false}, up_{false};
     std::atomic<uint64_t> ticks_{0}, wake_upto_{0}, announce_tick_{0};
+    TickRing *ring_ = nullptr;  // device-sealed collectives: their outbox (under mu_)
+    uint64_t ring_sent_ = 0;    // ring records a completed tick of ours carried
+    void flush_ring();
+    uint64_t unsent() const;
     int efd_ = -1;
 };
 

@@ -22,13 +22,20 @@ namespace {
 
 // ---------------------------------------------------------------- RCCL
 
-// RCCL over xGMI: a ring of depth() slot pairs in pinned, device-mapped host
-// memory (OCM_TICK_MAPPED=0: HBM slots with H2D/D2H copies queued around the
-// collective), one ncclAllGather per tick queued on one stream, an event per
-// slot for completion. The tick thread writes its records straight into the
-// send slot before queueing the tick and reads the peers' records straight
-// out of the receive slots once the slot's event has fired.
-// OCM_TICK_DEPTH (default 1) ticks may be queued at once.
+// RCCL over xGMI: a ring of depth() tick slots, one ncclAllGather per tick on
+// one stream, an event per slot for completion.
+//
+// Device-sealed (default, OCM_TICK_SEAL=1): the transport appends records to a
+// TickRing in pinned host memory; each tick is [seal kernel -> allgather], and
+// the seal moves the unsent records into that tick's HBM send slot when the
+// tick executes. Records therefore never wait behind queued ticks, and up to
+// OCM_TICK_DEPTH (default 3) ticks stay queued while traffic lasts: the GPU
+// runs them back to back (an allgather queued behind another costs ~3.5 us,
+// a launch-and-wait 12-16 us; profiles/rccl_tick_floor_r02.json).
+// Host-filled (OCM_TICK_SEAL=0): the tick thread fills the send slot in pinned
+// host memory before queueing the tick (depth 1 by default).
+// The gathered slots land in pinned, device-mapped host memory, read in place
+// (OCM_TICK_MAPPED=0: HBM plus a D2H copy queued behind the collective).
 class RcclCollective : public Collective {
 public:
     ~RcclCollective() override {
@@ -42,47 +49,64 @@ public:
             if (sl.ev) (void)hipEventDestroy(sl.ev);
             if (sl.hsend) (void)hipHostFree(sl.hsend);
             if (sl.hrecv) (void)hipHostFree(sl.hrecv);
-            if (!mapped_) {
-                if (sl.dsend) (void)hipFree(sl.dsend);
-                if (sl.drecv) (void)hipFree(sl.drecv);
-            }
+            if (sealed_ || !mapped_) (void)hipFree(sl.dsend);
+            if (!mapped_) (void)hipFree(sl.drecv);
         }
+        if (out_) (void)hipHostFree(out_);
+        if (consumed_) (void)hipFree(consumed_);
         if (stream_) (void)hipStreamDestroy(stream_);
     }
     int init(int gpu, int rank, int n, const uint8_t *id, size_t bytes, std::string *err) {
         gpu_ = gpu;
         n_ = n;
         bytes_ = bytes;
-        const char *m = std::getenv("OCM_TICK_MAPPED");
-        mapped_ = !(m && std::strcmp(m, "0") == 0);
+        auto flag = [](const char *k, bool dflt) {
+            const char *v = std::getenv(k);
+            return v && *v ? std::strcmp(v, "0") != 0 : dflt;
+        };
+        mapped_ = flag("OCM_TICK_MAPPED", true);
+        sealed_ = flag("OCM_TICK_SEAL", true) && bytes == sizeof(TickSlot);
         const char *d = std::getenv("OCM_TICK_DEPTH");
-        // Depth 1 by default: measured on MI355X, queueing ticks ahead makes a
-        // record wait behind empty ones (profiles/ctrl_probe_r02b.json).
-        const int depth = std::max(1, std::min(d && *d ? std::atoi(d) : 1, 64));
+        const int depth = std::max(1, std::min(d && *d ? std::atoi(d) : (sealed_ ? 3 : 1), 64));
         if (hipSetDevice(gpu) != hipSuccess || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
             *err = "rccl: no stream on gpu " + std::to_string(gpu);
             return -1;
         }
+        const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable;
+        bool ok = true;
+        if (sealed_) {
+            ok = hipHostMalloc(reinterpret_cast<void **>(&out_), sizeof(TickRing), fl) == hipSuccess &&
+                 hipHostGetDevicePointer(reinterpret_cast<void **>(&out_dev_), out_, 0) == hipSuccess &&
+                 hipMalloc(reinterpret_cast<void **>(&consumed_), sizeof(uint64_t)) == hipSuccess &&
+                 hipMemset(consumed_, 0, sizeof(uint64_t)) == hipSuccess;
+            if (ok) std::memset(out_, 0, sizeof(TickRing));
+        }
         ring_.resize((size_t)depth);
         for (auto &sl : ring_) {
-            bool ok = hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) == hipSuccess;
-            if (mapped_) {
-                const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable;
+            ok = ok && hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) == hipSuccess;
+            if (sealed_) {
+                ok = ok && hipMalloc(&sl.dsend, bytes) == hipSuccess;
+            } else if (mapped_) {
                 ok = ok && hipHostMalloc(&sl.hsend, bytes, fl) == hipSuccess &&
-                     hipHostMalloc(&sl.hrecv, bytes * (size_t)n, fl) == hipSuccess &&
-                     hipHostGetDevicePointer(&sl.dsend, sl.hsend, 0) == hipSuccess &&
+                     hipHostGetDevicePointer(&sl.dsend, sl.hsend, 0) == hipSuccess;
+            } else {
+                ok = ok && hipMalloc(&sl.dsend, bytes) == hipSuccess && hipHostMalloc(&sl.hsend, bytes) == hipSuccess;
+            }
+            if (mapped_) {
+                ok = ok && hipHostMalloc(&sl.hrecv, bytes * (size_t)n, fl) == hipSuccess &&
                      hipHostGetDevicePointer(&sl.drecv, sl.hrecv, 0) == hipSuccess;
             } else {
-                ok = ok && hipMalloc(&sl.dsend, bytes) == hipSuccess && hipMalloc(&sl.drecv, bytes * (size_t)n) == hipSuccess &&
-                     hipHostMalloc(&sl.hsend, bytes) == hipSuccess && hipHostMalloc(&sl.hrecv, bytes * (size_t)n) == hipSuccess;
+                ok = ok && hipMalloc(&sl.drecv, bytes * (size_t)n) == hipSuccess &&
+                     hipHostMalloc(&sl.hrecv, bytes * (size_t)n) == hipSuccess;
             }
-            if (!ok) {
-                (void)hipGetLastError();
-                *err = "rccl: no memory for the tick slots";
-                return -1;
-            }
-            std::memset(sl.hsend, 0, bytes);
+            if (!ok) break;
+            if (sl.hsend) std::memset(sl.hsend, 0, bytes);
             std::memset(sl.hrecv, 0, bytes * (size_t)n);
+        }
+        if (!ok) {
+            (void)hipGetLastError();
+            *err = "rccl: no memory for the tick slots";
+            return -1;
         }
         ncclUniqueId uid;
         std::memcpy(&uid, id, sizeof(uid));
@@ -107,13 +131,18 @@ public:
     }
     void request_abort() { abort_req_ = true; }
     int depth() const override { return (int)ring_.size(); }
+    TickRing *ring() override { return sealed_ ? out_ : nullptr; }
     void *send_slot(int i) override { return ring_[(size_t)i].hsend; }
     const void *recv_slots(int i) override { return ring_[(size_t)i].hrecv; }
     int start(int i) override {
         if (aborted_) return -1;
         Slot &sl = ring_[(size_t)i];
         (void)hipSetDevice(gpu_);
-        if (!mapped_ && hipMemcpyAsync(sl.dsend, sl.hsend, bytes_, hipMemcpyHostToDevice, stream_) != hipSuccess) return -1;
+        if (sealed_) {
+            if (tick_seal_launch(out_dev_, consumed_, static_cast<TickSlot *>(sl.dsend), stream_) != hipSuccess) return -1;
+        } else if (!mapped_ && hipMemcpyAsync(sl.dsend, sl.hsend, bytes_, hipMemcpyHostToDevice, stream_) != hipSuccess) {
+            return -1;
+        }
         if (ncclAllGather(sl.dsend, sl.drecv, bytes_, ncclUint8, comm_, stream_) != ncclSuccess) return -1;
         if (!mapped_ && hipMemcpyAsync(sl.hrecv, sl.drecv, bytes_ * (size_t)n_, hipMemcpyDeviceToHost, stream_) != hipSuccess)
             return -1;
@@ -149,11 +178,13 @@ private:
     };
     int gpu_ = 0, n_ = 1;
     size_t bytes_ = 0;
-    bool mapped_ = true;
+    bool mapped_ = true, sealed_ = true;
     unsigned polls_ = 0;
     ncclComm_t comm_ = nullptr;
     hipStream_t stream_ = nullptr;
     std::vector<Slot> ring_;
+    TickRing *out_ = nullptr, *out_dev_ = nullptr;  // sealed: the outbox (host view / device view)
+    uint64_t *consumed_ = nullptr;                  // sealed: records sealed so far (HBM, this stream only)
     std::atomic<bool> abort_req_{false};
     bool aborted_ = false;
 };
@@ -323,9 +354,27 @@ bool TickTransport::post(int dest, const Msg &m) {
         r.dest = dest;
         r.msg = m;
         out_.push_back(r);
+        flush_ring();
     }
     cv_.notify_all();
     return true;
+}
+
+// Device-sealed collectives: move queued records into the outbox ring while it
+// has room (records the seal kernels have not taken yet stay in it). Under mu_.
+void TickTransport::flush_ring() {
+    if (!ring_) return;
+    uint64_t pub = ring_->published;
+    while (!out_.empty() && pub - ring_sent_ < kTickRing) {
+        ring_->rec[pub & (kTickRing - 1)] = out_.front();
+        out_.pop_front();
+        pub++;
+    }
+    __atomic_store_n(&ring_->published, pub, __ATOMIC_RELEASE);  // the records before the count
+}
+
+uint64_t TickTransport::unsent() const {
+    return out_.size() + (ring_ ? ring_->published - ring_sent_ : 0);
 }
 
 std::vector<Msg> TickTransport::drain() {
@@ -353,8 +402,14 @@ bool TickTransport::take_announce(uint64_t *tick) {
 
 std::vector<TickRecord> TickTransport::take_unsent() {
     std::lock_guard<std::mutex> lk(mu_);
-    std::vector<TickRecord> v(out_.begin(), out_.end());
+    // Ring records past the last completed tick of ours (one sealed into a tick
+    // that then failed may also have reached its peer: the fallback may repeat it).
+    std::vector<TickRecord> v;
+    if (ring_)
+        for (uint64_t j = ring_sent_; j < ring_->published; j++) v.push_back(ring_->rec[j & (kTickRing - 1)]);
+    v.insert(v.end(), out_.begin(), out_.end());
     out_.clear();
+    if (ring_) ring_sent_ = ring_->published;
     return v;
 }
 
@@ -385,6 +440,11 @@ void TickTransport::run() {
     }
     Collective *coll = coll_.get();
     const uint64_t depth = (uint64_t)std::max(1, coll->depth());
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        ring_ = coll->ring();
+        flush_ring();
+    }
     up_ = true;
     signal();
     uint64_t issued = 0, done = 0, target = 0;
@@ -398,7 +458,7 @@ void TickTransport::run() {
             std::unique_lock<std::mutex> lk(mu_);
             if (done == issued && issued >= target) {
                 // Idle: sleep until there is something to send or a peer calls a tick.
-                cv_.wait(lk, [&] { return stop_.load() || !out_.empty() || wake_upto_.load() > target; });
+                cv_.wait(lk, [&] { return stop_.load() || unsent() > 0 || wake_upto_.load() > target; });
                 if (stop_) break;
                 if (wake_upto_.load() <= target) {
                     // We start the burst: the peers must join tick issued + 1.
@@ -411,13 +471,16 @@ void TickTransport::run() {
             // Queue ticks up to the target, at most `depth` in flight.
             while (issued < target && issued - done < depth) {
                 const int i = (int)(issued % depth);
-                TickSlot *slot = static_cast<TickSlot *>(coll->send_slot(i));
-                slot->count = 0;
-                while (!out_.empty() && slot->count < (uint32_t)kTickMsgs) {
-                    slot->rec[slot->count++] = out_.front();
-                    out_.pop_front();
+                if (!ring_) {  // host-filled: the slot's records are fixed now
+                    TickSlot *slot = static_cast<TickSlot *>(coll->send_slot(i));
+                    slot->count = 0;
+                    slot->first = 0;
+                    while (!out_.empty() && slot->count < (uint32_t)kTickMsgs) {
+                        slot->rec[slot->count++] = out_.front();
+                        out_.pop_front();
+                    }
+                    slot->busy = out_.empty() ? 0 : 1;
                 }
-                slot->busy = out_.empty() ? 0 : 1;
                 if (announce_.load()) signal();  // let the event loop wake the peers first
                 lk.unlock();
                 const int rc = coll->start(i);
@@ -451,6 +514,12 @@ void TickTransport::run() {
         size_t delivered = 0;
         {
             std::lock_guard<std::mutex> lk(mu_);
+            if (ring_) {
+                // Our own slot says how far the seals got through the outbox.
+                const TickSlot &mine = got[rank_];
+                ring_sent_ = std::max<uint64_t>(ring_sent_, mine.first + std::min<uint32_t>(mine.count, kTickMsgs));
+                flush_ring();
+            }
             for (int k = 0; k < n_; k++) {
                 const TickSlot &sl = got[k];
                 if (sl.count || sl.busy) traffic = true;

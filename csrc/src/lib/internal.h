@@ -165,6 +165,7 @@ struct State {
     hipStream_t svc_stream = nullptr;
     unsigned svc_blocks = kServiceBlocksDefault;          // gang size (OCM_SERVICE_BLOCKS)
     unsigned svc_solo_tiles = kServiceSoloTilesDefault;  // requests of <= this many tiles stay on workgroup 0
+    unsigned svc_solo_tiles_host_get = 1;  // ... for gets from the host tier (OCM_SERVICE_SOLO_TILES_HOST_GET)
     unsigned svc_proto = kServiceProtoDefault;           // hand-off protocol bits (OCM_SERVICE_PROTO)
     bool svc_running = false;
     bool svc_park_kernel = false;  // park the service during kernel transfers above svc_max (OCM_SERVICE_PARK_KERNEL)
@@ -289,7 +290,7 @@ int sync_stream();
 int service_start(unsigned long long first_seq);
 void service_park();
 void service_stop();
-int service_xfer(XferArgs x);
+int service_xfer(XferArgs x, unsigned solo_tiles);
 // `done` (optional, async launches on a lane): receives the kernel-published
 // completion flag of the launch, or flag == nullptr when the op has none.
 int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async,

@@ -108,6 +108,7 @@ int ocm_init(void) {
     s.svc_max = sm && *sm ? std::strtoull(sm, nullptr, 0) : kServiceMaxDefault;
     s.svc_blocks = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_BLOCKS", kServiceBlocksDefault), 1024));
     s.svc_solo_tiles = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES", kServiceSoloTilesDefault));
+    s.svc_solo_tiles_host_get = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES_HOST_GET", 1));
     s.svc_proto = (unsigned)env_int("OCM_SERVICE_PROTO", (int)kServiceProtoDefault) & 31u;
     s.launch_flags = env_int("OCM_LAUNCH_FLAG", 1) != 0;
     s.svc_park_kernel = env_int("OCM_SERVICE_PARK_KERNEL", 0) != 0;

@@ -199,13 +199,13 @@ void service_stop() {
 }
 
 // Run one normalized transfer through the resident kernel and wait for it.
-int service_xfer(XferArgs x) {
+int service_xfer(XferArgs x, unsigned solo_tiles) {
     State &s = S();
     if (xfer_normalize(x) != hipSuccess) OCM_FAIL(-1, "invalid transfer");
     const unsigned long long seq = ++s.svc_seq;
     if (!s.svc_running && service_start(seq) != 0) return -1;
     // The host sizes the gang and the completion count every workgroup agrees on.
-    const unsigned long long active = service_gang_size(x, s.svc_blocks, s.svc_solo_tiles);
+    const unsigned long long active = service_gang_size(x, s.svc_blocks, solo_tiles);
     auto gang_word = [&]() {
         unsigned long long target = 0;
         if (active > 1) {
@@ -323,7 +323,12 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         if (x.n_ext > 1) x.unit_shift = (uint32_t)log2_exact(a->stripe_unit);
         if (wait_alloc(a) != 0) return -1;  // keep program order with queued async ops
         if (honor_dep(a, nullptr, true) != 0) return -1;
-        if (service_xfer(x) == 0) return 0;
+        // Gets from the host tier are bound by PCIe read round trips: two tiles
+        // already go faster on two workgroups (64 KiB: 7.7 vs 8.4 us); puts and
+        // HBM owners keep small requests on workgroup 0 (profiles/svc_v4_r02.json).
+        const unsigned solo = (!put && !a->any_gpu) ? std::min(s.svc_solo_tiles, s.svc_solo_tiles_host_get)
+                                                    : s.svc_solo_tiles;
+        if (service_xfer(x, solo) == 0) return 0;
         OCM_WARN("copy service failed (%s); falling back to launches", last_error());
         s.svc_max = 0;
     }

@@ -1,6 +1,6 @@
 """Control-plane transport cost: remote ocm_alloc p50 with the records on TCP
 (self queue) vs an RCCL ncclAllGather tick (1-rank communicator, OCM_TICK_SELF;
-variants: pipeline depth 4 / 1, slots in mapped host memory / HBM with copies)
+variants: device-sealed outbox at depth 3 / 1 / 6, host-filled slots)
 vs the socket-ring collective, on one GPU. Leases off so every allocation
 takes the full REQ_ALLOC -> DO_ALLOC -> reply path.
 
@@ -34,15 +34,29 @@ def run(ctrl, tick_self, **extra_env):
             return {k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()}
 
 
+VARIANTS = {
+    "tcp": ("tcp", False, {}),
+    "rccl_tick": ("rccl", True, {}),  # device-sealed outbox (library default depth)
+    "rccl_tick_sealed_depth1": ("rccl", True, {"OCM_TICK_DEPTH": "1"}),
+    "rccl_tick_sealed_depth2": ("rccl", True, {"OCM_TICK_DEPTH": "2"}),
+    "rccl_tick_sealed_depth3": ("rccl", True, {"OCM_TICK_DEPTH": "3"}),
+    "rccl_tick_host_filled": ("rccl", True, {"OCM_TICK_SEAL": "0"}),
+    "socket_tick": ("socket", True, {}),
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="")
+    ap.add_argument("--variants", default="tcp,rccl_tick,rccl_tick_sealed_depth1,rccl_tick_sealed_depth3,"
+                                          "rccl_tick_host_filled,socket_tick")
+    ap.add_argument("--repeat", type=int, default=1)
     a = ap.parse_args()
-    out = {"tcp": run("tcp", False),
-           "rccl_tick": run("rccl", True),  # one tick in flight, mapped slots
-           "rccl_tick_depth2": run("rccl", True, OCM_TICK_DEPTH="2"),
-           "rccl_tick_hbm_slots": run("rccl", True, OCM_TICK_MAPPED="0"),
-           "socket_tick": run("socket", True)}
+    out = {}
+    for v in a.variants.split(","):
+        ctrl, tick_self, env = VARIANTS[v]
+        for r in range(a.repeat):
+            out[v if a.repeat == 1 else f"{v}#{r}"] = run(ctrl, tick_self, **env)
     print(json.dumps(out, indent=1))
     if a.out:
         with open(a.out, "w") as f:

@@ -33,7 +33,9 @@ CONFIGS["proto0"] = {"OCM_SERVICE_PROTO": "0"}
 CONFIGS["trace"] = {"OCM_SERVICE_PROTO": "17"}
 # requests of <= N tiles stay on workgroup 0
 for n in (0, 1, 2, 4, 8):
-    CONFIGS[f"solo{n}"] = {"OCM_SERVICE_SOLO_TILES": str(n)}
+    CONFIGS[f"solo{n}"] = {"OCM_SERVICE_SOLO_TILES": str(n), "OCM_SERVICE_SOLO_TILES_HOST_GET": str(n)}
+# host-tier gets only: the round-2 default (1) against the earlier shared threshold (2)
+CONFIGS["hostget2"] = {"OCM_SERVICE_SOLO_TILES_HOST_GET": "2"}
 for g in (1, 16, 32, 64, 128, 256):
     CONFIGS[f"svc_g{g}"] = {"OCM_SERVICE_MAX": str(64 << 20), "OCM_SERVICE_BLOCKS": str(g)}
 
