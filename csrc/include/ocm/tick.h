@@ -70,6 +70,10 @@ struct TickRing {
 // Queue the seal of one tick on `stream`: *consumed (device memory, only this
 // stream touches it) -> slot->first, up to kTickMsgs records of `ring` -> slot.
 hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, hipStream_t stream);
+// Queue a one-lane kernel that stores `seq` to `flag` (pinned, device-mapped
+// host memory) at system scope: the host sees a tick end ~6 us sooner than
+// through an event query (tools/launch_probe.hip, profiles/launch_flag_r01.json).
+hipError_t tick_done_launch(uint64_t *flag, uint64_t seq, hipStream_t stream);
 
 class Collective {
 public:

@@ -29,9 +29,13 @@ namespace {
 // TickRing in pinned host memory; each tick is [seal kernel -> allgather], and
 // the seal moves the unsent records into that tick's HBM send slot when the
 // tick executes. Records therefore never wait behind queued ticks, and up to
-// OCM_TICK_DEPTH (default 3) ticks stay queued while traffic lasts: the GPU
+// OCM_TICK_DEPTH (default 2) ticks stay queued while traffic lasts: the GPU
 // runs them back to back (an allgather queued behind another costs ~3.5 us,
-// a launch-and-wait 12-16 us; profiles/rccl_tick_floor_r02.json).
+// a launch-and-wait 12-16 us; profiles/rccl_tick_floor_r02.json). A one-lane
+// kernel after each collective stores the tick's number to pinned host memory,
+// which the tick thread polls (no runtime query on the fast path).
+// 1-daemon remote alloc p50: depth 2 and 3 29.9 us, depth 1 42.9 us, p99 69 /
+// 96 / 48 us (profiles/ctrl_probe_r02e_sealed.json).
 // Host-filled (OCM_TICK_SEAL=0): the tick thread fills the send slot in pinned
 // host memory before queueing the tick (depth 1 by default).
 // The gathered slots land in pinned, device-mapped host memory, read in place
@@ -53,6 +57,7 @@ public:
             if (!mapped_) (void)hipFree(sl.drecv);
         }
         if (out_) (void)hipHostFree(out_);
+        if (done_) (void)hipHostFree(done_);
         if (consumed_) (void)hipFree(consumed_);
         if (stream_) (void)hipStreamDestroy(stream_);
     }
@@ -67,14 +72,17 @@ public:
         mapped_ = flag("OCM_TICK_MAPPED", true);
         sealed_ = flag("OCM_TICK_SEAL", true) && bytes == sizeof(TickSlot);
         const char *d = std::getenv("OCM_TICK_DEPTH");
-        const int depth = std::max(1, std::min(d && *d ? std::atoi(d) : (sealed_ ? 3 : 1), 64));
+        const int depth = std::max(1, std::min(d && *d ? std::atoi(d) : (sealed_ ? 2 : 1), 64));
         if (hipSetDevice(gpu) != hipSuccess || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
             *err = "rccl: no stream on gpu " + std::to_string(gpu);
             return -1;
         }
         const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable;
         bool ok = true;
-        if (sealed_) {
+        ok = hipHostMalloc(reinterpret_cast<void **>(&done_), 64, fl) == hipSuccess &&
+             hipHostGetDevicePointer(reinterpret_cast<void **>(&done_dev_), done_, 0) == hipSuccess;
+        if (ok) __atomic_store_n(done_, 0ull, __ATOMIC_RELAXED);
+        if (ok && sealed_) {
             ok = hipHostMalloc(reinterpret_cast<void **>(&out_), sizeof(TickRing), fl) == hipSuccess &&
                  hipHostGetDevicePointer(reinterpret_cast<void **>(&out_dev_), out_, 0) == hipSuccess &&
                  hipMalloc(reinterpret_cast<void **>(&consumed_), sizeof(uint64_t)) == hipSuccess &&
@@ -146,6 +154,8 @@ public:
         if (ncclAllGather(sl.dsend, sl.drecv, bytes_, ncclUint8, comm_, stream_) != ncclSuccess) return -1;
         if (!mapped_ && hipMemcpyAsync(sl.hrecv, sl.drecv, bytes_ * (size_t)n_, hipMemcpyDeviceToHost, stream_) != hipSuccess)
             return -1;
+        sl.seq = ++started_;
+        if (tick_done_launch(done_dev_, sl.seq, stream_) != hipSuccess) return -1;
         if (ring_.size() == 1) return 0;
         return hipEventRecord(sl.ev, stream_) == hipSuccess ? 0 : -1;
     }
@@ -156,12 +166,17 @@ public:
             aborted_ = true;
             return -1;
         }
+        // The tick's done kernel stored its sequence number: seen without a runtime call.
+        if (__atomic_load_n(done_, __ATOMIC_ACQUIRE) >= ring_[(size_t)i].seq) return 1;
+        if ((++polls_ & 255) != 0) return 0;
+        // Backstop every 256 polls: the runtime's view (errors surface here), and
+        // RCCL's async error (a dead peer never joins the collective).
         // One tick in flight: the stream is exactly that tick, and a stream query
         // measured cheaper than an event query (profiles/ctrl_probe_r02c.json).
         const hipError_t q = ring_.size() == 1 ? hipStreamQuery(stream_) : hipEventQuery(ring_[(size_t)i].ev);
         if (q == hipSuccess) return 1;
         if (q != hipErrorNotReady) return -1;
-        if ((++polls_ & 63) == 0) {
+        {
             ncclResult_t async = ncclSuccess;
             if (ncclCommGetAsyncError(comm_, &async) == ncclSuccess && async != ncclSuccess && async != ncclInProgress)
                 return -1;
@@ -175,6 +190,7 @@ private:
     struct Slot {
         void *hsend = nullptr, *hrecv = nullptr, *dsend = nullptr, *drecv = nullptr;
         hipEvent_t ev = nullptr;
+        uint64_t seq = 0;  // tick number its done kernel stores
     };
     int gpu_ = 0, n_ = 1;
     size_t bytes_ = 0;
@@ -185,6 +201,8 @@ private:
     std::vector<Slot> ring_;
     TickRing *out_ = nullptr, *out_dev_ = nullptr;  // sealed: the outbox (host view / device view)
     uint64_t *consumed_ = nullptr;                  // sealed: records sealed so far (HBM, this stream only)
+    uint64_t *done_ = nullptr, *done_dev_ = nullptr;  // last tick whose done kernel ran (pinned host)
+    uint64_t started_ = 0;
     std::atomic<bool> abort_req_{false};
     bool aborted_ = false;
 };

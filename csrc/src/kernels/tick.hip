@@ -36,7 +36,18 @@ __global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uin
     }
 }
 
+__global__ __launch_bounds__(64) void tick_done_kernel(uint64_t *flag, uint64_t seq) {
+    // Stream order: the collective before this kernel has finished and its
+    // stores to the gathered slots are released at its end.
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
+
+hipError_t tick_done_launch(uint64_t *flag, uint64_t seq, hipStream_t stream) {
+    hipLaunchKernelGGL(tick_done_kernel, dim3(1), dim3(64), 0, stream, flag, seq);
+    return hipGetLastError();
+}
 
 hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, hipStream_t stream) {
     hipLaunchKernelGGL(tick_seal_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot);

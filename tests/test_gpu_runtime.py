@@ -124,6 +124,14 @@ def test_bench_two_ranks_sharing_one_gpu():
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert res["n_gpus"] == 2 and res["value"] > 0 and res["config"]["remote_tier"] == "hbm", res
     assert res["autotune"]["ranks"] == 2 and res["autotune"]["put"] in res["autotune"]["GiBps"], res["autotune"]
+    # per-peer table and the control-plane extra (RCCL cannot put two ranks on one GPU:
+    # its entry records an error or a TCP fallback, the TCP entry must be measured)
+    assert res["peers_from_rank0"]["1"]["put_GiBps"] > 0, res["peers_from_rank0"]
+    assert res["control_plane"]["tcp"]["alloc_p50_us"] > 0, res["control_plane"]
+    assert "rccl" in res["control_plane"], res["control_plane"]
+    if os.path.isdir(os.path.join(REPO, "gpurun_out")):
+        with open(os.path.join(REPO, "gpurun_out", "bench_share2.json"), "w") as f:
+            json.dump(res, f)
 
 
 @pytest.mark.parametrize("policy", ["ring", "stripe"])
