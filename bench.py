@@ -99,13 +99,16 @@ class Phases:
     A step that raises on one rank is published through the same all-gather the
     other ranks wait on, so all of them stop together (BenchAbort) instead of
     waiting in a barrier the failed rank never reaches. Test hook:
-    OCM_BENCH_RAISE="<rank>:<phase>" raises inside that phase on that rank."""
+    OCM_BENCH_RAISE="<rank>:<phase>" raises inside that phase on that rank
+    (OCM_BENCH_RAISE_ONCE: only the first time that phase runs)."""
 
     def __init__(self, dist, world: int, rank: int):
         self.dist, self.world, self.rank = dist, world, rank
         self.current = "init"
         inj = os.environ.get("OCM_BENCH_RAISE", "")
         self.inject = tuple(inj.split(":", 1)) if ":" in inj else None
+        once = os.environ.get("OCM_BENCH_RAISE_ONCE", "")  # the same, first run of the phase only
+        self.inject_once = tuple(once.split(":", 1)) if ":" in once else None
 
     def run(self, name: str, fn):
         self.current = name
@@ -113,6 +116,9 @@ class Phases:
         try:
             if self.inject and int(self.inject[0]) == self.rank and self.inject[1] == name:
                 raise RuntimeError(f"injected failure (OCM_BENCH_RAISE) in phase {name}")
+            if self.inject_once and int(self.inject_once[0]) == self.rank and self.inject_once[1] == name:
+                self.inject_once = None
+                raise RuntimeError(f"injected failure (OCM_BENCH_RAISE_ONCE) in phase {name}")
             val = fn()
         except Exception as e:  # noqa: BLE001 - published to every rank below
             err = f"{type(e).__name__}: {e}"[:600]
@@ -410,20 +416,9 @@ def main() -> int:
         # ---- the sweep pair: 2 x max + 1 bytes each side (reference: 2 GiB + 1) ----
         pair_bytes = 2 * max_bytes + 1
         rflags = {"auto": 0, "loopback": api.OCM_ALLOC_LOOPBACK, "host": api.OCM_ALLOC_HOST_TIER}[args.remote]
-        pair = ph.run("pair_alloc", lambda: client.alloc(remote_kind, local_bytes=pair_bytes, remote_bytes=pair_bytes,
-                                                         flags=rflags))
-        info = pair.remote_info()
-
-        # ---- setup (untimed): pick the put/get kernel configuration over the
-        # xGMI links, every rank at once (all-to-all load), slowest rank decides.
-        # CPU runs (memcpy data path) do it too, so the multi-rank protocol is tested ----
-        tuned = None
-        if world > 1 and not args.no_autotune:
-            tuned = ph.run("autotune", lambda: wl.autotune(pair, min(256 << 20, max_bytes), reps=3,
-                                                           gather=lambda obj: gather_obj(dist, obj, world)))
 
         # verify: pattern -> put -> clobber -> get -> check
-        def verify():
+        def verify(pair):
             pair.fill(seed=1234 + rank, nbytes=max_bytes)
             pair.put(0, 0, max_bytes)
             pair.fill(seed=0, nbytes=max_bytes)
@@ -432,7 +427,41 @@ def main() -> int:
             if bad:
                 raise RuntimeError(f"{bad} words differ after put/get round trip")
 
-        ph.run("verify", verify)
+        def prepare(flags):
+            """Allocate the pair, pick the kernel configuration over the links (setup,
+            untimed: every rank at once, the slowest rank decides; CPU runs do it too,
+            so the multi-rank protocol is tested) and verify a round trip."""
+            held = {}
+
+            def alloc():
+                held["pair"] = client.alloc(remote_kind, local_bytes=pair_bytes, remote_bytes=pair_bytes, flags=flags)
+                return held["pair"]
+
+            try:
+                pair = ph.run("pair_alloc", alloc)
+                tuned = None
+                if world > 1 and not args.no_autotune:
+                    tuned = ph.run("autotune", lambda: wl.autotune(pair, min(256 << 20, max_bytes), reps=3,
+                                                                   gather=lambda obj: gather_obj(dist, obj, world)))
+                ph.run("verify", lambda: verify(pair))
+                return pair, tuned
+            except BenchAbort:
+                if "pair" in held:
+                    _local(held["pair"].free)
+                raise
+
+        fallback = None
+        try:
+            pair, tuned = prepare(rflags)
+        except BenchAbort as e:
+            # Peer HBM unusable on this node (e.g. cross-device IPC refused): measure the
+            # same sweep with the remote halves in the peers' pinned host tiers instead of
+            # reporting nothing, and say so in the JSON (config.remote_tier, fallback).
+            if world == 1 or args.remote != "auto":
+                raise
+            fallback = {"from": "peer hbm", "to": "peer host tier", "phase": e.phase, "rank_errors": e.errors}
+            pair, tuned = prepare(api.OCM_ALLOC_HOST_TIER)
+        info = pair.remote_info()
         sizes = wl.sweep_sizes(args.min_bytes, max_bytes)
 
         def warmup():
@@ -530,6 +559,8 @@ def main() -> int:
         }
         if tuned:
             result["autotune"] = tuned
+        if fallback:
+            result["fallback"] = fallback
         if optim:
             result["fused_remote_adam"] = optim
         if baseline:

@@ -513,7 +513,9 @@ void Daemon::on_app_conn(int fd, uint32_t events) {
             r.status = MSG_RESPONSE;
             const int sfd = arena_ ? arena_->dup_slab_fd(m.u.region.slab_id) : -1;
             r.err = sfd >= 0 ? 0 : ENOENT;
-            if (mbox_send_fd(fd, &r, kMsgBytes, sfd, 1000) != 1) OCM_WARN("rank %d: slab fd reply to pid %d failed", rank_, (int)m.pid);
+            // Never block the event loop: the app waits for this reply, so its queue has room;
+            // if not, it times out and falls back to the /proc path.
+            if (mbox_send_fd(fd, &r, kMsgBytes, sfd, 0) != 1) OCM_WARN("rank %d: slab fd reply to pid %d failed", rank_, (int)m.pid);
             if (sfd >= 0) close(sfd);
             continue;
         }

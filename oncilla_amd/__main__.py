@@ -55,7 +55,7 @@ def _stats(args) -> int:
     with api.Client(daemon_rank=args.rank, ns=args.ns) as c:
         n = c.lib.ocm_num_nodes()
         keys = ["gpu", "num_apps", "gpu_used", "gpu_capacity", "host_used", "host_capacity", "n_alloc", "n_free",
-                "n_reclaimed", "n_spilled", "n_slabs", "n_leases", "lease_allocs", "ctrl_ticks"]
+                "n_reclaimed", "n_spilled", "n_slabs", "n_leases", "lease_allocs", "ctrl_ticks", "xgmi_peers", "max_hops"]
         print("rank " + " ".join(f"{k:>13}" for k in keys))
         for r in range(n):
             try:

@@ -136,3 +136,32 @@ def test_host_tier_of_another_gpus_daemon(mesh_factory):
         assert a.remote_info()["extents"][0]["tier"] == api.OCM_TIER_HOST
         assert _roundtrip(a, n, seed=31) == 0
         a.free()
+
+
+def test_bench_on_real_gpus():
+    """The driver's scaling launch on this box's GPUs (up to 4): one rank and one
+    daemon per physical GPU, striped over every peer, autotune over xGMI, the
+    per-peer table with link types, and the control-plane extra with RCCL
+    ticks between real ranks."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    k = min(NDEV, 4)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(k),
+                        "--master-addr", "127.0.0.1", "--master-port", "29671", os.path.join(repo, "bench.py"),
+                        "--gpus", str(k), "--steps", "1", "--warmup", "1", "--max-bytes", str(64 << 20),
+                        "--alloc-samples", "50", "--no-characterize"],
+                       capture_output=True, text=True, timeout=600, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["n_gpus"] == k and res["value"] > 0 and res["config"]["remote_tier"] == "hbm", res
+    assert res["config"]["extents_per_pair"] == k - 1
+    peers = res["peers_from_rank0"]
+    assert sorted(peers) == [str(p) for p in range(1, k)], peers
+    for p, row in peers.items():
+        assert row["owner_gpu"] == int(p) and row["put_GiBps"] > 0 and row["link"] is not None, row
+    cp = res["control_plane"]
+    assert cp["tcp"]["alloc_p50_us"] > 0 and cp["rccl"]["ticks_rank0"] > 0, cp
