@@ -210,6 +210,10 @@ private:
 // ---------------------------------------------------------------- sockets
 
 // Ring allgather over abstract unix sockets, done inside start() (depth 1).
+// OCM_TICK_SOCKET_SEAL=1 gives it an outbox ring sealed inside start(), the
+// CPU stand-in for the RCCL seal kernel: the device-sealed protocol (ring
+// accounting, progress from the sender's own gathered slot) then runs
+// multi-rank on CPU meshes (tests/test_ctrl_tick.py).
 class SocketCollective : public Collective {
 public:
     ~SocketCollective() override {
@@ -223,6 +227,11 @@ public:
         bytes_ = bytes;
         send_.assign(bytes, 0);
         recv_.assign(bytes * (size_t)n, 0);
+        const char *sl = std::getenv("OCM_TICK_SOCKET_SEAL");
+        if (sl && std::strcmp(sl, "1") == 0 && bytes == sizeof(TickSlot)) {
+            outbox_.reset(new TickRing());
+            std::memset(outbox_.get(), 0, sizeof(TickRing));
+        }
         if (n == 1) return 0;
         listen_ = mbox_listen("ocm_" + ns + "_coll" + std::to_string(rank), 4);
         if (listen_ < 0) {
@@ -243,7 +252,19 @@ public:
     }
     void *send_slot(int) override { return send_.data(); }
     const void *recv_slots(int) override { return recv_.data(); }
+    TickRing *ring() override { return outbox_.get(); }
     int start(int) override {
+        if (outbox_) {  // what tick_seal_kernel does, when the tick runs
+            TickSlot *slot = reinterpret_cast<TickSlot *>(send_.data());
+            const uint64_t pub = __atomic_load_n(&outbox_->published, __ATOMIC_ACQUIRE);
+            const uint64_t pending = pub - consumed_;
+            const uint32_t n = (uint32_t)std::min<uint64_t>(pending, kTickMsgs);
+            for (uint32_t r = 0; r < n; r++) slot->rec[r] = outbox_->rec[(consumed_ + r) & (kTickRing - 1)];
+            slot->count = n;
+            slot->busy = pending > n ? 1u : 0u;
+            slot->first = consumed_;
+            consumed_ += n;
+        }
         char *out = recv_.data();
         std::memcpy(out + (size_t)rank_ * bytes_, send_.data(), bytes_);
         // Ring: at step s send block (rank - s) right, receive block (rank - s - 1) from the left.
@@ -285,6 +306,8 @@ private:
     int rank_ = 0, n_ = 1, left_ = -1, right_ = -1, listen_ = -1;
     size_t bytes_ = 0;
     std::vector<char> send_, recv_;
+    std::unique_ptr<TickRing> outbox_;  // OCM_TICK_SOCKET_SEAL
+    uint64_t consumed_ = 0;
     std::atomic<bool> aborted_{false};
 };
 

@@ -30,8 +30,11 @@ def _wait_tick_up(c, n):
     raise AssertionError("tick transport never came up")
 
 
-def test_socket_tick_mesh_suite(mesh_factory, native, tool):
-    m = mesh_factory(4, extra_args=["--ctrl", "socket"])
+@pytest.mark.parametrize("sealed", ["0", "1"])
+def test_socket_tick_mesh_suite(mesh_factory, native, tool, sealed):
+    # sealed=1: the socket collective emulates the RCCL seal kernel (outbox ring
+    # sealed when the tick runs), so the device-sealed protocol runs multi-rank here
+    m = mesh_factory(4, extra_args=["--ctrl", "socket"], env={"OCM_TICK_SOCKET_SEAL": sealed})
     with api.Client(daemon_rank=0, ns=m.ns) as c:
         _wait_tick_up(c, 4)
         t0 = [c.stats(r)["ctrl_ticks"] for r in range(4)]
@@ -51,8 +54,9 @@ def test_socket_tick_mesh_suite(mesh_factory, native, tool):
             assert rc == 0, out + m.logs()
 
 
-def test_socket_tick_concurrent_churn(mesh_factory):
-    m = mesh_factory(4, extra_args=["--ctrl", "socket"])
+@pytest.mark.parametrize("sealed", ["0", "1"])
+def test_socket_tick_concurrent_churn(mesh_factory, sealed):
+    m = mesh_factory(4, extra_args=["--ctrl", "socket"], env={"OCM_TICK_SOCKET_SEAL": sealed})
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     code = textwrap.dedent(f"""
         import sys; sys.path.insert(0, {repo!r})
@@ -72,8 +76,9 @@ def test_socket_tick_concurrent_churn(mesh_factory):
         assert all(c.stats(r)["ctrl_ticks"] > 0 for r in range(4))
 
 
-def test_tick_peer_death_falls_back_to_tcp(mesh_factory):
-    m = mesh_factory(3, extra_args=["--ctrl", "socket"])
+@pytest.mark.parametrize("sealed", ["0", "1"])
+def test_tick_peer_death_falls_back_to_tcp(mesh_factory, sealed):
+    m = mesh_factory(3, extra_args=["--ctrl", "socket"], env={"OCM_TICK_SOCKET_SEAL": sealed})
     with api.Client(daemon_rank=0, ns=m.ns) as c:
         _wait_tick_up(c, 3)
         m.kill(2)
