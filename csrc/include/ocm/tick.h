@@ -91,6 +91,7 @@ public:
     virtual int test(int i) = 0;    // 1 done, 0 in flight, -1 failed
     virtual void abort() {}
     virtual const char *name() const = 0;
+    virtual std::string error() const { return std::string(); }  // why start/test failed, if known
 };
 
 // Collective constructors block until every rank joined; `cancel` aborts them.
@@ -148,6 +149,7 @@ private:
     std::atomic<uint64_t> ticks_{0}, wake_upto_{0}, announce_tick_{0};
     TickRing *ring_ = nullptr;  // device-sealed collectives: their outbox (under mu_)
     uint64_t ring_sent_ = 0;    // ring records a completed tick of ours carried
+    uint64_t ring_pub_ = 0;     // records appended (host shadow of ring_->published)
     void flush_ring();
     uint64_t unsent() const;
     int efd_ = -1;

@@ -741,7 +741,8 @@ void Daemon::on_tick() {
             if (r != rank_) send_tcp(r, w);
     }
     if (tick_->failed()) {
-        for (TickRecord &rec : tick_->take_unsent()) send_tcp(rec.dest, rec.msg);
+        // send_rank: records to ourselves (OCM_TICK_SELF) go back to the local queue
+        for (TickRecord &rec : tick_->take_unsent()) send_rank(rec.dest, rec.msg);
     }
 }
 

@@ -20,8 +20,6 @@ namespace ocm {
 
 namespace {
 
-// ---------------------------------------------------------------- RCCL
-
 // RCCL over xGMI: a ring of depth() tick slots, one ncclAllGather per tick on
 // one stream, an event per slot for completion.
 //
@@ -147,15 +145,19 @@ public:
         Slot &sl = ring_[(size_t)i];
         (void)hipSetDevice(gpu_);
         if (sealed_) {
-            if (tick_seal_launch(out_dev_, consumed_, static_cast<TickSlot *>(sl.dsend), stream_) != hipSuccess) return -1;
+            if (!out_dev_ || !consumed_ || !sl.dsend || !sl.drecv || !done_dev_) return why("tick slots missing");
+            const hipError_t e = tick_seal_launch(out_dev_, consumed_, static_cast<TickSlot *>(sl.dsend), stream_);
+            if (e != hipSuccess) return why(std::string("seal launch: ") + hipGetErrorString(e));
         } else if (!mapped_ && hipMemcpyAsync(sl.dsend, sl.hsend, bytes_, hipMemcpyHostToDevice, stream_) != hipSuccess) {
             return -1;
         }
-        if (ncclAllGather(sl.dsend, sl.drecv, bytes_, ncclUint8, comm_, stream_) != ncclSuccess) return -1;
+        const ncclResult_t nr = ncclAllGather(sl.dsend, sl.drecv, bytes_, ncclUint8, comm_, stream_);
+        if (nr != ncclSuccess) return why(std::string("ncclAllGather: ") + ncclGetErrorString(nr));
         if (!mapped_ && hipMemcpyAsync(sl.hrecv, sl.drecv, bytes_ * (size_t)n_, hipMemcpyDeviceToHost, stream_) != hipSuccess)
             return -1;
         sl.seq = ++started_;
-        if (tick_done_launch(done_dev_, sl.seq, stream_) != hipSuccess) return -1;
+        const hipError_t de = tick_done_launch(done_dev_, sl.seq, stream_);
+        if (de != hipSuccess) return why(std::string("done launch: ") + hipGetErrorString(de));
         if (ring_.size() == 1) return 0;
         return hipEventRecord(sl.ev, stream_) == hipSuccess ? 0 : -1;
     }
@@ -164,7 +166,7 @@ public:
         // joins the collective, so the event would never fire.
         if (abort_req_.load()) {
             aborted_ = true;
-            return -1;
+            return why("aborted");
         }
         // The tick's done kernel stored its sequence number: seen without a runtime call.
         if (__atomic_load_n(done_, __ATOMIC_ACQUIRE) >= ring_[(size_t)i].seq) return 1;
@@ -175,18 +177,24 @@ public:
         // measured cheaper than an event query (profiles/ctrl_probe_r02c.json).
         const hipError_t q = ring_.size() == 1 ? hipStreamQuery(stream_) : hipEventQuery(ring_[(size_t)i].ev);
         if (q == hipSuccess) return 1;
-        if (q != hipErrorNotReady) return -1;
+        if (q != hipErrorNotReady) return why(std::string("tick completion: ") + hipGetErrorString(q));
         {
             ncclResult_t async = ncclSuccess;
             if (ncclCommGetAsyncError(comm_, &async) == ncclSuccess && async != ncclSuccess && async != ncclInProgress)
-                return -1;
+                return why(std::string("rccl async error: ") + ncclGetErrorString(async));
         }
         return 0;
     }
     void abort() override { abort_req_ = true; }
     const char *name() const override { return "rccl"; }
+    std::string error() const override { return err_; }
 
 private:
+    int why(const std::string &e) {
+        err_ = e;
+        return -1;
+    }
+    std::string err_;
     struct Slot {
         void *hsend = nullptr, *hrecv = nullptr, *dsend = nullptr, *drecv = nullptr;
         hipEvent_t ev = nullptr;
@@ -404,18 +412,22 @@ bool TickTransport::post(int dest, const Msg &m) {
 // Device-sealed collectives: move queued records into the outbox ring while it
 // has room (records the seal kernels have not taken yet stay in it). Under mu_.
 void TickTransport::flush_ring() {
-    if (!ring_) return;
-    uint64_t pub = ring_->published;
+    if (!ring_ || out_.empty()) return;
+    uint64_t pub = ring_pub_;  // never read back: the ring may sit behind a write-combined BAR
     while (!out_.empty() && pub - ring_sent_ < kTickRing) {
         ring_->rec[pub & (kTickRing - 1)] = out_.front();
         out_.pop_front();
         pub++;
     }
-    __atomic_store_n(&ring_->published, pub, __ATOMIC_RELEASE);  // the records before the count
+    if (pub == ring_pub_) return;
+    __builtin_ia32_sfence();                                      // the records before the count
+    __atomic_store_n(&ring_->published, pub, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();                                      // and out of the write-combining buffers
+    ring_pub_ = pub;
 }
 
 uint64_t TickTransport::unsent() const {
-    return out_.size() + (ring_ ? ring_->published - ring_sent_ : 0);
+    return out_.size() + (ring_ ? ring_pub_ - ring_sent_ : 0);
 }
 
 std::vector<Msg> TickTransport::drain() {
@@ -447,10 +459,10 @@ std::vector<TickRecord> TickTransport::take_unsent() {
     // that then failed may also have reached its peer: the fallback may repeat it).
     std::vector<TickRecord> v;
     if (ring_)
-        for (uint64_t j = ring_sent_; j < ring_->published; j++) v.push_back(ring_->rec[j & (kTickRing - 1)]);
+        for (uint64_t j = ring_sent_; j < ring_pub_; j++) v.push_back(ring_->rec[j & (kTickRing - 1)]);
     v.insert(v.end(), out_.begin(), out_.end());
     out_.clear();
-    if (ring_) ring_sent_ = ring_->published;
+    ring_sent_ = ring_pub_;
     return v;
 }
 
@@ -490,7 +502,9 @@ void TickTransport::run() {
     signal();
     uint64_t issued = 0, done = 0, target = 0;
     auto fail = [&] {
-        if (!stop_) OCM_WARN("rank %d: %s tick transport failed; falling back to TCP", rank_, coll->name());
+        if (!stop_)
+            OCM_WARN("rank %d: %s tick transport failed (%s); falling back to TCP", rank_, coll->name(),
+                     coll->error().empty() ? "collective error" : coll->error().c_str());
         failed_ = true;
         signal();
     };

@@ -45,11 +45,13 @@ __global__ __launch_bounds__(64) void tick_done_kernel(uint64_t *flag, uint64_t 
 }  // namespace
 
 hipError_t tick_done_launch(uint64_t *flag, uint64_t seq, hipStream_t stream) {
+    (void)hipGetLastError();  // report this launch, not an earlier call's error
     hipLaunchKernelGGL(tick_done_kernel, dim3(1), dim3(64), 0, stream, flag, seq);
     return hipGetLastError();
 }
 
 hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, hipStream_t stream) {
+    (void)hipGetLastError();  // report this launch, not an earlier call's error
     hipLaunchKernelGGL(tick_seal_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot);
     return hipGetLastError();
 }

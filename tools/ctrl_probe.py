@@ -24,14 +24,25 @@ def run(ctrl, tick_self, **extra_env):
     if tick_self:
         env["OCM_TICK_SELF"] = "1"
     with Mesh(1, gpus=[0], extra_args=["--ctrl", ctrl], env=env) as m:
-        with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
-            deadline = time.time() + 30
-            while tick_self and c.stats(0)["ctrl_ticks"] == 0 and time.time() < deadline:
-                c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=1 << 20).free()
-                time.sleep(0.05)
-            r = wl.alloc_latency(c, api.OCM_REMOTE_GPU, 300, local_bytes=4096, remote_bytes=1 << 20)
-            r["ticks"] = c.stats(0)["ctrl_ticks"]
-            return {k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()}
+        try:
+            r = _measure(m, tick_self)
+            if tick_self and r["ticks"] == 0:
+                r["daemon_log"] = [l for l in m.logs().splitlines() if " W " in l or " E " in l][-5:]
+            return r
+        except Exception:
+            print(m.logs()[-4000:], file=sys.stderr)
+            raise
+
+
+def _measure(m, tick_self):
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        deadline = time.time() + 30
+        while tick_self and c.stats(0)["ctrl_ticks"] == 0 and time.time() < deadline:
+            c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=1 << 20).free()
+            time.sleep(0.05)
+        r = wl.alloc_latency(c, api.OCM_REMOTE_GPU, 300, local_bytes=4096, remote_bytes=1 << 20)
+        r["ticks"] = c.stats(0)["ctrl_ticks"]
+        return {k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()}
 
 
 VARIANTS = {
