@@ -82,6 +82,7 @@ private:
         int fd = -1;
         pid_t peer_pid = -1;       // SO_PEERCRED
         pid_t app_pid = 0;         // set by MSG_CONNECT
+        bool same_user = true;     // SO_PEERCRED uid is ours or root (others: OCM_ALLOW_ANY_UID)
     };
     struct Pending {
         uint64_t seq = 0;

@@ -204,3 +204,30 @@ def test_data_server_reaps_connections(mesh_factory):
     time.sleep(0.3)
     assert threads() <= base + 3, (base, threads())
     assert m.daemons[1].alive()
+
+
+@pytest.mark.skipif(os.geteuid() != 0, reason="needs root to switch to another uid")
+def test_other_users_get_no_slab_fds(mesh_factory, monkeypatch):
+    """With OCM_ALLOW_ANY_UID=1 another user may attach, but MSG_SLAB_FD hands it a
+    host-tier slab only if one of its own allocations lives there: a memfd opens
+    the whole slab, i.e. other apps' data."""
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    m = mesh_factory(1, env={"OCM_ALLOW_ANY_UID": "1"})
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)  # host tier: slab 1
+        code = textwrap.dedent(f"""
+            import os, socket, struct
+            os.setgid(65534); os.setuid(65534)
+            s = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+            s.connect(b"\\0ocm_{m.ns}_d0")
+            s.settimeout(5)
+            region = bytearray(128)
+            struct.pack_into("<I", region, 40, 1)  # Region.slab_id
+            s.send(struct.pack("<IIiiQii128s", 24, 1, 0, 0, 7, -1, 0, bytes(region)))  # MSG_SLAB_FD
+            data, anc, _, _ = s.recvmsg(160, socket.CMSG_SPACE(4))
+            err = struct.unpack_from("<i", data, 28)[0]
+            print(err, len(anc))
+        """)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=30)
+        assert r.stdout.split() == ["13", "0"], r.stdout + r.stderr  # EACCES, no fd attached
+        a.free()
