@@ -1002,4 +1002,85 @@ long long ocm_x_pattern(void *p, uint64_t words, uint64_t first, uint32_t seed, 
     return (e == hipSuccess && rc == 0) ? (long long)bad : -1;
 }
 
+// ---- PyTorch pluggable allocator: tensors in disaggregated memory ----
+// torch.cuda.memory.CUDAPluggableAllocator(libocm.so, "ocm_torch_alloc",
+// "ocm_torch_free") behind a torch.cuda.MemPool (oncilla_amd.torch_pool): each
+// block torch's caching allocator asks for is the remote half of a pair with
+// no local half, one extent (a tensor needs contiguous addresses), in another
+// daemon's HBM (or its pinned host tier) and addressed in place over xGMI.
+// torch caches the blocks; a block comes back here only when torch releases it.
+}  // extern "C"
+
+namespace {
+struct TorchPool {
+    std::mutex mu;
+    std::map<void *, ocm_alloc_t> live;
+    struct ocm_alloc_ex_params ex = {-1, 0, 1, 0, 0};  // any owner, single extent
+    uint64_t bytes = 0;
+};
+TorchPool &torch_pool() {
+    static TorchPool *p = new TorchPool();  // never destroyed: torch may free at exit
+    return *p;
+}
+}  // namespace
+
+extern "C" {
+
+// remote_rank -1: rank0 places; flags: enum ocm_alloc_flags (e.g. OCM_ALLOC_HOST_TIER).
+void ocm_x_torch_pool_config(int remote_rank, uint32_t flags) {
+    TorchPool &tp = torch_pool();
+    std::lock_guard<std::mutex> lk(tp.mu);
+    tp.ex.remote_rank = remote_rank;
+    tp.ex.flags = flags & ~(uint32_t)OCM_ALLOC_STRIPE;  // one extent: contiguous addresses
+    tp.ex.stripe_width = 1;
+}
+
+void *ocm_torch_alloc(ssize_t size, int device, void *stream) {
+    (void)stream;  // the memory is ready when the owner answers; torch orders its reuse
+    State &s = S();
+    if (size <= 0 || !s.inited || s.device < 0 || device != s.device) return nullptr;  // torch reports the OOM
+    TorchPool &tp = torch_pool();
+    struct ocm_alloc_ex_params ex;
+    {
+        std::lock_guard<std::mutex> lk(tp.mu);
+        ex = tp.ex;
+    }
+    struct ocm_alloc_params p = {0, (uint64_t)size, OCM_REMOTE_GPU};
+    ocm_alloc_t a = ocm_alloc_ex(&p, &ex);
+    if (!a) return nullptr;
+    void *ptr = ocm_remotebuf(a);
+    if (!ptr) {
+        ocm_free(a);
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(tp.mu);
+    tp.live[ptr] = a;
+    tp.bytes += (uint64_t)size;
+    return ptr;
+}
+
+void ocm_torch_free(void *ptr, ssize_t size, int device, void *stream) {
+    (void)device;
+    (void)stream;
+    TorchPool &tp = torch_pool();
+    ocm_alloc_t a = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(tp.mu);
+        auto it = tp.live.find(ptr);
+        if (it == tp.live.end()) return;
+        a = it->second;
+        tp.live.erase(it);
+        tp.bytes -= std::min<uint64_t>(tp.bytes, (uint64_t)(size > 0 ? size : 0));
+    }
+    if (S().inited) ocm_free(a);
+}
+
+// {blocks held by torch, their bytes}
+void ocm_x_torch_pool_stats(uint64_t out[2]) {
+    TorchPool &tp = torch_pool();
+    std::lock_guard<std::mutex> lk(tp.mu);
+    out[0] = tp.live.size();
+    out[1] = tp.bytes;
+}
+
 }  // extern "C"

@@ -186,6 +186,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_batch": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, ctypes.POINTER(u64), i32, i32]),
             "ocm_x_link_info": (i32, [i32, i32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
             "ocm_x_extent_handle": (i32, [vp, i32, ctypes.c_char_p]),
+            "ocm_x_torch_pool_config": (None, [i32, ctypes.c_uint32]),
+            "ocm_x_torch_pool_stats": (None, [ctypes.POINTER(u64)]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(lib, name)

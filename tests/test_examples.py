@@ -89,3 +89,9 @@ def test_train_zero_gpu_shared(native):
     env = {k: v for k, v in os.environ.items() if k != "OCM_NO_GPU"}
     out = _torchrun(2, 29662, ["--share-gpu"], env=env)
     assert "2 ranks" in out and "peer HBM" in out and "mode=fused" in out
+
+
+@pytest.mark.gpu
+def test_remote_weights_gpu(native):
+    out = _run([sys.executable, os.path.join(REPO, "examples", "remote_weights.py")])
+    assert "forward matches the local copy: True" in out

@@ -165,3 +165,19 @@ def test_bench_on_real_gpus():
         assert row["owner_gpu"] == int(p) and row["put_GiBps"] > 0 and row["link"] is not None, row
     cp = res["control_plane"]
     assert cp["tcp"]["alloc_p50_us"] > 0 and cp["rccl"]["ticks_rank0"] > 0, cp
+
+
+def test_torch_tensors_in_another_gpus_hbm(mesh_factory):
+    """RemoteMemPool with the owner on GPU 1: a matmul on GPU 0 reads its operand
+    over xGMI, in place."""
+    from oncilla_amd.torch_pool import RemoteMemPool
+
+    m = mesh_factory(2, gpus=[0, 1])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        pool = RemoteMemPool(c, remote_rank=1)
+        with pool:
+            w = torch.full((2048, 2048), 0.5, device="cuda:0")
+        assert c.stats(1)["gpu_used"] >= 16 << 20
+        x = torch.ones((64, 2048), device="cuda:0")
+        assert torch.equal(x @ w, torch.full((64, 2048), 1024.0, device="cuda:0"))
+        del w, pool

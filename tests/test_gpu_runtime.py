@@ -514,3 +514,40 @@ def test_stream_wait_orders_host_tier_memcpy(mesh_factory):
         a.get(0, 0, n)
         assert int((loc != 7).sum()) == 0
         a.free()
+
+
+def test_torch_tensors_in_peer_hbm(mesh_factory):
+    """RemoteMemPool: tensors allocated under it are blocks of another daemon's HBM
+    (same-GPU stand-in here), used in place by torch kernels, and returned to the
+    owner when torch releases them."""
+    import gc
+
+    from oncilla_amd.torch_pool import RemoteMemPool
+
+    m = mesh_factory(2, gpus=[0, 0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        before = c.stats(1)["gpu_used"]
+        pool = RemoteMemPool(c, remote_rank=1)
+        with pool:
+            x = torch.arange(1 << 22, device="cuda:0", dtype=torch.float32)
+            w = torch.ones((1024, 1024), device="cuda:0")
+        st = RemoteMemPool.stats()
+        assert st["blocks"] >= 1 and st["bytes"] >= 16 << 20, st
+        assert c.stats(1)["gpu_used"] >= before + (16 << 20)
+        y = torch.ones(4, device="cuda:0")  # outside the pool: ordinary device memory
+        assert RemoteMemPool.stats() == st
+        assert float((x * 2).sum()) == float(2 * torch.arange(1 << 22, dtype=torch.float64).sum())
+        assert torch.equal(w @ w, torch.full((1024, 1024), 1024.0, device="cuda:0"))
+        del x, w, y
+        gc.collect()
+        torch.cuda.synchronize()
+        del pool
+        gc.collect()
+        torch.cuda.empty_cache()
+        torch.cuda.synchronize()
+        assert RemoteMemPool.stats()["blocks"] == 0
+        deadline = time.time() + 10  # a capacity lease taken on rank 1 goes back after 2 s idle
+        while c.stats(1)["gpu_used"] != before and time.time() < deadline:
+            time.sleep(0.1)
+        assert c.stats(1)["gpu_used"] == before
+
