@@ -403,19 +403,35 @@ def main() -> int:
         client = ph.run("client_init", attach)
         remote_kind = api.OCM_REMOTE_GPU if use_gpu else api.OCM_REMOTE_RDMA
 
-        # ---- p50 ocm_alloc latency (remote pair, and the local malloc path) ----
-        def latency():
-            lat_remote = wl.alloc_latency(client, remote_kind, args.alloc_samples, local_bytes=64 << 10,
-                                          remote_bytes=1 << 20)
-            lat_local = wl.alloc_latency(client, api.OCM_LOCAL_HOST, args.alloc_samples, local_bytes=1 << 20)
-            leases, _ = _local(lambda: client.stats()["lease_allocs"])
-            return lat_remote, lat_local, leases
+        rflags = {"auto": 0, "loopback": api.OCM_ALLOC_LOOPBACK, "host": api.OCM_ALLOC_HOST_TIER}[args.remote]
+        # Peer HBM unusable on this node (e.g. cross-device IPC refused on the first real
+        # multi-GPU node): measure with the remote halves in the peers' pinned host tiers
+        # instead of reporting nothing, and say so in the JSON (fallback, config.remote_tier).
+        can_fall_back = world > 1 and args.remote == "auto"
+        fallback = None
 
-        lat_remote, lat_local, leases = ph.run("alloc_latency", latency)
+        # ---- p50 ocm_alloc latency (remote pair, and the local malloc path) ----
+        def latency(flags):
+            def run():
+                lat_remote = wl.alloc_latency(client, remote_kind, args.alloc_samples, local_bytes=64 << 10,
+                                              remote_bytes=1 << 20, flags=flags)
+                lat_local = wl.alloc_latency(client, api.OCM_LOCAL_HOST, args.alloc_samples, local_bytes=1 << 20)
+                leases, _ = _local(lambda: client.stats()["lease_allocs"])
+                return lat_remote, lat_local, leases
+
+            return run
+
+        try:
+            lat_remote, lat_local, leases = ph.run("alloc_latency", latency(rflags))
+        except BenchAbort as e:
+            if not can_fall_back:
+                raise
+            fallback = {"from": "peer hbm", "to": "peer host tier", "phase": e.phase, "rank_errors": e.errors}
+            rflags = api.OCM_ALLOC_HOST_TIER
+            lat_remote, lat_local, leases = ph.run("alloc_latency", latency(rflags))
 
         # ---- the sweep pair: 2 x max + 1 bytes each side (reference: 2 GiB + 1) ----
         pair_bytes = 2 * max_bytes + 1
-        rflags = {"auto": 0, "loopback": api.OCM_ALLOC_LOOPBACK, "host": api.OCM_ALLOC_HOST_TIER}[args.remote]
 
         # verify: pattern -> put -> clobber -> get -> check
         def verify(pair):
@@ -450,14 +466,10 @@ def main() -> int:
                     _local(held["pair"].free)
                 raise
 
-        fallback = None
         try:
             pair, tuned = prepare(rflags)
         except BenchAbort as e:
-            # Peer HBM unusable on this node (e.g. cross-device IPC refused): measure the
-            # same sweep with the remote halves in the peers' pinned host tiers instead of
-            # reporting nothing, and say so in the JSON (config.remote_tier, fallback).
-            if world == 1 or args.remote != "auto":
+            if not can_fall_back or fallback is not None:
                 raise
             fallback = {"from": "peer hbm", "to": "peer host tier", "phase": e.phase, "rank_errors": e.errors}
             pair, tuned = prepare(api.OCM_ALLOC_HOST_TIER)

@@ -119,16 +119,18 @@ def test_bench_eight_ranks_fail_fast(native, inject):
         assert res["phase"] == "verify" and list(res["rank_errors"]) == ["5"]
 
 
-def test_bench_falls_back_to_host_tier_when_peer_hbm_fails(native):
+@pytest.mark.parametrize("phase", ["verify", "alloc_latency"])
+def test_bench_falls_back_to_host_tier_when_peer_hbm_fails(native, phase):
     """--device gpu paths cannot run here, so drive the fallback on CPU ranks by
-    injecting a failure into the first verify: the bench re-prepares the pair once
-    and still reports a measured value, with the fallback recorded."""
-    env = dict(os.environ, OCM_BENCH_RAISE_ONCE="1:verify")
+    injecting a failure into the first run of a phase: the bench redoes it with the
+    remote halves in the host tier and still reports a measured value, with the
+    fallback recorded."""
+    env = dict(os.environ, OCM_BENCH_RAISE_ONCE=f"1:{phase}")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29591", os.path.join(REPO, "bench.py"),
+                        "--master-addr", "127.0.0.1", "--master-port", str(29591 + len(phase)), os.path.join(REPO, "bench.py"),
                         "--gpus", "2", "--device", "cpu", "--steps", "1", "--warmup", "1", "--max-bytes",
                         str(1 << 20), "--alloc-samples", "10"], capture_output=True, text=True, timeout=300,
                        cwd="/tmp", env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     res = _last_json(r.stdout)
-    assert res["value"] > 0 and res["fallback"]["phase"] == "verify" and list(res["fallback"]["rank_errors"]) == ["1"]
+    assert res["value"] > 0 and res["fallback"]["phase"] == phase and list(res["fallback"]["rank_errors"]) == ["1"]
