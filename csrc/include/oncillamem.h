@@ -28,6 +28,7 @@
 #include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <sys/types.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -172,6 +173,16 @@ int ocm_rank(void);        /* rank of the daemon this process is attached to */
 int ocm_num_nodes(void);   /* daemons in the mesh */
 int ocm_device(void);      /* HIP device the library copies on, -1 when CPU-only */
 const char *ocm_last_error(void);
+
+/* PyTorch pluggable-allocator hooks (torch.cuda.memory.CUDAPluggableAllocator;
+ * Python wrapper: oncilla_amd.torch_pool.RemoteMemPool). A block is the remote
+ * half of a single-extent pair with no local half, placed per
+ * ocm_x_torch_pool_config (remote_rank -1: rank0 places; flags: enum
+ * ocm_alloc_flags) and addressed in place by the caller's GPU. The process must
+ * have called ocm_init; `device` must be the library's device. */
+void *ocm_torch_alloc(ssize_t size, int device, void *stream);
+void ocm_torch_free(void *ptr, ssize_t size, int device, void *stream);
+void ocm_x_torch_pool_config(int remote_rank, uint32_t flags);
 
 #ifdef __cplusplus
 }

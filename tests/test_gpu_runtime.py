@@ -516,24 +516,26 @@ def test_stream_wait_orders_host_tier_memcpy(mesh_factory):
         a.free()
 
 
-def test_torch_tensors_in_peer_hbm(mesh_factory):
+@pytest.mark.parametrize("host_tier", [False, True])
+def test_torch_tensors_in_peer_hbm(mesh_factory, host_tier):
     """RemoteMemPool: tensors allocated under it are blocks of another daemon's HBM
-    (same-GPU stand-in here), used in place by torch kernels, and returned to the
-    owner when torch releases them."""
+    (same-GPU stand-in here) or its pinned host tier, used in place by torch
+    kernels, and returned to the owner when torch releases them."""
     import gc
 
     from oncilla_amd.torch_pool import RemoteMemPool
 
+    used = "host_used" if host_tier else "gpu_used"
     m = mesh_factory(2, gpus=[0, 0])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
-        before = c.stats(1)["gpu_used"]
-        pool = RemoteMemPool(c, remote_rank=1)
+        before = c.stats(1)[used]
+        pool = RemoteMemPool(c, remote_rank=1, host_tier=host_tier)
         with pool:
             x = torch.arange(1 << 22, device="cuda:0", dtype=torch.float32)
             w = torch.ones((1024, 1024), device="cuda:0")
         st = RemoteMemPool.stats()
         assert st["blocks"] >= 1 and st["bytes"] >= 16 << 20, st
-        assert c.stats(1)["gpu_used"] >= before + (16 << 20)
+        assert c.stats(1)[used] >= before + (16 << 20)
         y = torch.ones(4, device="cuda:0")  # outside the pool: ordinary device memory
         assert RemoteMemPool.stats() == st
         assert float((x * 2).sum()) == float(2 * torch.arange(1 << 22, dtype=torch.float64).sum())
@@ -547,7 +549,7 @@ def test_torch_tensors_in_peer_hbm(mesh_factory):
         torch.cuda.synchronize()
         assert RemoteMemPool.stats()["blocks"] == 0
         deadline = time.time() + 10  # a capacity lease taken on rank 1 goes back after 2 s idle
-        while c.stats(1)["gpu_used"] != before and time.time() < deadline:
+        while c.stats(1)[used] != before and time.time() < deadline:
             time.sleep(0.1)
-        assert c.stats(1)["gpu_used"] == before
+        assert c.stats(1)[used] == before
 
