@@ -1,3 +1,7 @@
+// Tick control transport: daemon<->daemon records carried by collectives
+// (ocm/tick.h). Reference parity: the control RPC it can replace, one TCP
+// connection per 160-byte record (src/mem.c:62-111 send_recv_msg / send_msg,
+// SURVEY K11); the MI355X design carries the records over RCCL on xGMI.
 #include "ocm/tick.h"
 
 #include <hip/hip_runtime_api.h>
