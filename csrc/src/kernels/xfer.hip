@@ -145,6 +145,49 @@ struct TileSpan {
     uint64_t n;
 };
 
+// Two tile spans with all their loads in flight before the first store: a
+// workgroup that copies two tiles from a far source (host tier over PCIe, peer
+// HBM over xGMI) pays one read round trip instead of two. Each span is at most
+// one tile, i.e. one round of kThreads x kUnroll vectors. Spans whose source and
+// destination disagree mod 16 (unaligned user offsets) go one after the other.
+template <int ST>
+__device__ __forceinline__ void span_copy2(const TileSpan &a, const TileSpan &b) {
+    const bool vec = (((uintptr_t)a.src ^ (uintptr_t)a.dst) & 15u) == 0 &&
+                     (((uintptr_t)b.src ^ (uintptr_t)b.dst) & 15u) == 0 &&
+                     a.n <= (uint64_t)kThreads * kUnroll * 16 && b.n <= (uint64_t)kThreads * kUnroll * 16;
+    if (!vec) {
+        span_copy<ST>(a.dst, a.src, a.n);
+        span_copy<ST>(b.dst, b.src, b.n);
+        return;
+    }
+    const int tid = threadIdx.x;
+    // byte heads up to 16-byte alignment (same offset mod 16 on both sides)
+    const uint64_t ha = ((16u - ((uintptr_t)a.dst & 15u)) & 15u) < a.n ? ((16u - ((uintptr_t)a.dst & 15u)) & 15u) : a.n;
+    const uint64_t hb = ((16u - ((uintptr_t)b.dst & 15u)) & 15u) < b.n ? ((16u - ((uintptr_t)b.dst & 15u)) & 15u) : b.n;
+    if ((uint64_t)tid < ha) store_byte<ST>(a.dst + tid, load_byte<ST>(a.src + tid));
+    if ((uint64_t)tid < hb) store_byte<ST>(b.dst + tid, load_byte<ST>(b.src + tid));
+    const uint32_t nva = (uint32_t)((a.n - ha) >> 4), nvb = (uint32_t)((b.n - hb) >> 4);
+    const __amdgpu_buffer_rsrc_t rsa = span_rsrc(a.src + ha, nva << 4), rda = span_rsrc(a.dst + ha, nva << 4);
+    const __amdgpu_buffer_rsrc_t rsb = span_rsrc(b.src + hb, nvb << 4), rdb = span_rsrc(b.dst + hb, nvb << 4);
+    u32x4 va[kUnroll], vb[kUnroll];
+#pragma unroll
+    for (int k = 0; k < kUnroll; k++)
+        va[k] = __builtin_amdgcn_raw_buffer_load_b128(rsa, (int)((k * kThreads + tid) << 4), 0, load_aux<ST>());
+#pragma unroll
+    for (int k = 0; k < kUnroll; k++)
+        vb[k] = __builtin_amdgcn_raw_buffer_load_b128(rsb, (int)((k * kThreads + tid) << 4), 0, load_aux<ST>());
+#pragma unroll
+    for (int k = 0; k < kUnroll; k++)
+        __builtin_amdgcn_raw_buffer_store_b128(va[k], rda, (int)((k * kThreads + tid) << 4), 0, store_aux<ST>());
+#pragma unroll
+    for (int k = 0; k < kUnroll; k++)
+        __builtin_amdgcn_raw_buffer_store_b128(vb[k], rdb, (int)((k * kThreads + tid) << 4), 0, store_aux<ST>());
+    const uint64_t ta = (a.n - ha) & 15u, tb = (b.n - hb) & 15u;
+    const uint64_t oa = ha + ((uint64_t)nva << 4), ob = hb + ((uint64_t)nvb << 4);
+    if ((uint64_t)tid < ta) store_byte<ST>(a.dst + oa + tid, load_byte<ST>(a.src + oa + tid));
+    if ((uint64_t)tid < tb) store_byte<ST>(b.dst + ob + tid, load_byte<ST>(b.src + ob + tid));
+}
+
 // Span of tile `ti` of a transfer of [rem_off, rem_off + len) in striped
 // coordinates. `E` holds the extent bases (`E::ext[]`); it is read in place
 // (kernarg segment or LDS): copying it to a local array would put the
@@ -513,7 +556,10 @@ __device__ __forceinline__ void service_copy(const unsigned long long *sh, uint6
     const XferArgs &a = *reinterpret_cast<const XferArgs *>(sh + 2);  // read in place (no scratch copy)
     const uint64_t ntiles = service_tiles(a);
     const uint64_t base = a.rem_off & ~((1ull << a.tile_shift) - 1);
-    for (uint64_t ti = first; ti < ntiles; ti += stride) {
+    // tiles two at a time: both tiles' loads in flight at once (span_copy2)
+    uint64_t ti = first;
+    for (; ti + stride < ntiles; ti += 2 * stride) span_copy2<ST>(tile_span(a, ti, base), tile_span(a, ti + stride, base));
+    if (ti < ntiles) {
         TileSpan sp = tile_span(a, ti, base);
         span_copy<ST>(sp.dst, sp.src, sp.n);
     }
