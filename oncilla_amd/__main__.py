@@ -2,6 +2,7 @@
 
     python -m oncilla_amd mesh --gpus 8 [--policy stripe] [--state-file F]   # foreground, Ctrl-C stops
     python -m oncilla_amd stats --ns NS [--rank 0]                           # every daemon's counters
+    python -m oncilla_amd metrics --ns NS [--port 9464]                      # Prometheus /metrics
     python -m oncilla_amd build [--sanitize address|thread]
 
 `mesh` prints the environment apps need (OCM_NS; OCM_DAEMON_RANK is the
@@ -67,6 +68,14 @@ def _stats(args) -> int:
     return 0
 
 
+def _metrics(args) -> int:
+    from .utils.metrics import serve
+
+    print(f"serving http://127.0.0.1:{args.port}/metrics for namespace {args.ns}", flush=True)
+    serve(args.ns, args.port, args.rank)
+    return 0
+
+
 def _build(args) -> int:
     from .utils.build import build
 
@@ -88,10 +97,14 @@ def main(argv=None) -> int:
     s = sub.add_parser("stats", help="print every daemon's counters")
     s.add_argument("--ns", required=True)
     s.add_argument("--rank", type=int, default=0, help="daemon to attach to")
+    x = sub.add_parser("metrics", help="serve every daemon's counters in the Prometheus text format")
+    x.add_argument("--ns", required=True)
+    x.add_argument("--port", type=int, default=9464)
+    x.add_argument("--rank", type=int, default=0, help="daemon to attach to")
     b = sub.add_parser("build", help="build the native tree (CMake + Ninja, gfx950)")
     b.add_argument("--sanitize", default=None, choices=["address", "thread"])
     args = ap.parse_args(argv)
-    return {"mesh": _mesh, "stats": _stats, "build": _build}[args.cmd](args)
+    return {"mesh": _mesh, "stats": _stats, "metrics": _metrics, "build": _build}[args.cmd](args)
 
 
 if __name__ == "__main__":

@@ -153,3 +153,28 @@ def test_mesh_on_open_address_needs_a_key(tmp_path, native):
     r = subprocess.run([f"{native}/ocmd", nf, "--rank", "1", "--gpu", "none", "--bind", "0.0.0.0"], env=env,
                        capture_output=True, text=True, timeout=30)
     assert r.returncode != 0 and "OCM_MESH_KEY" in (r.stdout + r.stderr)
+
+
+def test_prometheus_metrics_exporter(mesh_factory, monkeypatch):
+    """`python -m oncilla_amd metrics`: every daemon's counters as Prometheus gauges."""
+    import threading
+    import urllib.request
+
+    from oncilla_amd import api
+    from oncilla_amd.utils.metrics import serve
+
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    m = mesh_factory(3)
+    ready, stop = threading.Event(), threading.Event()
+    th = threading.Thread(target=serve, args=(m.ns, 0, 1, ready, stop), daemon=True)
+    th.start()
+    assert ready.wait(30)
+    try:
+        text = urllib.request.urlopen(f"http://127.0.0.1:{ready.port}/metrics", timeout=10).read().decode()
+    finally:
+        stop.set()
+        th.join(10)
+    for r in range(3):
+        assert f'oncilla_up{{rank="{r}"}} 1' in text
+        assert f'oncilla_host_capacity{{rank="{r}",gpu="-1"}}' in text
+    assert "# TYPE oncilla_n_alloc gauge" in text
