@@ -159,8 +159,7 @@ struct State {
     OpCounters ctr;
     // persistent copy service (small blocking one-sided ops)
     ServiceSlot *svc = nullptr;
-    ServiceReq *svc_req = nullptr;   // request record (&svc->req, or fine-grained HBM: svc_req_hbm)
-    bool svc_req_hbm = false;        // OCM_SERVICE_DOORBELL=hbm: the record in BAR-mapped HBM
+    ServiceReq *svc_req = nullptr;   // request record (&svc->req)
     unsigned long long svc_gang_total = 0;  // gang completions this instance counts to (device counter mirror)
     ServiceBox *svc_box = nullptr;   // device-memory mailbox of the gang
     hipStream_t svc_stream = nullptr;

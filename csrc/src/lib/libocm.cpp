@@ -775,7 +775,7 @@ void ocm_x_service_stats(uint64_t out[5]) {
     out[1] = s.svc_ns_post;
     out[2] = s.svc_ns_wait;
     out[3] = s.svc ? __atomic_load_n(&s.svc->gpu_ticks, __ATOMIC_ACQUIRE) : 0;
-    out[4] = s.svc_req_hbm ? 1 : 0;  // doorbell record in BAR-mapped HBM (OCM_SERVICE_DOORBELL=hbm)
+    out[4] = 0;  // doorbell record in host memory (a BAR-mapped HBM record measured slower: profiles/svc_doorbell_hbm_ab_r02.json)
 }
 
 // Copy-service phase stamps of the last request (OCM_SERVICE_PROTO with the

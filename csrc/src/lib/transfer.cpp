@@ -6,9 +6,6 @@
 // src/rdma.c:47-92,241-302; extoll_read/extoll_write over extoll_rma2_transfer,
 // src/extoll.c:40-167,286-310, 8 MiB x 2 outstanding) become
 // gfx950 kernel launches or the resident copy service here.
-#include <setjmp.h>
-#include <signal.h>
-
 #include "internal.h"
 
 namespace ocmlib {
@@ -134,32 +131,6 @@ int sync_stream() {
 
 // ---- persistent copy service ----
 
-namespace {
-sigjmp_buf g_touch_jmp;
-void on_touch_fault(int) { siglongjmp(g_touch_jmp, 1); }
-}  // namespace
-
-// Whether this CPU can write `p` (fine-grained HBM is CPU-mapped only on
-// large-BAR systems): a fault on the first touch marks it unusable instead of
-// killing the process. Called once, on the opt-in path only.
-bool cpu_can_touch(void *p) {
-    struct sigaction sa, old_segv, old_bus;
-    std::memset(&sa, 0, sizeof(sa));
-    sa.sa_handler = on_touch_fault;
-    sigemptyset(&sa.sa_mask);
-    sigaction(SIGSEGV, &sa, &old_segv);
-    sigaction(SIGBUS, &sa, &old_bus);
-    bool ok = false;
-    if (sigsetjmp(g_touch_jmp, 1) == 0) {
-        volatile unsigned long long *q = static_cast<volatile unsigned long long *>(p);
-        q[0] = 0;
-        ok = q[0] == 0;
-    }
-    sigaction(SIGSEGV, &old_segv, nullptr);
-    sigaction(SIGBUS, &old_bus, nullptr);
-    return ok;
-}
-
 int service_start(unsigned long long first_seq) {
     State &s = S();
     DeviceGuard g(s.device);
@@ -173,23 +144,6 @@ int service_start(unsigned long long first_seq) {
         }
         std::memset(s.svc, 0, sizeof(ServiceSlot));
         s.svc_req = &s.svc->req;
-        const char *db = std::getenv("OCM_SERVICE_DOORBELL");
-        if (db && !std::strcmp(db, "hbm")) {
-            // The request record in fine-grained HBM that this CPU writes through the
-            // BAR (large-BAR systems map it for the CPU); workgroup 0 then polls its
-            // own HBM instead of reading host memory across PCIe.
-            void *r = nullptr;
-            if (hipExtMallocWithFlags(&r, sizeof(ServiceReq), hipDeviceMallocFinegrained) == hipSuccess &&
-                hipMemset(r, 0, sizeof(ServiceReq)) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
-                cpu_can_touch(r)) {
-                s.svc_req = static_cast<ServiceReq *>(r);
-                s.svc_req_hbm = true;
-            } else {
-                (void)hipGetLastError();
-                if (r) (void)hipFree(r);
-                OCM_WARN("OCM_SERVICE_DOORBELL=hbm: no CPU-mapped fine-grained HBM; the doorbell stays in host memory");
-            }
-        }
         if (hipMalloc(reinterpret_cast<void **>(&s.svc_box), sizeof(ServiceBox)) != hipSuccess) {
             (void)hipGetLastError();
             s.svc_box = nullptr;
@@ -236,8 +190,6 @@ void service_stop() {
         s.svc_running = false;
     }
     (void)hipStreamDestroy(s.svc_stream);
-    if (s.svc_req_hbm) (void)hipFree(s.svc_req);
-    s.svc_req_hbm = false;
     s.svc_req = nullptr;
     (void)hipHostFree(s.svc);
     if (s.svc_box) (void)hipFree(s.svc_box);

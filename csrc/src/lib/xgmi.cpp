@@ -109,17 +109,20 @@ int export_local(xgmi_t x) {
         x->mine.host = 0;
     } else {
         if (x->memfd < 0) OCM_FAIL(-1, "host buffers passed by the caller cannot be exported; let xgmi_new allocate");
-        snprintf(reinterpret_cast<char *>(x->mine.handle), sizeof(x->mine.handle), "/proc/%d/fd/%d", (int)getpid(),
-                 x->memfd);
-        x->mine.host = 1;
+        x->mine.host = 1;  // the memfd rides along with the record
     }
     return 0;
 }
 
-int import_remote(xgmi_t x, const Reg &r) {
-    if (r.magic != kMagic) OCM_FAIL(-1, "bad registration record");
+// Takes ownership of `passed` (the peer's memfd for a host buffer, or -1).
+int import_remote(xgmi_t x, const Reg &r, int passed) {
+    if (r.magic != kMagic || (r.host && passed < 0)) {
+        if (passed >= 0) close(passed);
+        OCM_FAIL(-1, "bad registration record");
+    }
     x->rlen = r.len;
     if (!r.host) {
+        if (passed >= 0) close(passed);
         if (x->device < 0) OCM_FAIL(-1, "peer buffer is HBM but this process has no GPU");
         hipIpcMemHandle_t h;
         std::memcpy(&h, r.handle, sizeof(h));
@@ -130,10 +133,7 @@ int import_remote(xgmi_t x, const Reg &r) {
         x->rgpu = true;
         return 0;
     }
-    char path[65] = {0};
-    std::memcpy(path, r.handle, 64);
-    int fd = open(path, O_RDWR | O_CLOEXEC);
-    if (fd < 0) OCM_FAIL(-1, "open %s: %s", path, strerror(errno));
+    const int fd = passed;
     size_t maplen = (r.len + 4095) & ~size_t(4095);
     void *p = mmap(nullptr, maplen, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     close(fd);
@@ -150,14 +150,26 @@ int import_remote(xgmi_t x, const Reg &r) {
     return 0;
 }
 
+// Registration records travel with the host buffer's memfd attached
+// (SCM_RIGHTS): the peer maps it even if this process has exited by then,
+// which a /proc/<pid>/fd path would not survive.
 int exchange(xgmi_t x) {
     if (export_local(x) != 0) return -1;
-    if (send_kind(x->fd, K_REG, &x->mine, sizeof(x->mine)) != 0) OCM_FAIL(-1, "registration send failed");
-    Reg r;
-    uint8_t k = 0;
-    if (recv_kind(x->fd, &k, &r, sizeof(r), 10000) != (int)sizeof(r) || k != K_REG)
+    char out[1 + sizeof(Reg)];
+    out[0] = (char)K_REG;
+    std::memcpy(out + 1, &x->mine, sizeof(Reg));
+    if (mbox_send_fd(x->fd, out, sizeof(out), x->mine.host ? x->memfd : -1, 10000) != 1)
+        OCM_FAIL(-1, "registration send failed");
+    char in[1 + sizeof(Reg)];
+    int passed = -1;
+    struct pollfd q = {x->fd, POLLIN, 0};
+    if (poll(&q, 1, 10000) <= 0 || mbox_recv_fd(x->fd, in, sizeof(in), &passed, 10000) != 1 || in[0] != (char)K_REG) {
+        if (passed >= 0) close(passed);
         OCM_FAIL(-1, "registration receive failed");
-    return import_remote(x, r);
+    }
+    Reg r;
+    std::memcpy(&r, in + 1, sizeof(r));
+    return import_remote(x, r, passed);
 }
 
 int copy(xgmi_t x, bool write, size_t loff, size_t roff, size_t n) {

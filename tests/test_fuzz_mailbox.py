@@ -112,8 +112,8 @@ def test_other_users_are_refused(mesh_factory):
         s = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
         s.connect(b"\\0ocm_{m.ns}_d0")
         s.settimeout(5)
-        s.send(bytes(160))
         try:
+            s.send(bytes(160))  # the daemon may already have closed it (EPIPE)
             data = s.recv(160)
         except OSError as e:
             data = b""

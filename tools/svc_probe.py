@@ -36,8 +36,7 @@ for n in (0, 1, 2, 4, 8):
     CONFIGS[f"solo{n}"] = {"OCM_SERVICE_SOLO_TILES": str(n), "OCM_SERVICE_SOLO_TILES_HOST_GET": str(n)}
 # host-tier gets only: the round-2 default (1) against the earlier shared threshold (2)
 CONFIGS["hostget2"] = {"OCM_SERVICE_SOLO_TILES_HOST_GET": "2"}
-# the request record in BAR-mapped fine-grained HBM instead of host memory
-CONFIGS["dbhbm"] = {"OCM_SERVICE_DOORBELL": "hbm"}
+
 for g in (1, 16, 32, 64, 128, 256):
     CONFIGS[f"svc_g{g}"] = {"OCM_SERVICE_MAX": str(64 << 20), "OCM_SERVICE_BLOCKS": str(g)}
 
