@@ -45,6 +45,10 @@ enum Loc { LOC_HOST = 0, LOC_PINNED = 1, LOC_DEVICE = 2 };
 // launch + sync (13.7-14.9 us) up to 4 MiB on HBM pairs: 8.8 us at 128 KiB-1 MiB,
 // 11.8 us at 4 MiB; requests of <= 2 tiles (64 KiB) stay on workgroup 0 (4.6 us at 4 KiB).
 constexpr uint64_t kServiceMaxDefault = 4ull << 20;
+// Pairs whose remote half is all host tier: the gang stays ahead of the DMA
+// engines up to 16 MiB (8 MiB 152/155 us against 164/164, 16 MiB 300/303 against
+// 312/312 put/get; profiles/svc_max_ab_r02.json). OCM_SERVICE_MAX_HOST.
+constexpr uint64_t kServiceMaxHostDefault = 16ull << 20;
 constexpr int kServiceBlocksDefault = 32;
 constexpr int kServiceSoloTilesDefault = 2;
 constexpr unsigned kServiceProtoDefault = kServiceProtoWT;
@@ -171,7 +175,10 @@ struct State {
     bool svc_park_kernel = false;  // park the service during kernel transfers above svc_max (OCM_SERVICE_PARK_KERNEL)
     unsigned long long svc_seq = 0;
     uint64_t svc_ops = 0, svc_ns_post = 0, svc_ns_wait = 0;  // service diagnostics (ocm_x_service_stats)
-    uint64_t svc_max = kServiceMaxDefault;
+    uint64_t svc_max = kServiceMaxDefault;           // 0: the service is off (or failed)
+    uint64_t svc_max_host = kServiceMaxHostDefault;  // the same bound for host-tier-only pairs
+    // Largest blocking op the service takes for a pair with (`hbm`) or without HBM extents.
+    uint64_t svc_limit(bool hbm) const { return svc_max == 0 ? 0 : (hbm ? svc_max : svc_max_host); }
     unsigned long long svc_idle_ticks = 200000ull;  // 2 ms at 100 MHz: live only during bursts of small ops
     // network tier
     std::map<std::string, NetConn> net_conns;  // "ip:port#stream" -> connection

@@ -106,6 +106,8 @@ int ocm_init(void) {
     if (const char *k = std::getenv("OCM_LOCAL_CACHE")) s.dev_cache_cap = std::strtoull(k, nullptr, 0);
     const char *sm = std::getenv("OCM_SERVICE_MAX");
     s.svc_max = sm && *sm ? std::strtoull(sm, nullptr, 0) : kServiceMaxDefault;
+    const char *smh = std::getenv("OCM_SERVICE_MAX_HOST");  // unset: follows an explicit OCM_SERVICE_MAX
+    s.svc_max_host = smh && *smh ? std::strtoull(smh, nullptr, 0) : (sm && *sm ? s.svc_max : kServiceMaxHostDefault);
     s.svc_blocks = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_BLOCKS", kServiceBlocksDefault), 1024));
     s.svc_solo_tiles = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES", kServiceSoloTilesDefault));
     s.svc_solo_tiles_host_get = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES_HOST_GET", 1));
@@ -419,7 +421,7 @@ static int onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
         // Large blocking ops: launch on the allocation's lane under the lock, wait
         // outside it, so other threads' ops proceed meanwhile. Small ones keep the
         // copy service (no launch) and the network tier its own blocking path.
-        const bool service = a->loc == LOC_DEVICE && a->all_dev_ok && p->bytes <= s.svc_max;
+        const bool service = a->loc == LOC_DEVICE && a->all_dev_ok && p->bytes <= s.svc_limit(a->any_gpu);
         if (async || s.device < 0 || service || a->any_net)
             return xfer(a, put, lin, a->loc, p->dest_offset, p->bytes, async);
         if (xfer(a, put, lin, a->loc, p->dest_offset, p->bytes, true, &wait_done_flag) != 0) return -1;

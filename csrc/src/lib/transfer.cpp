@@ -311,7 +311,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         lin_dev && !dma_pick && (a->any_gpu || s.host_engine_kernel || len <= s.host_kernel_max);
     hipError_t err = hipSuccess;
     // Small blocking ops go to the resident copy service (no launch, no stream sync).
-    if (lin_dev && a->all_dev_ok && !async && len <= s.svc_max && !dma_pick) {
+    if (lin_dev && a->all_dev_ok && !async && len <= s.svc_limit(a->any_gpu) && !dma_pick) {
         XferArgs x;
         std::memset(&x, 0, sizeof(x));
         x.lin = lin;
@@ -338,7 +338,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     hipStream_t st = async ? lane_stream(a) : s.stream;
     if (honor_dep(a, st, false) != 0) return -1;
     if (use_kernel) {
-        if (s.svc_park_kernel && len > s.svc_max) service_park();  // A/B: no resident poller during the copy
+        if (s.svc_park_kernel && len > s.svc_limit(a->any_gpu)) service_park();  // A/B: no resident poller during the copy
         XferArgs x;
         std::memset(&x, 0, sizeof(x));
         x.lin = lin;

@@ -202,6 +202,27 @@ def test_copy_service_gang(mesh_factory, monkeypatch, blocks):
         a.free()
 
 
+def test_copy_service_host_tier_large(mesh_factory):
+    """Host-tier pairs keep blocking ops up to 16 MiB on the service gang (the
+    default OCM_SERVICE_MAX_HOST), striped over two owners' pinned slabs; sizes
+    around both service bounds, odd offsets, and the DMA path above them."""
+    m = mesh_factory(3, gpus=[0, 0, 0], policy="stripe")
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 20 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_HOST_TIER,
+                    stripe_unit=1 << 20)
+        assert all(e["tier"] == api.OCM_TIER_HOST for e in a.remote_info()["extents"])
+        for i, (size, off) in enumerate([((4 << 20) + 4, 12), (8 << 20, 1 << 20), ((16 << 20) - 4, 4096),
+                                         (16 << 20, 0), ((16 << 20) + 64, 64), (n, 0)]):
+            seed = 700 + i
+            a.fill(seed=seed)
+            a.put(off, off, size)
+            a.fill(seed=0)
+            a.get(off, off, size)
+            assert a.check(seed=seed, offset=off, nbytes=size - size % 4, first_word=off // 4) == 0, (size, off)
+        a.free()
+
+
 def test_launch_flag_completion(mesh_factory, monkeypatch):
     """Blocking launch-path ops complete on the kernel-published lane flag
     (service off): odd sizes/offsets up to the flag limit and above it (event

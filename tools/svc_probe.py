@@ -37,6 +37,8 @@ for n in (0, 1, 2, 4, 8):
 # host-tier gets only: the round-2 default (1) against the earlier shared threshold (2)
 CONFIGS["hostget2"] = {"OCM_SERVICE_SOLO_TILES_HOST_GET": "2"}
 
+# the service/SDMA crossover: the service takes blocking ops up to 16 MiB
+CONFIGS["svcmax16"] = {"OCM_SERVICE_MAX": str(16 << 20)}
 for g in (1, 16, 32, 64, 128, 256):
     CONFIGS[f"svc_g{g}"] = {"OCM_SERVICE_MAX": str(64 << 20), "OCM_SERVICE_BLOCKS": str(g)}
 
