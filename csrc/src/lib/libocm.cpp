@@ -1074,7 +1074,15 @@ void ocm_torch_free(void *ptr, ssize_t size, int device, void *stream) {
         tp.live.erase(it);
         tp.bytes -= std::min<uint64_t>(tp.bytes, (uint64_t)(size > 0 ? size : 0));
     }
-    if (S().inited) ocm_free(a);
+    State &s = S();
+    if (!s.inited) return;
+    {
+        // hipFree semantics: kernels still reading or writing the block finish
+        // before its bytes go back to the owner (which may hand them out again).
+        DeviceGuard g(s.device);
+        if (hipDeviceSynchronize() != hipSuccess) (void)hipGetLastError();
+    }
+    ocm_free(a);
 }
 
 // {blocks held by torch, their bytes}
