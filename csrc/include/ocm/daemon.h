@@ -19,6 +19,7 @@
 #include <memory>
 #include <set>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "ocm/arena.h"
@@ -27,6 +28,7 @@
 #include "ocm/netdata.h"
 #include "ocm/nodefile.h"
 #include "ocm/pmsg.h"
+#include "ocm/siphash.h"
 #include "ocm/sock.h"
 #include "ocm/tick.h"
 
@@ -227,11 +229,13 @@ private:
     // checkpoint / resume
     uint64_t boot_id_ = 0;               // this process lifetime
     size_t pinned_cpus_ = 0;             // event loop restricted to this many CPUs near the GPU (0: not pinned)
-    uint64_t mesh_token_ = 0;            // HELLO must carry it (hash of namespace + mesh key)
+    SipKey mesh_key_{};                  // HELLO MAC key (namespace + OCM_MESH_KEY)
+    std::unordered_map<uint64_t, uint64_t> hello_seen_;  // nonce -> ts_ms of HELLOs accepted in the window
+    bool hello_ok(const Msg &m);
     uint64_t data_token_ = 0;            // network-tier data server: random per boot
     NodeLinks links_{};                  // xGMI link table of our GPU (sent to rank0 after ADD_NODE)
     void probe_links();
-    void send_hello(int fd);
+    void send_hello(int fd, int dst_rank);
     bool resumed_ = false;               // rank0 restored its directory from state_file
     uint64_t saved_version_ = 0;
     long last_save_ms_ = 0;

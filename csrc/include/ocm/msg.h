@@ -129,6 +129,20 @@ struct NodeLinks {
 
 static_assert(sizeof(NodeLinks) <= 128, "NodeLinks fits the message union");
 
+// MSG_HELLO body: the first record on a mesh link. mac = SipHash-2-4 under the
+// key derived from namespace + OCM_MESH_KEY over (src, dst, ts_ms, nonce); the
+// acceptor checks dst, a +-10 min clock window and that the nonce is new, so a
+// recorded HELLO cannot be replayed.
+struct Hello {
+    int32_t src_rank;
+    int32_t dst_rank;
+    uint64_t ts_ms;   // CLOCK_REALTIME of the sender
+    uint64_t nonce;   // random per HELLO
+    uint64_t mac;
+    uint8_t pad[96];
+};
+static_assert(sizeof(Hello) == 128, "Hello fills the message union");
+
 struct Msg {
     uint32_t type;     // MsgType
     uint32_t status;   // MsgStatus
@@ -142,6 +156,7 @@ struct Msg {
         Region region;
         NodeConfig node;
         NodeLinks links;
+        Hello hello;
         uint8_t raw[128];
     } u;
 };

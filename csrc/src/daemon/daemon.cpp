@@ -198,10 +198,9 @@ int Daemon::init() {
             }
             OCM_WARN("rank %d: UNAUTHENTICATED mesh on %s (OCM_MESH_INSECURE=1, no OCM_MESH_KEY)", rank_, bind.c_str());
         }
-        // FNV-1a over namespace + shared key: strangers on the mesh port cannot join.
-        uint64_t h = 1469598103934665603ull;
-        for (char ch : ns_ + '\x1f' + cfg_.mesh_key) h = (h ^ (uint8_t)ch) * 1099511628211ull;
-        mesh_token_ = h ? h : 1;
+        // HELLOs are signed with a key derived from namespace + shared key:
+        // strangers on the mesh port cannot join, and a recorded HELLO cannot be replayed.
+        mesh_key_ = sip_derive_key(ns_ + '\x1f' + cfg_.mesh_key);
     }
     if (rank_ == 0) {
         gov_ = std::make_unique<Governor>(n_, cfg_.policy, cfg_.stripe_unit);
@@ -276,7 +275,7 @@ int Daemon::init() {
             OCM_WARN("rank %d unreachable; continuing without it", r);
             continue;
         }
-        send_hello(fd);
+        send_hello(fd, r);
         set_nonblocking(fd, true);
         auto c = std::make_unique<Conn>();
         c->fd = fd;

@@ -36,11 +36,10 @@ using namespace dm;
 
 void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
     if (from_fd >= 0) {
-        // An inbound link is anonymous until its HELLO carries our mesh token.
+        // An inbound link is anonymous until its HELLO carries a valid MAC.
         auto it = conns_.find(from_fd);
         if (it == conns_.end()) return;
-        if (it->second->peer_rank < 0 &&
-            (m.type != MSG_HELLO || m.seq != mesh_token_ || m.src_rank < 0 || m.src_rank >= n_ || m.src_rank == rank_)) {
+        if (it->second->peer_rank < 0 && !hello_ok(m)) {
             OCM_WARN("rank %d: dropping unauthenticated mesh link (%s)", rank_, msg_type_str(m.type));
             drop_conn(from_fd);
             return;

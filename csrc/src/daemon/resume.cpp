@@ -27,14 +27,58 @@
 namespace ocm {
 using namespace dm;
 
-void Daemon::send_hello(int fd) {
+namespace {
+
+uint64_t realtime_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    return (uint64_t)ts.tv_sec * 1000ull + (uint64_t)ts.tv_nsec / 1000000ull;
+}
+
+constexpr uint64_t kHelloWindowMs = 10ull * 60 * 1000;  // clock skew tolerated between daemons
+
+uint64_t hello_mac(const SipKey &k, const Hello &h) {
+    const uint64_t w[4] = {(uint64_t)(uint32_t)h.src_rank | ((uint64_t)(uint32_t)h.dst_rank << 32), h.ts_ms, h.nonce,
+                           (uint64_t)MSG_HELLO};
+    return siphash24(k, w, sizeof(w));
+}
+
+}  // namespace
+
+void Daemon::send_hello(int fd, int dst_rank) {
     Msg hello;
     std::memset(&hello, 0, sizeof(hello));
     hello.type = MSG_HELLO;
     hello.src_rank = rank_;
     hello.rank = rank_;
-    hello.seq = mesh_token_;
+    Hello &h = hello.u.hello;
+    h.src_rank = rank_;
+    h.dst_rank = dst_rank;
+    h.ts_ms = realtime_ms();
+    std::ifstream ur("/dev/urandom", std::ios::binary);
+    ur.read(reinterpret_cast<char *>(&h.nonce), sizeof(h.nonce));
+    if (!ur) h.nonce ^= boot_id_ ^ (h.ts_ms << 20) ^ (uint64_t)fd;
+    h.mac = hello_mac(mesh_key_, h);
     send_all(fd, &hello, sizeof(hello));
+}
+
+// First record of an inbound mesh link: a HELLO signed for us, fresh, never seen.
+bool Daemon::hello_ok(const Msg &m) {
+    const Hello &h = m.u.hello;
+    if (m.type != MSG_HELLO || m.src_rank < 0 || m.src_rank >= n_ || m.src_rank == rank_ || h.src_rank != m.src_rank ||
+        h.dst_rank != rank_ || hello_mac(mesh_key_, h) != h.mac)
+        return false;
+    const uint64_t now = realtime_ms();
+    const uint64_t skew = now > h.ts_ms ? now - h.ts_ms : h.ts_ms - now;
+    if (skew > kHelloWindowMs) {
+        OCM_WARN("rank %d: HELLO from rank %d is %llu ms off our clock", rank_, m.src_rank, (unsigned long long)skew);
+        return false;
+    }
+    for (auto it = hello_seen_.begin(); it != hello_seen_.end();) {  // forget what the window no longer admits
+        const uint64_t age = now > it->second ? now - it->second : it->second - now;
+        it = age > 2 * kHelloWindowMs ? hello_seen_.erase(it) : std::next(it);
+    }
+    return hello_seen_.emplace(h.nonce, h.ts_ms).second;  // a replay repeats its nonce
 }
 
 void Daemon::join_rank0() {
@@ -122,7 +166,7 @@ void Daemon::try_rejoin_rank0() {
     const NodeEntry &ne = nf_.nodes[0];
     int fd = tcp_connect(ne.ip, ne.ocm_port, 50);
     if (fd < 0) return;
-    send_hello(fd);
+    send_hello(fd, 0);
     set_nonblocking(fd, true);
     auto c = std::make_unique<Conn>();
     c->fd = fd;

@@ -260,6 +260,10 @@ public:
             *err = "socket collective: left neighbour never connected";
             return -1;
         }
+        if (mbox_peer_uid(left_) != (int)getuid()) {  // the ring is same-user daemons only
+            *err = "socket collective: left neighbour runs as another user";
+            return -1;
+        }
         return 0;
     }
     void *send_slot(int) override { return send_.data(); }

@@ -18,6 +18,7 @@
 #include "ocm/msg.h"
 #include "ocm/nodefile.h"
 #include "ocm/range_alloc.h"
+#include "ocm/siphash.h"
 
 using namespace ocm;
 
@@ -358,6 +359,19 @@ static void t_governor_topology() {
     }
 }
 
+// SipHash-2-4 reference vectors (key 00..0f; messages "" and 00..0e), and the
+// HELLO record fits the 160 B wire format.
+static void t_siphash() {
+    const SipKey k{0x0706050403020100ull, 0x0f0e0d0c0b0a0908ull};
+    uint8_t m[15];
+    for (int i = 0; i < 15; i++) m[i] = (uint8_t)i;
+    CHECK(siphash24(k, m, 0) == 0x726fdb47dd0e0e31ull);
+    CHECK(siphash24(k, m, 15) == 0xa129ca6149be45e5ull);
+    const SipKey a = sip_derive_key("ns\x1fsecret"), b = sip_derive_key("ns\x1fsecreT");
+    CHECK((a.k0 != b.k0 || a.k1 != b.k1) && a.k0 != a.k1);
+    CHECK(offsetof(Msg, u.hello.mac) == 32 + 24);
+}
+
 int main() {
     struct T {
         const char *name;
@@ -367,7 +381,7 @@ int main() {
                  {"governor_topology", t_governor_topology},
                  {"governor_checkpoint", t_governor_checkpoint},
                  {"stripe_geometry", t_stripe_geometry},
-                 {"arena_host", t_arena_host}};
+                 {"arena_host", t_arena_host},   {"siphash", t_siphash}};
     for (auto &t : tests) {
         int before = g_fail;
         t.fn();

@@ -126,8 +126,9 @@ class Mesh:
                 if not d.alive():
                     raise RuntimeError(f"ocmd rank {d.rank} exited ({d.proc.returncode}):\n{d.log()}")
                 if time.time() > deadline:
+                    logs = "".join(f"--- ocmd rank {x.rank} ---\n{x.log()[-2000:]}\n" for x in self.daemons)
                     self.stop()
-                    raise TimeoutError(f"ocmd rank {d.rank} not ready after {timeout}s:\n{d.log()}")
+                    raise TimeoutError(f"ocmd rank {d.rank} not ready after {timeout}s:\n{logs}")
                 time.sleep(0.02)
 
     def start(self, timeout: float = 60.0) -> "Mesh":

@@ -43,6 +43,7 @@ def test_bench_multi_rank(native, n):
     assert len(res["alloc_p50_us_per_rank"]) == n
     # control-plane extra: the same allocation path on TCP links and on socket-collective ticks
     cp = res["control_plane"]
+    assert "alloc_p50_us" in cp["tcp"] and "alloc_p50_us" in cp["socket"], cp
     assert cp["tcp"]["alloc_p50_us"] > 0 and cp["tcp"]["ticks_rank0"] == 0, cp
     assert cp["socket"]["alloc_p50_us"] > 0 and cp["socket"]["ticks_rank0"] > 0, cp
 

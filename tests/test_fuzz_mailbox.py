@@ -159,6 +159,77 @@ def test_mesh_port_rejects_strangers(mesh_factory):
         a.free()
 
 
+def _siphash24(k0, k1, data):
+    """SipHash-2-4 (the daemon's HELLO MAC), for crafting HELLOs here."""
+    M = (1 << 64) - 1
+    rotl = lambda x, b: ((x << b) | (x >> (64 - b))) & M  # noqa: E731
+    v = [k0 ^ 0x736F6D6570736575, k1 ^ 0x646F72616E646F6D, k0 ^ 0x6C7967656E657261, k1 ^ 0x7465646279746573]
+
+    def rnd():
+        v[0] = (v[0] + v[1]) & M; v[1] = rotl(v[1], 13) ^ v[0]; v[0] = rotl(v[0], 32)  # noqa: E702
+        v[2] = (v[2] + v[3]) & M; v[3] = rotl(v[3], 16) ^ v[2]  # noqa: E702
+        v[0] = (v[0] + v[3]) & M; v[3] = rotl(v[3], 21) ^ v[0]  # noqa: E702
+        v[2] = (v[2] + v[1]) & M; v[1] = rotl(v[1], 17) ^ v[2]; v[2] = rotl(v[2], 32)  # noqa: E702
+
+    def absorb(m):
+        v[3] ^= m
+        rnd()
+        rnd()
+        v[0] ^= m
+
+    full = len(data) & ~7
+    for i in range(0, full, 8):
+        absorb(int.from_bytes(data[i:i + 8], "little"))
+    absorb(((len(data) & 0xFF) << 56) | int.from_bytes(data[full:], "little"))
+    v[2] ^= 0xFF
+    for _ in range(4):
+        rnd()
+    return v[0] ^ v[1] ^ v[2] ^ v[3]
+
+
+def test_siphash_reference_vectors():
+    key = bytes(range(16))
+    k0, k1 = int.from_bytes(key[:8], "little"), int.from_bytes(key[8:], "little")
+    assert _siphash24(k0, k1, b"") == 0x726FDB47DD0E0E31
+    assert _siphash24(k0, k1, bytes(range(15))) == 0xA129CA6149BE45E5
+
+
+def _hello(ns, key, src, dst, ts_ms, nonce):
+    mat = (ns + "\x1f" + key).encode()
+    k0 = _siphash24(0x6F6E63696C6C6131, 0x6D6573682D6B6579, mat)
+    k1 = _siphash24(0x6F6E63696C6C6132, 0x6D6573682D6B6579, mat)
+    words = struct.pack("<QQQQ", (src & 0xFFFFFFFF) | ((dst & 0xFFFFFFFF) << 32), ts_ms, nonce, 11)
+    mac = _siphash24(k0, k1, words)
+    body = struct.pack("<iiQQQ", src, dst, ts_ms, nonce, mac).ljust(128, b"\0")
+    return MSG.pack(11, 0, 0, src, 0, src, 0, body)  # MSG_HELLO
+
+
+def test_mesh_hello_is_signed_fresh_and_single_use(mesh_factory):
+    """A HELLO needs a MAC under the mesh key, our rank as its destination, a
+    timestamp within the window and a nonce never seen before: a recorded HELLO
+    replayed on a new connection is refused."""
+    m = mesh_factory(2, env={"OCM_MESH_KEY": "k3y-for-the-test"})
+    port = m.ports[0]
+    now = int(time.time() * 1000)
+
+    def attempt(rec):
+        before = m.logs().count("dropping unauthenticated mesh link")
+        s = socket.create_connection(("127.0.0.1", port), timeout=5)
+        s.sendall(rec)
+        time.sleep(0.3)
+        s.close()
+        time.sleep(0.1)
+        return m.logs().count("dropping unauthenticated mesh link") > before  # True: refused
+
+    assert attempt(_hello(m.ns, "wrong key", 1, 0, now, 1))
+    assert attempt(_hello(m.ns, m.key, 1, 1, now, 2))                    # addressed to another rank
+    assert attempt(_hello(m.ns, m.key, 1, 0, now - 3600 * 1000, 3))       # an hour old
+    good = _hello(m.ns, m.key, 1, 0, now, 0x5EED)
+    assert not attempt(good)                                               # accepted
+    assert attempt(good)                                                   # the same bytes again: replay
+    assert all(d.alive() for d in m.daemons), m.logs()[-3000:]
+
+
 def test_data_server_requires_token(mesh_factory):
     m = mesh_factory(2, rank_env={0: {"OCM_HOST_ALIAS": "A"}, 1: {"OCM_HOST_ALIAS": "B"}})
     port = m.ready_info()[1]["data_port"]
