@@ -51,6 +51,24 @@ public:
             else
                 (void)ncclCommDestroy(comm_);
         }
+        // Queued ticks read and write the slots: free them only once the stream
+        // has drained (an abort ends a collective stuck on a dead peer). If it
+        // does not drain within 2 s, leak them rather than free memory a kernel
+        // may still touch.
+        if (stream_) {
+            (void)hipSetDevice(gpu_);
+            bool drained = false;
+            for (int i = 0; i < 20000 && !drained; i++) {
+                const hipError_t q = hipStreamQuery(stream_);
+                drained = q != hipErrorNotReady;
+                if (!drained) usleep(100);
+            }
+            (void)hipGetLastError();
+            if (!drained) {
+                OCM_WARN("rccl tick stream did not drain; leaving its %zu slots allocated", ring_.size());
+                return;
+            }
+        }
         for (auto &sl : ring_) {
             if (sl.ev) (void)hipEventDestroy(sl.ev);
             if (sl.hsend) (void)hipHostFree(sl.hsend);
