@@ -301,12 +301,18 @@ def ctrl_extra(dist, world: int, rank: int, local_rank: int, use_gpu: bool, samp
         if err is None:
             def run():
                 with api.Client(daemon_rank=rank, gpu=(local_rank if use_gpu else None), ns=ns) as c:
-                    if ctrl != "tcp":  # the transport comes up right after the mesh is complete
-                        deadline = time.time() + 10
+                    up = True
+                    if ctrl != "tcp":
+                        # The transport comes up after the mesh is complete (an RCCL
+                        # communicator over 8 GPUs can take seconds to initialise);
+                        # until then records ride TCP.
+                        deadline = time.time() + 30
                         while c.stats(rank)["ctrl_ticks"] == 0 and time.time() < deadline:
                             c.alloc(kind, local_bytes=4096, remote_bytes=1 << 20).free()
+                        up = c.stats(rank)["ctrl_ticks"] > 0
                     lat = wl.alloc_latency(c, kind, samples, local_bytes=4096, remote_bytes=1 << 20)
                     lat["ticks"] = c.stats(rank)["ctrl_ticks"]
+                    lat["up"] = up
                     return lat
 
             r, err = _local(run)
@@ -319,7 +325,8 @@ def ctrl_extra(dist, world: int, rank: int, local_rank: int, use_gpu: bool, samp
         out[ctrl] = {"alloc_p50_us": round(max(x["r"]["alloc_p50_us"] for x in res), 2),
                      "alloc_p99_us": round(max(x["r"]["alloc_p99_us"] for x in res), 2),
                      "free_p50_us": round(max(x["r"]["free_p50_us"] for x in res), 2),
-                     "ticks_rank0": res[0]["r"]["ticks"], "samples_per_rank": samples}
+                     "ticks_rank0": res[0]["r"]["ticks"], "samples_per_rank": samples,
+                     "transport_up_all_ranks": all(x["r"]["up"] for x in res)}
     return out
 
 
