@@ -1,0 +1,180 @@
+"""Randomised put/get against a host-side shadow of both halves.
+
+Every step picks an operation at random:
+- write random bytes into the local half
+- blocking or async put/get of a random (size, local offset, remote offset)
+- a batch of disjoint ops in one launch
+- a full read-back check
+Sizes run from 1 B to 24 MiB, so every path is drawn: copy-service solo and gang, launch path, DMA engines,
+unaligned heads and tails, and stripe-unit crossings. After each step the local half must equal its shadow.
+The remote half is checked through full gets. The pair is placed on a loopback HBM owner, a striped HBM pair,
+or the pinned host tier.
+
+    python tools/gpu_fuzz.py [--seconds 60] [--seed 1] [--configs hbm,stripe,host] [--out f.json]
+
+Exit 0 and one JSON line when every check passed. On the first mismatch it exits 1 and names the step.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+
+CONFIGS = {
+    # name: (daemons, policy, alloc flags name, stripe unit)
+    "hbm": (2, "ring", "OCM_ALLOC_LOOPBACK", 0),
+    "stripe": (4, "stripe", "OCM_ALLOC_STRIPE", 64 << 10),
+    "host": (2, "ring", "OCM_ALLOC_HOST_TIER", 0),
+}
+
+
+def _size(rng, cap):
+    r = rng.random()
+    if r < 0.35:
+        n = int(rng.integers(1, 4097))            # small: service solo, odd sizes
+    elif r < 0.7:
+        n = int(rng.integers(4096, 1 << 20))      # mid: service gang
+    elif r < 0.92:
+        n = int(rng.integers(1 << 20, 8 << 20))   # launch path / host-tier gang
+    else:
+        n = int(rng.integers(8 << 20, 24 << 20))  # above the service limits
+    return max(1, min(n, cap))
+
+
+def fuzz(client, api, name, seconds, seed, nbytes):
+    import torch
+
+    daemons, policy, flag, unit = CONFIGS[name]
+    flags = getattr(api, flag)
+    a = client.alloc(api.OCM_REMOTE_GPU if client.device >= 0 else api.OCM_REMOTE_RDMA, local_bytes=nbytes,
+                     remote_bytes=nbytes, flags=flags, stripe_unit=unit)
+    rng = np.random.default_rng(seed)
+    local = a.local_tensor()
+    on_dev = local.is_cuda
+    shadow_l = np.zeros(nbytes, dtype=np.uint8)
+    shadow_r = np.zeros(nbytes, dtype=np.uint8)
+    local.zero_()
+    a.put(0, 0, nbytes)  # both halves zero
+    if on_dev:
+        torch.cuda.synchronize()
+
+    def sync_local():
+        if on_dev:
+            torch.cuda.synchronize()
+
+    def check_local(step, what):
+        got = local.cpu().numpy() if on_dev else local.numpy()
+        bad = np.flatnonzero(got != shadow_l)
+        if bad.size:
+            raise AssertionError(f"{name} step {step} ({what}): {bad.size} local bytes differ, first at {bad[0]}")
+
+    counts = {}
+    t_end = time.time() + seconds
+    step = 0
+    while time.time() < t_end:
+        step += 1
+        r = rng.random()
+        if r < 0.15:
+            n = _size(rng, nbytes)
+            off = int(rng.integers(0, nbytes - n + 1))
+            data = rng.integers(0, 256, n, dtype=np.uint8)
+            local[off:off + n].copy_(torch.from_numpy(data))
+            sync_local()
+            shadow_l[off:off + n] = data
+            what = "write_local"
+        elif r < 0.75:
+            n = _size(rng, nbytes)
+            loff = int(rng.integers(0, nbytes - n + 1))
+            roff = int(rng.integers(0, nbytes - n + 1))
+            put = rng.random() < 0.5
+            asy = rng.random() < 0.25
+            (a.put if put else a.get)(loff, roff, n, async_=asy)
+            if asy:
+                a.wait()
+            if put:
+                shadow_r[roff:roff + n] = shadow_l[loff:loff + n]
+            else:
+                shadow_l[loff:loff + n] = shadow_r[roff:roff + n]
+            what = f"{'put' if put else 'get'}{'_async' if asy else ''}"
+        elif r < 0.9:
+            # disjoint local and remote ranges: batch ops run concurrently
+            k = int(rng.integers(2, 17))
+            span = nbytes // k
+            lslots = rng.permutation(k)
+            rslots = rng.permutation(k)
+            ops = []
+            for i in range(k):
+                n = int(rng.integers(1, max(2, min(span, 1 << 20))))
+                lo = int(lslots[i]) * span + int(rng.integers(0, span - n + 1))
+                ro = int(rslots[i]) * span + int(rng.integers(0, span - n + 1))
+                put = int(rng.random() < 0.5)
+                ops.append((put, lo, ro, n))
+            asy = rng.random() < 0.3
+            a.batch(ops, async_=asy)
+            if asy:
+                a.wait()
+            for put, lo, ro, n in ops:  # disjoint: order does not matter
+                if put:
+                    shadow_r[ro:ro + n] = shadow_l[lo:lo + n]
+            for put, lo, ro, n in ops:
+                if not put:
+                    shadow_l[lo:lo + n] = shadow_r[ro:ro + n]
+            what = "batch"
+        else:
+            # the remote half, through a full get
+            a.get(0, 0, nbytes)
+            shadow_l[:] = shadow_r
+            what = "full_get"
+        counts[what] = counts.get(what, 0) + 1
+        check_local(step, what)
+    a.get(0, 0, nbytes)
+    shadow_l[:] = shadow_r
+    check_local(step, "final")
+    a.free()
+    return {"steps": step, "ops": counts}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=60)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--configs", default="hbm,stripe,host")
+    ap.add_argument("--bytes", type=int, default=32 << 20)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    from oncilla_amd import api
+    from oncilla_amd.parallel.mesh import Mesh
+
+    import torch
+
+    gpu = 0 if torch.cuda.device_count() > 0 and not os.environ.get("OCM_NO_GPU") else None
+    res = {}
+    for i, name in enumerate(args.configs.split(",")):
+        daemons, policy, _, _ = CONFIGS[name]
+        with Mesh(daemons, gpus=[gpu] * daemons, policy=policy) as m:
+            with api.Client(daemon_rank=0, gpu=gpu, ns=m.ns) as c:
+                try:
+                    res[name] = fuzz(c, api, name, args.seconds / len(args.configs.split(",")), args.seed + i,
+                                     args.bytes)
+                except AssertionError as e:
+                    print(json.dumps({"ok": False, "config": name, "error": str(e)}), flush=True)
+                    return 1
+        print(name, json.dumps(res[name]), flush=True)
+    line = json.dumps({"ok": True, "seed": args.seed, "bytes": args.bytes, "configs": res})
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+    print(line)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
