@@ -4,6 +4,7 @@ Every step picks an operation at random:
 - write random bytes into the local half
 - blocking or async put/get of a random (size, local offset, remote offset)
 - a batch of disjoint ops in one launch
+- a plan of 1-3 such batches captured into a HIP graph and replayed twice (GPU only)
 - a full read-back check
 Sizes run from 1 B to 24 MiB, so every path is drawn: copy-service solo and gang, launch path, DMA engines,
 unaligned heads and tails, and stripe-unit crossings. After each step the local half must equal its shadow.
@@ -75,6 +76,27 @@ def fuzz(client, api, name, seconds, seed, nbytes):
         if bad.size:
             raise AssertionError(f"{name} step {step} ({what}): {bad.size} local bytes differ, first at {bad[0]}")
 
+    def rand_batch():
+        # disjoint local and remote ranges: the ops of one batch run concurrently
+        k = int(rng.integers(2, 17))
+        span = nbytes // k
+        lslots, rslots = rng.permutation(k), rng.permutation(k)
+        ops = []
+        for i in range(k):
+            n = int(rng.integers(1, max(2, min(span, 1 << 20))))
+            lo = int(lslots[i]) * span + int(rng.integers(0, span - n + 1))
+            ro = int(rslots[i]) * span + int(rng.integers(0, span - n + 1))
+            ops.append((int(rng.random() < 0.5), lo, ro, n))
+        return ops
+
+    def apply_batch(ops):
+        for put, lo, ro, n in ops:  # disjoint: order does not matter
+            if put:
+                shadow_r[ro:ro + n] = shadow_l[lo:lo + n]
+        for put, lo, ro, n in ops:
+            if not put:
+                shadow_l[lo:lo + n] = shadow_r[ro:ro + n]
+
     counts = {}
     t_end = time.time() + seconds
     step = 0
@@ -103,30 +125,25 @@ def fuzz(client, api, name, seconds, seed, nbytes):
             else:
                 shadow_l[loff:loff + n] = shadow_r[roff:roff + n]
             what = f"{'put' if put else 'get'}{'_async' if asy else ''}"
-        elif r < 0.9:
-            # disjoint local and remote ranges: batch ops run concurrently
-            k = int(rng.integers(2, 17))
-            span = nbytes // k
-            lslots = rng.permutation(k)
-            rslots = rng.permutation(k)
-            ops = []
-            for i in range(k):
-                n = int(rng.integers(1, max(2, min(span, 1 << 20))))
-                lo = int(lslots[i]) * span + int(rng.integers(0, span - n + 1))
-                ro = int(rslots[i]) * span + int(rng.integers(0, span - n + 1))
-                put = int(rng.random() < 0.5)
-                ops.append((put, lo, ro, n))
+        elif r < 0.85:
+            ops = rand_batch()
             asy = rng.random() < 0.3
             a.batch(ops, async_=asy)
             if asy:
                 a.wait()
-            for put, lo, ro, n in ops:  # disjoint: order does not matter
-                if put:
-                    shadow_r[ro:ro + n] = shadow_l[lo:lo + n]
-            for put, lo, ro, n in ops:
-                if not put:
-                    shadow_l[lo:lo + n] = shadow_r[ro:ro + n]
+            apply_batch(ops)
             what = "batch"
+        elif r < 0.9 and on_dev:
+            # a plan: 1-3 batch stages run in order, captured once, replayed twice
+            stages = [rand_batch() for _ in range(int(rng.integers(1, 4)))]
+            with client.plan() as plan:
+                for ops in stages:
+                    plan.add(a, ops)
+                for _ in range(2):
+                    plan.launch()
+                    for ops in stages:
+                        apply_batch(ops)
+            what = "plan"
         else:
             # the remote half, through a full get
             a.get(0, 0, nbytes)
