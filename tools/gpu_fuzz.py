@@ -9,7 +9,7 @@ Every step picks an operation at random:
 Sizes run from 1 B to 24 MiB, so every path is drawn: copy-service solo and gang, launch path, DMA engines,
 unaligned heads and tails, and stripe-unit crossings. After each step the local half must equal its shadow.
 The remote half is checked through full gets. The pair is placed on a loopback HBM owner, a striped HBM pair,
-or the pinned host tier.
+or the pinned host tier. Config `copy` fuzzes two-sided ocm_copy between allocations of every kind.
 
     python tools/gpu_fuzz.py [--seconds 60] [--seed 1] [--configs hbm,stripe,host] [--out f.json]
 
@@ -158,11 +158,95 @@ def fuzz(client, api, name, seconds, seed, nbytes):
     return {"steps": step, "ops": counts}
 
 
+class _Obj:
+    """One allocation and the shadows of its halves."""
+
+    def __init__(self, api, client, kind, nbytes, flags=0):
+        import torch
+
+        remote = kind in (api.OCM_REMOTE_GPU, api.OCM_REMOTE_RDMA)
+        self.a = client.alloc(kind, local_bytes=nbytes, remote_bytes=nbytes if remote else 0, flags=flags)
+        self.remote = remote
+        self.t = self.a.local_tensor()
+        self.t.zero_()
+        if self.t.is_cuda:
+            torch.cuda.synchronize()
+        self.l = np.zeros(nbytes, dtype=np.uint8)
+        self.r = np.zeros(nbytes, dtype=np.uint8) if remote else None
+        if remote:
+            self.a.put(0, 0, nbytes)
+
+    def local_now(self):
+        return self.t.cpu().numpy() if self.t.is_cuda else self.t.numpy().copy()
+
+
+def fuzz_copy(client, api, seconds, seed, nbytes):
+    """ocm_copy (two-sided) between random kinds, modelled step by step:
+    op_flag 0 swaps dst and src; local->remote stages through dst's local half
+    (local[src_offset_2] -> remote[dest_offset_2]); remote->local reads into
+    src's local half first; remote->remote copies directly."""
+    import torch
+
+    rng = np.random.default_rng(seed)
+    on_gpu = client.device >= 0
+    kinds = [api.OCM_LOCAL_HOST, api.OCM_REMOTE_RDMA, api.OCM_REMOTE_RDMA]
+    if on_gpu:
+        kinds += [api.OCM_LOCAL_GPU, api.OCM_REMOTE_GPU, api.OCM_REMOTE_GPU]
+    objs = [_Obj(api, client, k, nbytes, api.OCM_ALLOC_HOST_TIER if i % 2 else 0) for i, k in enumerate(kinds)]
+    counts = {}
+    t_end = time.time() + seconds
+    step = 0
+    while time.time() < t_end:
+        step += 1
+        if rng.random() < 0.2:
+            o = objs[int(rng.integers(len(objs)))]
+            n = _size(rng, nbytes)
+            off = int(rng.integers(0, nbytes - n + 1))
+            data = rng.integers(0, 256, n, dtype=np.uint8)
+            o.t[off:off + n].copy_(torch.from_numpy(data))
+            if o.t.is_cuda:
+                torch.cuda.synchronize()
+            o.l[off:off + n] = data
+            what = "write_local"
+        else:
+            i, j = rng.choice(len(objs), 2, replace=False)
+            dst, src = objs[int(i)], objs[int(j)]
+            n = _size(rng, nbytes)
+            so, do, so2, do2 = (int(rng.integers(0, nbytes - n + 1)) for _ in range(4))
+            flag = int(rng.random() < 0.6)
+            api.copy(dst.a, src.a, n, src_offset=so, dest_offset=do, src_offset_2=so2, dest_offset_2=do2,
+                     op_flag=flag)
+            d, sr = (dst, src) if flag else (src, dst)
+            if not sr.remote and not d.remote:
+                d.l[do:do + n] = sr.l[so:so + n]
+            elif not sr.remote and d.remote:
+                d.l[do:do + n] = sr.l[so:so + n]
+                d.r[do2:do2 + n] = d.l[so2:so2 + n]
+            elif sr.remote and not d.remote:
+                sr.l[so2:so2 + n] = sr.r[do2:do2 + n]
+                d.l[do:do + n] = sr.l[so:so + n]
+            else:
+                d.r[do:do + n] = sr.r[so:so + n]
+            what = ("local" if not sr.remote else "remote") + "_to_" + ("local" if not d.remote else "remote")
+        counts[what] = counts.get(what, 0) + 1
+        for k, o in enumerate(objs):
+            bad = np.flatnonzero(o.local_now() != o.l)
+            if bad.size:
+                raise AssertionError(f"copy step {step} ({what}): object {k} local differs at {bad.size} bytes")
+    for k, o in enumerate(objs):  # remote halves, through full gets
+        if o.remote:
+            o.a.get(0, 0, nbytes)
+            if not np.array_equal(o.local_now(), o.r):
+                raise AssertionError(f"copy final: object {k} remote half differs")
+        o.a.free()
+    return {"steps": step, "ops": counts}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=60)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--configs", default="hbm,stripe,host")
+    ap.add_argument("--configs", default="hbm,stripe,host,copy")
     ap.add_argument("--bytes", type=int, default=32 << 20)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
@@ -175,12 +259,15 @@ def main() -> int:
     gpu = 0 if torch.cuda.device_count() > 0 and not os.environ.get("OCM_NO_GPU") else None
     res = {}
     for i, name in enumerate(args.configs.split(",")):
-        daemons, policy, _, _ = CONFIGS[name]
+        daemons, policy, _, _ = CONFIGS.get(name, (2, "ring", None, 0))
         with Mesh(daemons, gpus=[gpu] * daemons, policy=policy) as m:
             with api.Client(daemon_rank=0, gpu=gpu, ns=m.ns) as c:
                 try:
-                    res[name] = fuzz(c, api, name, args.seconds / len(args.configs.split(",")), args.seed + i,
-                                     args.bytes)
+                    secs = args.seconds / len(args.configs.split(","))
+                    if name == "copy":
+                        res[name] = fuzz_copy(c, api, secs, args.seed + i, min(args.bytes, 8 << 20))
+                    else:
+                        res[name] = fuzz(c, api, name, secs, args.seed + i, args.bytes)
                 except AssertionError as e:
                     print(json.dumps({"ok": False, "config": name, "error": str(e)}), flush=True)
                     return 1
