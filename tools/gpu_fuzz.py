@@ -158,6 +158,29 @@ def fuzz(client, api, name, seconds, seed, nbytes):
     return {"steps": step, "ops": counts}
 
 
+def fuzz_threads(client, api, name, seconds, seed, nbytes, threads):
+    """`threads` threads at once, each on its own pair: the library's shared
+    machinery (copy service, lanes, library stream, locks) under concurrency."""
+    import threading
+
+    out, errs = [None] * threads, []
+
+    def work(k):
+        try:
+            out[k] = fuzz(client, api, name, seconds, seed * 100 + k, nbytes // threads)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(f"thread {k}: {e}")
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errs:
+        raise AssertionError("; ".join(errs))
+    return {"threads": threads, "steps": sum(o["steps"] for o in out)}
+
+
 class _Obj:
     """One allocation and the shadows of its halves."""
 
@@ -248,6 +271,7 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--configs", default="hbm,stripe,host,copy")
     ap.add_argument("--bytes", type=int, default=32 << 20)
+    ap.add_argument("--threads", type=int, default=1, help="threads, each fuzzing its own pair at once")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
 
@@ -266,6 +290,8 @@ def main() -> int:
                     secs = args.seconds / len(args.configs.split(","))
                     if name == "copy":
                         res[name] = fuzz_copy(c, api, secs, args.seed + i, min(args.bytes, 8 << 20))
+                    elif args.threads > 1:
+                        res[name] = fuzz_threads(c, api, name, secs, args.seed + i, args.bytes, args.threads)
                     else:
                         res[name] = fuzz(c, api, name, secs, args.seed + i, args.bytes)
                 except AssertionError as e:
