@@ -110,6 +110,11 @@ void xfer_batch_wave_ops(const XferBatchOp *ops, uint32_t n, uint64_t total_tile
 // tile shift for a remote layout: 4 KiB wave-tiles, or the stripe unit when smaller.
 uint32_t xfer_batch_tile_shift(uint32_t n_ext, uint32_t unit_shift);
 hipError_t xfer_batch_launch(const XferBatchArgs &a, const XferTuning &t, hipStream_t stream);
+// The same launch as a kernel node of `graph` after `dep` (nullptr: a root node);
+// *node is the new node (an empty node when there is nothing to copy). `a` must
+// stay alive as long as the graph.
+hipError_t xfer_batch_graph_node(hipGraph_t graph, hipGraphNode_t dep, const XferBatchArgs &a, const XferTuning &t,
+                                 hipGraphNode_t *node);
 
 // ---- persistent copy service (low-latency blocking one-sided ops) ----
 // A resident gang of `blocks` workgroups. Workgroup 0 polls one 128-byte

@@ -522,6 +522,27 @@ hipError_t xfer_batch_launch(const XferBatchArgs &a, const XferTuning &t, hipStr
     return hipGetLastError();
 }
 
+hipError_t xfer_batch_graph_node(hipGraph_t graph, hipGraphNode_t dep, const XferBatchArgs &a, const XferTuning &t,
+                                 hipGraphNode_t *node) {
+    const size_t ndep = dep ? 1 : 0;
+    if (a.total_tiles == 0 || a.n_ops == 0) return hipGraphAddEmptyNode(node, graph, dep ? &dep : nullptr, ndep);
+    if (a.n_ext < 1 || a.n_ext > (uint32_t)kXferMaxExtents || a.grid == 0) return hipErrorInvalidValue;
+    if (a.n_ops > (uint32_t)kXferInlineOps && (!a.ops || !a.wave_op)) return hipErrorInvalidValue;
+    // Parameters by address: `a` must outlive the graph (the plan's stage
+    // storage), whether or not the runtime copies them into the node.
+    void *params[] = {const_cast<XferBatchArgs *>(&a)};
+    hipKernelNodeParams kp;
+    std::memset(&kp, 0, sizeof(kp));
+    kp.func = t.nontemporal ? reinterpret_cast<void *>(&xfer_batch_kernel<true>)
+                            : reinterpret_cast<void *>(&xfer_batch_kernel<false>);
+    kp.gridDim = dim3(a.grid);
+    kp.blockDim = dim3(kThreads);
+    kp.sharedMemBytes = 0;
+    kp.kernelParams = params;
+    kp.extra = nullptr;
+    return hipGraphAddKernelNode(node, graph, dep ? &dep : nullptr, ndep, &kp);
+}
+
 // ---- persistent copy service ----
 
 namespace {

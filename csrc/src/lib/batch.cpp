@@ -259,7 +259,7 @@ int ocm_plan_add(ocm_plan_t p, ocm_alloc_t a, const struct ocm_params *ops, int 
     p->bytes += moved;
     p->n_ops += (uint64_t)n_ops;
     a->plans++;
-    plan_drop_graph(p);  // re-captured at the next launch
+    plan_drop_graph(p);  // rebuilt at the next launch (the stages may have moved)
     return 0;
 }
 
@@ -273,22 +273,24 @@ int ocm_plan_launch(ocm_plan_t p, void *stream) {
     DeviceGuard g(s.device);
     hipError_t e = hipSuccess;
     if (!p->exec) {
-        // Capture the stage chain once; every later launch is one hipGraphLaunch.
-        hipStream_t cs = nullptr;
-        e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
-        for (size_t i = 0; e == hipSuccess && i < p->stages.size(); i++)
-            e = xfer_batch_launch(p->stages[i].args, s.tuning, cs);
+        // Build the stage chain as a graph once (explicit kernel nodes, no stream
+        // capture: a capture would fail if another thread synchronized the device
+        // meanwhile, tools/gpu_fuzz.py --threads); every later launch is one
+        // hipGraphLaunch.
         hipGraph_t graph = nullptr;
-        hipError_t e2 = cs ? hipStreamEndCapture(cs, &graph) : hipErrorInvalidValue;
-        if (e == hipSuccess) e = e2;
+        e = hipGraphCreate(&graph, 0);
+        hipGraphNode_t prev = nullptr;
+        for (size_t i = 0; e == hipSuccess && i < p->stages.size(); i++) {
+            hipGraphNode_t node = nullptr;
+            e = xfer_batch_graph_node(graph, prev, p->stages[i].args, s.tuning, &node);
+            prev = node;
+        }
         if (e == hipSuccess) e = hipGraphInstantiate(&p->exec, graph, nullptr, nullptr, 0);
-        if (cs) (void)hipStreamDestroy(cs);
         if (e != hipSuccess) {
             (void)hipGetLastError();
             if (graph) (void)hipGraphDestroy(graph);
             p->exec = nullptr;
-            OCM_FAIL(-1, "ocm_plan_launch: graph capture: %s", hipGetErrorString(e));
+            OCM_FAIL(-1, "ocm_plan_launch: graph build: %s", hipGetErrorString(e));
         }
         p->graph = graph;
     }
