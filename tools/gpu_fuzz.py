@@ -4,7 +4,9 @@ Every step picks an operation at random:
 - write random bytes into the local half
 - blocking or async put/get of a random (size, local offset, remote offset)
 - a batch of disjoint ops in one launch
-- a plan of 1-3 such batches captured into a HIP graph and replayed twice (GPU only)
+- a plan of 1-3 such batches built into a HIP graph and replayed twice (GPU only)
+- torch writes on one stream -> async op after ocm_stream_wait -> snapshot on another stream after
+  ocm_stream_signal, with no host sync in between (GPU only)
 - a full read-back check
 Sizes run from 1 B to 24 MiB, so every path is drawn: copy-service solo and gang, launch path, DMA engines,
 unaligned heads and tails, and stripe-unit crossings. After each step the local half must equal its shadow.
@@ -97,6 +99,7 @@ def fuzz(client, api, name, seconds, seed, nbytes):
             if not put:
                 shadow_l[lo:lo + n] = shadow_r[ro:ro + n]
 
+    streams = (torch.cuda.Stream(device=local.device), torch.cuda.Stream(device=local.device)) if on_dev else None
     counts = {}
     t_end = time.time() + seconds
     step = 0
@@ -144,6 +147,41 @@ def fuzz(client, api, name, seconds, seed, nbytes):
                     for ops in stages:
                         apply_batch(ops)
             what = "plan"
+        elif r < 0.93 and on_dev:
+            # Stream interop, no host sync between the steps: torch writes the local
+            # half on s1 (behind a GPU sleep, so a missing wait reads stale bytes),
+            # the async op waits for s1 (ocm_stream_wait), and s2 snapshots the local
+            # half after the op (ocm_stream_signal).
+            n = _size(rng, nbytes)
+            off = int(rng.integers(0, nbytes - n + 1))
+            data = rng.integers(0, 256, n, dtype=np.uint8)
+            dev = torch.from_numpy(data).to(local.device)
+            torch.cuda.synchronize()
+            s1, s2 = streams
+            with torch.cuda.stream(s1):
+                if hasattr(torch.cuda, "_sleep"):
+                    torch.cuda._sleep(200000)
+                local[off:off + n].copy_(dev)
+            shadow_l[off:off + n] = data
+            a.stream_wait(s1)
+            m = _size(rng, nbytes)
+            loff = int(rng.integers(0, nbytes - m + 1))
+            roff = int(rng.integers(0, nbytes - m + 1))
+            put = rng.random() < 0.5
+            (a.put if put else a.get)(loff, roff, m, async_=True)
+            if put:
+                shadow_r[roff:roff + m] = shadow_l[loff:loff + m]
+            else:
+                shadow_l[loff:loff + m] = shadow_r[roff:roff + m]
+            a.stream_signal(s2)
+            with torch.cuda.stream(s2):
+                snap = local.clone()
+            s2.synchronize()
+            a.wait()
+            bad = np.flatnonzero(snap.cpu().numpy() != shadow_l)
+            if bad.size:
+                raise AssertionError(f"{name} step {step} (streams): snapshot differs at {bad.size} bytes")
+            what = "streams_put" if put else "streams_get"
         else:
             # the remote half, through a full get
             a.get(0, 0, nbytes)
