@@ -40,3 +40,29 @@ def test_fuzz_transfers_threads_gpu(native):
     stream capture failing when another thread synchronized the device during
     the capture; plans are now built from explicit graph nodes."""
     _run(15, dict(os.environ), 32 << 20, ("--threads", "4", "--configs", "hbm,stripe,host"))
+
+
+def _procs(mesh_factory, env, seconds, nbytes):
+    """Three fuzzing apps at once on one 4-daemon mesh, attached to different
+    daemons: the daemons serve concurrent allocations, frees and imports while
+    the apps move data."""
+    m = mesh_factory(4, gpus=[None if env.get("OCM_NO_GPU") else 0] * 4, policy="stripe")
+    ps = [subprocess.Popen([sys.executable, os.path.join(REPO, "tools", "gpu_fuzz.py"), "--ns", m.ns,
+                            "--daemon-rank", str(k), "--seconds", str(seconds), "--seed", str(90 + k),
+                            "--bytes", str(nbytes), "--configs", "hbm,stripe,host"],
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env) for k in range(3)]
+    outs = [p.communicate(timeout=300)[0] for p in ps]
+    for p, out in zip(ps, outs):
+        assert p.returncode == 0, out[-3000:] + m.logs()[-2000:]
+        assert json.loads([l for l in out.splitlines() if l.startswith("{")][-1])["ok"]
+    assert all(d.alive() for d in m.daemons)
+
+
+def test_fuzz_apps_share_a_mesh_cpu(native, mesh_factory, monkeypatch):
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    _procs(mesh_factory, dict(os.environ, OCM_NO_GPU="1"), 6, 4 << 20)
+
+
+@pytest.mark.gpu
+def test_fuzz_apps_share_a_mesh_gpu(native, mesh_factory):
+    _procs(mesh_factory, dict(os.environ), 15, 16 << 20)

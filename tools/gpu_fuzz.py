@@ -20,6 +20,7 @@ Exit 0 and one JSON line when every check passed. On the first mismatch it exits
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -310,6 +311,8 @@ def main() -> int:
     ap.add_argument("--configs", default="hbm,stripe,host,copy")
     ap.add_argument("--bytes", type=int, default=32 << 20)
     ap.add_argument("--threads", type=int, default=1, help="threads, each fuzzing its own pair at once")
+    ap.add_argument("--ns", default=None, help="attach to this running mesh instead of starting one per config")
+    ap.add_argument("--daemon-rank", type=int, default=0)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
 
@@ -322,8 +325,10 @@ def main() -> int:
     res = {}
     for i, name in enumerate(args.configs.split(",")):
         daemons, policy, _, _ = CONFIGS.get(name, (2, "ring", None, 0))
-        with Mesh(daemons, gpus=[gpu] * daemons, policy=policy) as m:
-            with api.Client(daemon_rank=0, gpu=gpu, ns=m.ns) as c:
+        with contextlib.ExitStack() as stack:
+            # --ns: attach to a running mesh (several fuzzing apps at once); else a mesh per config
+            ns = args.ns or stack.enter_context(Mesh(daemons, gpus=[gpu] * daemons, policy=policy)).ns
+            with api.Client(daemon_rank=args.daemon_rank, gpu=gpu, ns=ns) as c:
                 try:
                     secs = args.seconds / len(args.configs.split(","))
                     if name == "copy":
