@@ -574,3 +574,45 @@ def test_torch_tensors_in_peer_hbm(mesh_factory, host_tier):
             time.sleep(0.1)
         assert c.stats(1)[used] == before
 
+
+def test_torch_pool_random_churn(mesh_factory):
+    """Random tensor sizes created and dropped under RemoteMemPool, each filled
+    with its own value: torch splits and reuses the remote blocks, and no live
+    tensor may ever see another's bytes (overlapping blocks would show)."""
+    import gc
+    import random
+
+    from oncilla_amd.torch_pool import RemoteMemPool
+
+    m = mesh_factory(2, gpus=[0, 0])
+    rng = random.Random(5)
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        pool = RemoteMemPool(c, remote_rank=1)
+        live = {}
+        for step in range(400):
+            if live and rng.random() < 0.45:
+                k = rng.choice(list(live))
+                t, v = live.pop(k)
+                assert bool((t == v).all()), (step, k)
+                del t
+            else:
+                n = rng.choice([1, 7, 513, 4096, 100_000, 1 << 20, 3 << 20, 9 << 20])
+                with pool:
+                    t = torch.full((n,), float(step), device="cuda:0")
+                live[step] = (t, float(step))
+            if step % 50 == 49:
+                for k, (t, v) in live.items():
+                    assert bool((t == v).all()), (step, k)
+                torch.cuda.empty_cache()  # hands free blocks back to the owner mid-run
+        for k, (t, v) in live.items():
+            assert bool((t == v).all()), k
+        assert RemoteMemPool.stats()["blocks"] >= 1
+        live.clear()
+        del t  # the loop variable still holds the last tensor
+        gc.collect()
+        del pool
+        gc.collect()
+        torch.cuda.empty_cache()
+        torch.cuda.synchronize()
+        assert RemoteMemPool.stats()["blocks"] == 0
+
