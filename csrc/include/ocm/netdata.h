@@ -51,7 +51,7 @@ public:
     // the net: handle their own daemon hands them).
     DataServer(Arena *arena, int gpu, uint64_t token);
     ~DataServer();
-    int start(const std::string &bind_ip);  // ephemeral port
+    int start(const std::string &bind_ip, int port = 0);  // port 0: ephemeral
     int port() const { return port_; }
     void stop();
     // Open extent [offset, offset+bytes) of `slab_id` to network requests;

@@ -159,7 +159,20 @@ int Daemon::init() {
         data_token_ = tok ? tok : ((uint64_t)getpid() << 20) ^ (uint64_t)now_ms();
     }
     data_ = std::make_unique<DataServer>(arena_.get(), gpu_, data_token_);
-    if (data_->start(cfg_.bind_ip.empty() ? "0.0.0.0" : cfg_.bind_ip) != 0) {
+    // The nodefile's 5th column (the reference's rdmacm port) fixes the data
+    // server's port, for firewalled clusters; 0 or out of range: ephemeral.
+    const int want_port = nf_.nodes[rank_].data_port > 0 && nf_.nodes[rank_].data_port <= 65535
+                              ? nf_.nodes[rank_].data_port
+                              : 0;
+    const std::string data_bind = cfg_.bind_ip.empty() ? "0.0.0.0" : cfg_.bind_ip;
+    if (want_port && data_->start(data_bind, want_port) != 0) {
+        OCM_WARN("rank %d: data port %d unavailable; using an ephemeral port", rank_, want_port);
+        data_ = std::make_unique<DataServer>(arena_.get(), gpu_, data_token_);
+        if (data_->start(data_bind) != 0) data_.reset();
+    } else if (!want_port && data_->start(data_bind) != 0) {
+        data_.reset();
+    }
+    if (!data_) {
         OCM_WARN("rank %d: network data server unavailable; cross-node placement disabled here", rank_);
         data_.reset();
     }

@@ -50,8 +50,8 @@ DataServer::DataServer(Arena *arena, int gpu, uint64_t token) : arena_(arena), g
 
 DataServer::~DataServer() { stop(); }
 
-int DataServer::start(const std::string &bind_ip) {
-    listen_fd_ = tcp_listen(bind_ip, 0, 64);
+int DataServer::start(const std::string &bind_ip, int port) {
+    listen_fd_ = tcp_listen(bind_ip, port, 64);
     if (listen_fd_ < 0) return -1;
     struct sockaddr_in a;
     socklen_t l = sizeof(a);

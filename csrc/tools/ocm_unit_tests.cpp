@@ -372,7 +372,22 @@ static void t_siphash() {
     CHECK(offsetof(Msg, u.hello.mac) == 32 + 24);
 }
 
-int main() {
+int main(int argc, char **argv) {
+    if (argc > 1 && std::strcmp(argv[1], "--nodefile") == 0) {
+        // ocm_unit_tests --nodefile F...: parse each with the daemon's parser
+        int bad = 0;
+        for (int i = 2; i < argc; i++) {
+            NodeFile nf;
+            std::string err;
+            if (parse_nodefile(argv[i], &nf, &err) != 0) {
+                printf("FAIL %s: %s\n", argv[i], err.c_str());
+                bad++;
+            } else {
+                printf("OK %s: %zu daemons\n", argv[i], nf.nodes.size());
+            }
+        }
+        return bad ? 1 : 0;
+    }
     struct T {
         const char *name;
         std::function<void()> fn;

@@ -33,11 +33,16 @@ def free_ports(n: int) -> list[int]:
     return ports
 
 
-def write_nodefile(path: str, ports: Sequence[int], gpus: Optional[Sequence[int]] = None, host: str = "127.0.0.1") -> str:
+def write_nodefile(path: str, ports: Sequence[int], gpus: Optional[Sequence[int]] = None, host: str = "127.0.0.1",
+                   data_ports: Optional[Sequence[int]] = None) -> str:
+    """The reference's nodefile format plus a gpu column. data_ports (the
+    reference's rdmacm column) fix the network-tier data servers' ports; 0 lets
+    each daemon pick one."""
     lines = ["#rank dns ethernet_ip ocm_port rdmacm_port gpu"]
     for r, p in enumerate(ports):
         g = "" if gpus is None or gpus[r] is None else f" gpu={gpus[r]}"
-        lines.append(f"{r} localhost {host} {p} 0{g}")
+        d = 0 if data_ports is None else int(data_ports[r])
+        lines.append(f"{r} localhost {host} {p} {d}{g}")
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
     return path
@@ -72,7 +77,7 @@ class Mesh:
                  policy: str = "ring", extra_args: Sequence[str] = (), env: Optional[dict] = None,
                  workdir: Optional[str] = None, ports: Optional[Sequence[int]] = None, ranks: Optional[Sequence[int]] = None,
                  rank_env: Optional[dict] = None, bin_dir: Optional[str] = None, watch: bool = True,
-                 key: Optional[str] = None):
+                 key: Optional[str] = None, data_ports: Optional[Sequence[int]] = None):
         self.n = n
         self.gpus = list(gpus) if gpus is not None else [None] * n
         self.ns = ns or f"m{uuid.uuid4().hex[:10]}"
@@ -84,6 +89,7 @@ class Mesh:
         self.watch = watch  # daemons exit when this process does (no orphans after a crash)
         self.workdir = workdir or tempfile.mkdtemp(prefix=f"ocm_{self.ns}_")
         self.ports = list(ports) if ports is not None else free_ports(n)
+        self.data_ports = list(data_ports) if data_ports is not None else None
         self.ranks = list(ranks) if ranks is not None else list(range(n))  # which ranks THIS process launches
         self.nodefile = os.path.join(self.workdir, "nodefile")
         self.daemons: list[Daemon] = []
@@ -132,7 +138,7 @@ class Mesh:
                 time.sleep(0.02)
 
     def start(self, timeout: float = 60.0) -> "Mesh":
-        write_nodefile(self.nodefile, self.ports, self.gpus)
+        write_nodefile(self.nodefile, self.ports, self.gpus, data_ports=self.data_ports)
         for r in self.ranks:
             log = os.path.join(self.workdir, f"ocmd.{r}.log")
             open(log, "w").close()

@@ -45,3 +45,17 @@ def test_kernels_use_no_scratch(src, min_kernels):
     assert len(names) >= min_kernels and len(scratch) == len(names)
     assert all(s == 0 for s in scratch), dict(zip(names, scratch))
     assert all(s == 0 for s in spills), dict(zip(names, spills))
+
+
+def test_example_nodefiles_parse(native, tool):
+    """examples/nodefiles/* parse with the daemon's own parser (the reference
+    format, the one-node 8-GPU layout, two nodes with fixed data ports)."""
+    import glob
+    import os
+
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                          "examples", "nodefiles", "*")))
+    assert len(files) >= 3
+    rc, out = tool([f"{native}/ocm_unit_tests", "--nodefile", *files])
+    assert rc == 0, out
+    assert "OK" in out and "16 daemons" in out and "8 daemons" in out

@@ -45,6 +45,26 @@ def test_two_nodes_remote_is_network(mesh_factory):
         assert c.stats(1)["host_used"] == 0
 
 
+def test_data_ports_from_the_nodefile(mesh_factory):
+    """The nodefile's 5th column (the reference's rdmacm port) fixes each data
+    server's port, as a firewalled cluster needs; handles carry it."""
+    from oncilla_amd.parallel.mesh import free_ports
+
+    dports = free_ports(2)
+    m = mesh_factory(2, rank_env=hosts("nodeA", "nodeB"), data_ports=dports)
+    assert [r["data_port"] for r in m.ready_info()] == dports
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)
+        assert a.remote_info()["extents"][0]["net"]
+        assert f":{dports[1]}:" in a.extent_handle(0).decode()
+        a.fill(seed=5)
+        a.put(0, 0, 1 << 20)
+        a.fill(seed=0)
+        a.get(0, 0, 1 << 20)
+        assert a.check(seed=5) == 0
+        a.free()
+
+
 def test_same_host_preferred_over_network(mesh_factory):
     m = mesh_factory(4, rank_env=hosts("nodeA", "nodeA", "nodeB", "nodeB"))
     with api.Client(daemon_rank=2, ns=m.ns) as c:
