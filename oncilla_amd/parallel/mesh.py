@@ -43,8 +43,12 @@ def write_nodefile(path: str, ports: Sequence[int], gpus: Optional[Sequence[int]
         g = "" if gpus is None or gpus[r] is None else f" gpu={gpus[r]}"
         d = 0 if data_ports is None else int(data_ports[r])
         lines.append(f"{r} localhost {host} {p} {d}{g}")
-    with open(path, "w") as f:
+    # Atomic: ranks launched by different processes (torchrun) each write the
+    # same shared file, and a daemon may be reading it meanwhile.
+    tmp = f"{path}.{os.getpid()}.tmp"
+    with open(tmp, "w") as f:
         f.write("\n".join(lines) + "\n")
+    os.replace(tmp, path)
     return path
 
 

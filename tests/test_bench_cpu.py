@@ -34,7 +34,7 @@ def test_bench_multi_rank(native, n):
                         "--master-addr", "127.0.0.1", "--master-port", str(29533 + n), os.path.join(REPO, "bench.py"),
                         "--gpus", str(n), "--device", "cpu", "--steps", "2", "--warmup", "1", "--max-bytes",
                         str(4 << 20), "--alloc-samples", "20"], capture_output=True, text=True, timeout=300, cwd="/tmp")
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-1500:]
     res = _last_json(r.stdout)
     assert res["n_gpus"] == n and res["value"] > 0 and res["config"]["parallelism"] == f"stripe{n}"
     assert res["config"]["extents_per_pair"] == n - 1  # 8 MiB+1 pair = 9 stripe units: every peer gets one
