@@ -11,7 +11,8 @@ Every step picks an operation at random:
 Sizes run from 1 B to 24 MiB, so every path is drawn: copy-service solo and gang, launch path, DMA engines,
 unaligned heads and tails, and stripe-unit crossings. After each step the local half must equal its shadow.
 The remote half is checked through full gets. The pair is placed on a loopback HBM owner, a striped HBM pair,
-or the pinned host tier. Config `copy` fuzzes two-sided ocm_copy between allocations of every kind.
+or the pinned host tier, or (config `net`) on a daemon of another "node", through the network tier's data server.
+Config `copy` fuzzes two-sided ocm_copy between allocations of every kind.
 
     python tools/gpu_fuzz.py [--seconds 60] [--seed 1] [--configs hbm,stripe,host] [--out f.json]
 
@@ -36,7 +37,11 @@ CONFIGS = {
     "hbm": (2, "ring", "OCM_ALLOC_LOOPBACK", 0),
     "stripe": (4, "stripe", "OCM_ALLOC_STRIPE", 64 << 10),
     "host": (2, "ring", "OCM_ALLOC_HOST_TIER", 0),
+    # the owner on another "node" (OCM_HOST_ALIAS): the network tier's data server
+    "net": (2, "ring", "OCM_ALLOC_NO_SPILL", 0),
 }
+RANK_ENV = {"net": {0: {"OCM_HOST_ALIAS": "nodeA"}, 1: {"OCM_HOST_ALIAS": "nodeB"}}}
+NO_PLANS = {"net"}  # plans need device-addressable extents
 
 
 def _size(rng, cap):
@@ -59,6 +64,8 @@ def fuzz(client, api, name, seconds, seed, nbytes):
     flags = getattr(api, flag)
     a = client.alloc(api.OCM_REMOTE_GPU if client.device >= 0 else api.OCM_REMOTE_RDMA, local_bytes=nbytes,
                      remote_bytes=nbytes, flags=flags, stripe_unit=unit)
+    if name == "net" and not all(e["net"] for e in a.remote_info()["extents"]):
+        raise AssertionError(f"net: the remote half is not on another node: {a.remote_info()}")
     rng = np.random.default_rng(seed)
     local = a.local_tensor()
     on_dev = local.is_cuda
@@ -137,7 +144,7 @@ def fuzz(client, api, name, seconds, seed, nbytes):
                 a.wait()
             apply_batch(ops)
             what = "batch"
-        elif r < 0.9 and on_dev:
+        elif r < 0.9 and on_dev and name not in NO_PLANS:
             # a plan: 1-3 batch stages run in order, captured once, replayed twice
             stages = [rand_batch() for _ in range(int(rng.integers(1, 4)))]
             with client.plan() as plan:
@@ -327,7 +334,8 @@ def main() -> int:
         daemons, policy, _, _ = CONFIGS.get(name, (2, "ring", None, 0))
         with contextlib.ExitStack() as stack:
             # --ns: attach to a running mesh (several fuzzing apps at once); else a mesh per config
-            ns = args.ns or stack.enter_context(Mesh(daemons, gpus=[gpu] * daemons, policy=policy)).ns
+            ns = args.ns or stack.enter_context(Mesh(daemons, gpus=[gpu] * daemons, policy=policy,
+                                                     rank_env=RANK_ENV.get(name))).ns
             with api.Client(daemon_rank=args.daemon_rank, gpu=gpu, ns=ns) as c:
                 try:
                     secs = args.seconds / len(args.configs.split(","))
