@@ -23,12 +23,12 @@ def _run(seconds, env, nbytes, extra=()):
 
 
 def test_fuzz_transfers_cpu(native):
-    _run(6, dict(os.environ, OCM_NO_GPU="1"), 4 << 20)
+    _run(8, dict(os.environ, OCM_NO_GPU="1"), 4 << 20, ("--configs", "hbm,stripe,host,net,copy"))
 
 
 @pytest.mark.gpu
 def test_fuzz_transfers_gpu(native):
-    res = _run(24, dict(os.environ), 32 << 20)
+    res = _run(25, dict(os.environ), 32 << 20, ("--configs", "hbm,stripe,host,net,copy"))
     if os.path.isdir(os.path.join(REPO, "gpurun_out")):
         with open(os.path.join(REPO, "gpurun_out", "fuzz_gpu.json"), "w") as f:
             json.dump(res, f)
