@@ -40,6 +40,7 @@ def build(jobs: int | None = None, sanitize: bool | str = False, verbose: bool =
             f"-DCMAKE_CXX_COMPILER={ROCM}/llvm/bin/clang++",
             f"-DCMAKE_PREFIX_PATH={ROCM}",
             "-DCMAKE_BUILD_TYPE=Release",
+            "-DCMAKE_HIP_ARCHITECTURES=gfx950",
         ]
         if sanitize:
             cmd.append("-DOCM_SANITIZE=" + ("thread" if sanitize == "thread" else "ON"))
