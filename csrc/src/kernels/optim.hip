@@ -26,6 +26,12 @@ __device__ __forceinline__ char *state_ptr(const AdamArgs &a, uint64_t x) {
     if (a.n_ext == 1) return a.ext[0] + x;
     const uint64_t u = x >> a.unit_shift;
     const uint64_t mask = (1ull << a.unit_shift) - 1;
+    if (u <= 0xFFFFFFFFull) {
+        // Stripe over 3/5/6/7 peers: 64-bit division is a ~100-instruction
+        // software routine on gfx950, 32-bit a handful (unit counts fit easily).
+        const uint32_t u32 = (uint32_t)u, q = u32 / a.n_ext;
+        return a.ext[u32 - q * a.n_ext] + (((uint64_t)q << a.unit_shift) | (x & mask));
+    }
     return a.ext[u % a.n_ext] + (((u / a.n_ext) << a.unit_shift) | (x & mask));
 }
 
