@@ -186,12 +186,26 @@ void service_store_seq(ServiceReq *req, unsigned long long seq);
 //             every wave drains its stores: neither an acquire after the
 //             doorbell nor a system-scope release (buffer_wbl2) before `done`.
 //             Without WT: plain loads and stores, system acquire and release.
+//   GANGREC   gang requests go to a second host record on a page of their own
+//             (`gang_req`), which the first `direct_wgs` workgroups poll
+//             themselves: no relay through device memory (1.3 us across XCD
+//             L2s) for gangs that fit them; wider gangs are relayed to the
+//             rest as before. Workgroup 0's small-op record is read by
+//             workgroup 0 alone, which reads both records with one load
+//             instruction; direct pollers also watch the box's STOP word, so
+//             they leave with workgroup 0.
+//   WCREQ     the request record(s) in write-combined host memory (uncached on
+//             the CPU side, so GPU polls need no snoop of the CPU's caches; the
+//             host only ever writes them), `done` stays in coherent memory
 //   TRACE     diagnostics: stamp each workgroup's phases into ServiceBox::trace
-constexpr unsigned kServiceProtoWT = 1u, kServiceProtoTrace = 16u;
+constexpr unsigned kServiceProtoWT = 1u, kServiceProtoGangRec = 2u, kServiceProtoWCReq = 4u, kServiceProtoTrace = 16u;
 
-// first_seq >= 1: the first request this instance serves.
-hipError_t service_launch(ServiceReq *req, ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
-                          unsigned long long idle_ticks, unsigned blocks, unsigned proto, hipStream_t stream);
+// first_seq >= 1: the first request this instance serves. gang_req: the
+// GANGREC record (nullptr: gang requests are relayed by workgroup 0).
+// direct_wgs: with gang_req, workgroups 0..direct_wgs-1 poll it themselves.
+hipError_t service_launch(ServiceReq *req, ServiceReq *gang_req, ServiceSlot *slot, ServiceBox *box,
+                          unsigned long long first_seq, unsigned long long idle_ticks, unsigned blocks, unsigned proto,
+                          unsigned direct_wgs, hipStream_t stream);
 
 // Deterministic 32-bit word pattern (word i of a buffer) for data verification.
 hipError_t pattern_fill(void *p, uint64_t words, uint64_t first_word, uint32_t seed, hipStream_t stream);

@@ -634,47 +634,76 @@ __device__ __forceinline__ void service_serve(const unsigned long long *sh, unsi
 // The gang polls that device copy: 32 workgroups polling the host record
 // directly cost every op 3-4 us (profiles/svc_v3_direct_r02.json), and a relay
 // that re-hashed and fenced first cost the gang ~2 us (profiles/svc_trace_r02.json).
-__global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq, ServiceSlot *slot, ServiceBox *box,
+// GANGREC (grq != nullptr): gang requests sit in their own host record, which
+// workgroups 0..direct_wgs-1 poll themselves; workgroup 0 reads both records in
+// one load (lanes 0..15 the small-op record, 16..31 the gang record) and
+// relays only gangs wider than direct_wgs to the others. 16 direct pollers
+// cost small ops nothing measurable; 32 cost them ~1 us
+// (profiles/svc_direct_gang_ab_r02.json).
+__global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq, const ServiceReq *grq,
+                                                           ServiceSlot *slot, ServiceBox *box,
                                                            unsigned long long first_seq,
-                                                           unsigned long long idle_ticks, unsigned proto) {
+                                                           unsigned long long idle_ticks, unsigned proto,
+                                                           unsigned direct_wgs) {
     __shared__ __attribute__((aligned(16))) unsigned long long sh[16];
     const int tid = threadIdx.x;
     const bool lead = blockIdx.x == 0;
-    const unsigned long long *req =
-        lead ? reinterpret_cast<const unsigned long long *>(rq) : static_cast<const unsigned long long *>(box->rec);
+    const bool direct = grq != nullptr && blockIdx.x < direct_wgs;  // polls the host gang record itself
+    const unsigned long long relay_above = grq != nullptr ? direct_wgs : 1;  // gangs wider than this are relayed
+    const unsigned long long *req = reinterpret_cast<const unsigned long long *>(
+        lead ? static_cast<const void *>(rq) : direct ? static_cast<const void *>(grq) : static_cast<const void *>(box->rec));
+    const unsigned long long *greq = reinterpret_cast<const unsigned long long *>(grq);
     unsigned long long last = first_seq - 1;  // requests carry strictly increasing seqs
     unsigned long long idle_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long ticks_sum =
         lead ? __hip_atomic_load(&slot->gpu_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
     for (;;) {
+        int base = 0;  // first lane of the record being served (wave-uniform)
         if (tid < 64) {
             // One load instruction per poll: lanes 0..15 read the whole record
             // (args, gang word, sum, seq); a seq whose hash checks out is whole.
             unsigned long long w = 0, s;
             for (;;) {
                 if (tid < 16)
-                    w = lead ? __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                             : __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    w = (lead || direct) ? __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                         : __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if (direct && lead && tid < 32)
+                    w = __hip_atomic_load(greq + (tid - 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                else if (direct && !lead && tid == 16)
+                    w = __hip_atomic_load(&box->rec[15], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // lead's STOP
+                base = 0;
                 s = readlane64(w, 15);
+                if (direct) {
+                    const unsigned long long s2 = readlane64(w, 31 - 15 * (int)!lead);  // gang seq / box STOP
+                    if (s2 == kServiceStop) {  // the host parked it / workgroup 0 left
+                        s = kServiceStop;
+                        break;
+                    }
+                    if (lead && s2 > last && s2 != 0) {
+                        s = s2;  // the host posts one request at a time: at most one record is new
+                        base = 16;
+                    }
+                }
                 if (s == kServiceStop) break;
                 if (s > last) {
                     unsigned long long h = service_mix(0, s);
 #pragma unroll
-                    for (int i = 0; i <= kServiceReqGang; i++) h = service_mix(h, readlane64(w, i));
-                    if (h == readlane64(w, 14)) break;
+                    for (int i = 0; i <= kServiceReqGang; i++) h = service_mix(h, readlane64(w, base + i));
+                    if (h == readlane64(w, base + 14)) break;
                     continue;  // seq landed before the rest of the record: read it again
                 }
                 if (lead && __builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks) {
                     s = kServiceStop;
                     break;
                 }
-                if (lead)
+                if (lead || direct)
                     __builtin_amdgcn_s_sleep(8);  // ~0.2 us between PCIe polls
                 else
                     __builtin_amdgcn_s_sleep(1);
             }
-            if (lead && s != kServiceStop && (readlane64(w, kServiceReqGang) & 0xFFFFull) > 1 && tid < 16)
-                __hip_atomic_store(&box->rec[tid], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // relay, sc1
+            if (lead && s != kServiceStop && (readlane64(w, base + kServiceReqGang) & 0xFFFFull) > relay_above &&
+                tid >= base && tid < base + 16)
+                __hip_atomic_store(&box->rec[tid - base], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // relay, sc1
             // Data loads are sc1 (ST_WT protocol): they bypass this CU's L1 and are
             // not served from stale L2 copies of host or peer memory, so no acquire
             // fence is needed; the plain protocol keeps the system-scope acquire.
@@ -682,7 +711,8 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-            if (tid <= kServiceReqGang) sh[tid == kServiceReqGang ? 1 : 2 + tid] = w;  // args -> sh[2..], gang -> sh[1]
+            const int r = tid - base;  // this lane's word of the served record
+            if (r >= 0 && r <= kServiceReqGang) sh[r == kServiceReqGang ? 1 : 2 + r] = w;  // args -> sh[2..], gang -> sh[1]
             if (tid == 0) sh[0] = s;
         }
         __syncthreads();
@@ -737,13 +767,15 @@ void service_store_seq(ServiceReq *req, unsigned long long seq) {
     __builtin_ia32_sfence();
 }
 
-hipError_t service_launch(ServiceReq *req, ServiceSlot *slot, ServiceBox *box, unsigned long long first_seq,
-                          unsigned long long idle_ticks, unsigned blocks, unsigned proto, hipStream_t stream) {
-    if (!req || !slot || !box || blocks == 0 || first_seq == 0) return hipErrorInvalidValue;
+hipError_t service_launch(ServiceReq *req, ServiceReq *gang_req, ServiceSlot *slot, ServiceBox *box,
+                          unsigned long long first_seq, unsigned long long idle_ticks, unsigned blocks, unsigned proto,
+                          unsigned direct_wgs, hipStream_t stream) {
+    if (!req || !slot || !box || blocks == 0 || first_seq == 0 || (gang_req && direct_wgs == 0))
+        return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(box, 0, sizeof(ServiceBox), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(service_kernel, dim3(blocks), dim3(kThreads), 0, stream, req, slot, box, first_seq, idle_ticks,
-                       proto);
+    hipLaunchKernelGGL(service_kernel, dim3(blocks), dim3(kThreads), 0, stream, req, gang_req, slot, box, first_seq,
+                       idle_ticks, proto, direct_wgs);
     return hipGetLastError();
 }
 // ---- verification patterns (benchmarks and tests check data without a host round trip) ----

@@ -51,7 +51,17 @@ constexpr uint64_t kServiceMaxDefault = 4ull << 20;
 constexpr uint64_t kServiceMaxHostDefault = 16ull << 20;
 constexpr int kServiceBlocksDefault = 32;
 constexpr int kServiceSoloTilesDefault = 2;
-constexpr unsigned kServiceProtoDefault = kServiceProtoWT;
+// Write-through hand-offs, the records in write-combined memory, and gang
+// requests polled directly by the first 16 workgroups: small ops -0.1/-0.2 us,
+// host-tier 128 KiB-4 MiB and HBM 256 KiB-1 MiB gangs 1-1.5 us faster than the
+// relay (profiles/svc_direct_gang_ab_r02.json, svc_direct_hybrid_r02.json).
+constexpr unsigned kServiceProtoDefault = kServiceProtoWT | kServiceProtoGangRec | kServiceProtoWCReq;
+constexpr int kServiceDirectDefault = 16;
+// Direct gangs (at most kServiceDirectDefault workgroups) for ops up to these
+// sizes; wider relayed gangs above, where 16 workgroups copy too slowly
+// (host-tier 16 MiB get 310-320 vs 302 us; HBM 4 MiB 10.9 vs 9.1 us).
+constexpr uint64_t kServiceDirectMaxHost = 4ull << 20;
+constexpr uint64_t kServiceDirectMaxHbm = 1ull << 20;
 // Kernel-published completion of blocking launches (XferDone) up to this size.
 // Measured on HBM pairs (profiles/launch_flag_r01.json): 9.1-13.4 us against
 // 13.0-14.6 us with the runtime event up to 4 MiB; above that the per-workgroup
@@ -164,6 +174,8 @@ struct State {
     // persistent copy service (small blocking one-sided ops)
     ServiceSlot *svc = nullptr;
     ServiceReq *svc_req = nullptr;   // request record (&svc->req)
+    ServiceReq *svc_greq = nullptr;  // GANGREC: gang requests' record, a page of its own
+    char *svc_rec_pages = nullptr;   // separately allocated record pages (GANGREC / WCREQ), freed at stop
     unsigned long long svc_gang_total = 0;  // gang completions this instance counts to (device counter mirror)
     ServiceBox *svc_box = nullptr;   // device-memory mailbox of the gang
     hipStream_t svc_stream = nullptr;
@@ -171,6 +183,9 @@ struct State {
     unsigned svc_solo_tiles = kServiceSoloTilesDefault;  // requests of <= this many tiles stay on workgroup 0
     unsigned svc_solo_tiles_host_get = 1;  // ... for gets from the host tier (OCM_SERVICE_SOLO_TILES_HOST_GET)
     unsigned svc_proto = kServiceProtoDefault;           // hand-off protocol bits (OCM_SERVICE_PROTO)
+    unsigned svc_direct = kServiceDirectDefault;          // GANGREC direct pollers (OCM_SERVICE_DIRECT)
+    uint64_t svc_direct_max_host = kServiceDirectMaxHost;  // OCM_SERVICE_DIRECT_MAX_HOST
+    uint64_t svc_direct_max_hbm = kServiceDirectMaxHbm;    // OCM_SERVICE_DIRECT_MAX_HBM
     bool svc_running = false;
     bool svc_park_kernel = false;  // park the service during kernel transfers above svc_max (OCM_SERVICE_PARK_KERNEL)
     unsigned long long svc_seq = 0;
@@ -297,7 +312,7 @@ int sync_stream();
 int service_start(unsigned long long first_seq);
 void service_park();
 void service_stop();
-int service_xfer(XferArgs x, unsigned solo_tiles);
+int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm);
 // `done` (optional, async launches on a lane): receives the kernel-published
 // completion flag of the launch, or flag == nullptr when the op has none.
 int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async,

@@ -112,6 +112,9 @@ int ocm_init(void) {
     s.svc_solo_tiles = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES", kServiceSoloTilesDefault));
     s.svc_solo_tiles_host_get = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES_HOST_GET", 1));
     s.svc_proto = (unsigned)env_int("OCM_SERVICE_PROTO", (int)kServiceProtoDefault) & 31u;
+    s.svc_direct = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_DIRECT", kServiceDirectDefault), 1024));
+    if (const char *v = std::getenv("OCM_SERVICE_DIRECT_MAX_HOST"); v && *v) s.svc_direct_max_host = std::strtoull(v, nullptr, 0);
+    if (const char *v = std::getenv("OCM_SERVICE_DIRECT_MAX_HBM"); v && *v) s.svc_direct_max_hbm = std::strtoull(v, nullptr, 0);
     s.launch_flags = env_int("OCM_LAUNCH_FLAG", 1) != 0;
     s.svc_park_kernel = env_int("OCM_SERVICE_PARK_KERNEL", 0) != 0;
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");

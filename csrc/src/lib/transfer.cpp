@@ -155,12 +155,28 @@ int service_start(unsigned long long first_seq) {
             s.svc_max = 0;
             OCM_FAIL(-1, "copy service: no stream");
         }
+        const bool gangrec = (s.svc_proto & kServiceProtoGangRec) && s.svc_blocks > 1;
+        const bool wc = (s.svc_proto & kServiceProtoWCReq) != 0;
+        if (gangrec || wc) {
+            // page 0: the small-op record when write-combined; page 1: the gang record
+            const unsigned flags = (wc ? hipHostMallocWriteCombined : hipHostMallocCoherent) | hipHostMallocMapped;
+            if (hipHostMalloc(reinterpret_cast<void **>(&s.svc_rec_pages), 8192, flags) != hipSuccess) {
+                (void)hipGetLastError();
+                s.svc_rec_pages = nullptr;  // one coherent record, relay protocol
+            } else {
+                for (int i = 0; i < 8192 / 8; i++) __atomic_store_n(reinterpret_cast<unsigned long long *>(s.svc_rec_pages) + i, 0ull, __ATOMIC_RELAXED);
+                __builtin_ia32_sfence();
+                if (wc) s.svc_req = reinterpret_cast<ServiceReq *>(s.svc_rec_pages);
+                if (gangrec) s.svc_greq = reinterpret_cast<ServiceReq *>(s.svc_rec_pages + 4096);
+            }
+        }
     }
     __atomic_store_n(&s.svc->exited, 0ull, __ATOMIC_RELEASE);
     service_store_seq(s.svc_req, 0ull);  // clear a STOP left by a parked instance
+    if (s.svc_greq) service_store_seq(s.svc_greq, 0ull);
     s.svc_gang_total = 0;  // the launch zeroes the device counter
-    if (service_launch(s.svc_req, s.svc, s.svc_box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_proto,
-                       s.svc_stream) != hipSuccess) {
+    if (service_launch(s.svc_req, s.svc_greq, s.svc, s.svc_box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_proto,
+                       std::min(s.svc_direct, s.svc_blocks), s.svc_stream) != hipSuccess) {
         (void)hipGetLastError();
         s.svc_max = 0;
         OCM_FAIL(-1, "copy service launch failed");
@@ -176,6 +192,7 @@ void service_park() {
     if (!s.svc || !s.svc_running) return;
     DeviceGuard g(s.device);
     service_store_seq(s.svc_req, kServiceStop);
+    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
     (void)hipStreamSynchronize(s.svc_stream);
     s.svc_running = false;
 }
@@ -186,11 +203,15 @@ void service_stop() {
     DeviceGuard g(s.device);
     if (s.svc_running) {
         service_store_seq(s.svc_req, kServiceStop);
+        if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
         (void)hipStreamSynchronize(s.svc_stream);
         s.svc_running = false;
     }
     (void)hipStreamDestroy(s.svc_stream);
     s.svc_req = nullptr;
+    if (s.svc_rec_pages) (void)hipHostFree(s.svc_rec_pages);
+    s.svc_rec_pages = nullptr;
+    s.svc_greq = nullptr;
     (void)hipHostFree(s.svc);
     if (s.svc_box) (void)hipFree(s.svc_box);
     s.svc = nullptr;
@@ -199,13 +220,16 @@ void service_stop() {
 }
 
 // Run one normalized transfer through the resident kernel and wait for it.
-int service_xfer(XferArgs x, unsigned solo_tiles) {
+int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm) {
     State &s = S();
     if (xfer_normalize(x) != hipSuccess) OCM_FAIL(-1, "invalid transfer");
     const unsigned long long seq = ++s.svc_seq;
     if (!s.svc_running && service_start(seq) != 0) return -1;
-    // The host sizes the gang and the completion count every workgroup agrees on.
-    const unsigned long long active = service_gang_size(x, s.svc_blocks, solo_tiles);
+    // The host sizes the gang and the completion count every workgroup agrees on:
+    // up to the direct pollers (no relay) for ops they copy fast enough.
+    const bool direct = s.svc_greq && x.len <= (hbm ? s.svc_direct_max_hbm : s.svc_direct_max_host);
+    const unsigned long long active =
+        service_gang_size(x, direct ? std::min(s.svc_direct, s.svc_blocks) : s.svc_blocks, solo_tiles);
     auto gang_word = [&]() {
         unsigned long long target = 0;
         if (active > 1) {
@@ -215,8 +239,10 @@ int service_xfer(XferArgs x, unsigned solo_tiles) {
         return active | (target << 16);
     };
     unsigned long long gang = gang_word();
+    // GANGREC: gang requests go to the record the whole gang polls.
+    ServiceReq *rq = (active > 1 && s.svc_greq) ? s.svc_greq : s.svc_req;
     const uint64_t t0 = now_ns();
-    service_post(s.svc_req, x, gang, seq);
+    service_post(rq, x, gang, seq);
     const uint64_t t_posted = now_ns();
     for (unsigned spins = 1;; spins++) {
         if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) {
@@ -236,7 +262,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles) {
                 if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
                 if (service_start(seq) != 0) return -1;
                 gang = gang_word();              // counted afresh by the new instance
-                service_post(s.svc_req, x, gang, seq);  // start cleared the doorbell: re-post
+                service_post(rq, x, gang, seq);  // start cleared the doorbell: re-post
             }
             if (now_ns() - t0 > 10ull * 1000000000ull) OCM_FAIL(-1, "copy service did not complete a transfer in 10 s");
         }
@@ -328,7 +354,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         // HBM owners keep small requests on workgroup 0 (profiles/svc_v4_r02.json).
         const unsigned solo = (!put && !a->any_gpu) ? std::min(s.svc_solo_tiles, s.svc_solo_tiles_host_get)
                                                     : s.svc_solo_tiles;
-        if (service_xfer(x, solo) == 0) return 0;
+        if (service_xfer(x, solo, a->any_gpu) == 0) return 0;
         OCM_WARN("copy service failed (%s); falling back to launches", last_error());
         s.svc_max = 0;
     }

@@ -35,6 +35,13 @@ CONFIGS["trace"] = {"OCM_SERVICE_PROTO": "17"}
 for n in (0, 1, 2, 4, 8):
     CONFIGS[f"solo{n}"] = {"OCM_SERVICE_SOLO_TILES": str(n), "OCM_SERVICE_SOLO_TILES_HOST_GET": str(n)}
 # host-tier gets only: the round-2 default (1) against the earlier shared threshold (2)
+CONFIGS["gangrec"] = {"OCM_SERVICE_PROTO": "3"}  # write-through + gang requests in their own host record
+CONFIGS["wcreq"] = {"OCM_SERVICE_PROTO": "5"}  # write-through + the record in write-combined host memory
+CONFIGS["wcgang"] = {"OCM_SERVICE_PROTO": "7"}  # both
+CONFIGS["relay"] = {"OCM_SERVICE_PROTO": "1"}  # round-2 v4 default: one coherent record, WG0 relays every gang
+for g in (4, 8, 16):
+    CONFIGS[f"wcgang_g{g}"] = {"OCM_SERVICE_PROTO": "7", "OCM_SERVICE_BLOCKS": str(g)}
+    CONFIGS[f"wcreq_g{g}"] = {"OCM_SERVICE_PROTO": "5", "OCM_SERVICE_BLOCKS": str(g)}
 CONFIGS["hostget2"] = {"OCM_SERVICE_SOLO_TILES_HOST_GET": "2"}
 
 # the service/SDMA crossover: the service takes blocking ops up to 16 MiB
