@@ -186,6 +186,14 @@ struct State {
     unsigned svc_direct = kServiceDirectDefault;          // GANGREC direct pollers (OCM_SERVICE_DIRECT)
     uint64_t svc_direct_max_host = kServiceDirectMaxHost;  // OCM_SERVICE_DIRECT_MAX_HOST
     uint64_t svc_direct_max_hbm = kServiceDirectMaxHbm;    // OCM_SERVICE_DIRECT_MAX_HBM
+    // Smaller tiles for host-tier ops of svc_host_tile_min..max bytes (0: the 32 KiB
+    // default), so a direct gang spreads them over more CUs' miss queues. Gets use
+    // 16 KiB tiles there: 64/128/256 KiB 6.9/7.75/9.86 vs 7.6/8.3/10.4 us; 8 and 4 KiB
+    // tiles lose, and so do puts and a 32 KiB get as a gang of two
+    // (profiles/svc_host_tile_ab_r02.json).
+    unsigned svc_host_tile_shift_get = 14, svc_host_tile_shift_put = 0;  // OCM_SERVICE_HOST_TILE_SHIFT_GET/_PUT
+    uint64_t svc_host_tile_min = 64ull << 10;                             // OCM_SERVICE_HOST_TILE_MIN
+    uint64_t svc_host_tile_max = 256ull << 10;                            // OCM_SERVICE_HOST_TILE_MAX
     bool svc_running = false;
     bool svc_park_kernel = false;  // park the service during kernel transfers above svc_max (OCM_SERVICE_PARK_KERNEL)
     unsigned long long svc_seq = 0;

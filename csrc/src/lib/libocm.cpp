@@ -115,6 +115,10 @@ int ocm_init(void) {
     s.svc_direct = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_DIRECT", kServiceDirectDefault), 1024));
     if (const char *v = std::getenv("OCM_SERVICE_DIRECT_MAX_HOST"); v && *v) s.svc_direct_max_host = std::strtoull(v, nullptr, 0);
     if (const char *v = std::getenv("OCM_SERVICE_DIRECT_MAX_HBM"); v && *v) s.svc_direct_max_hbm = std::strtoull(v, nullptr, 0);
+    s.svc_host_tile_shift_get = (unsigned)std::max(0, env_int("OCM_SERVICE_HOST_TILE_SHIFT_GET", (int)s.svc_host_tile_shift_get));
+    s.svc_host_tile_shift_put = (unsigned)std::max(0, env_int("OCM_SERVICE_HOST_TILE_SHIFT_PUT", (int)s.svc_host_tile_shift_put));
+    if (const char *v = std::getenv("OCM_SERVICE_HOST_TILE_MAX"); v && *v) s.svc_host_tile_max = std::strtoull(v, nullptr, 0);
+    if (const char *v = std::getenv("OCM_SERVICE_HOST_TILE_MIN"); v && *v) s.svc_host_tile_min = std::strtoull(v, nullptr, 0);
     s.launch_flags = env_int("OCM_LAUNCH_FLAG", 1) != 0;
     s.svc_park_kernel = env_int("OCM_SERVICE_PARK_KERNEL", 0) != 0;
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");

@@ -223,6 +223,10 @@ void service_stop() {
 int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm) {
     State &s = S();
     if (xfer_normalize(x) != hipSuccess) OCM_FAIL(-1, "invalid transfer");
+    if (!hbm && x.len >= s.svc_host_tile_min && x.len <= s.svc_host_tile_max) {
+        const unsigned sh = x.put ? s.svc_host_tile_shift_put : s.svc_host_tile_shift_get;
+        if (sh >= 12 && sh < x.tile_shift) x.tile_shift = sh;
+    }
     const unsigned long long seq = ++s.svc_seq;
     if (!s.svc_running && service_start(seq) != 0) return -1;
     // The host sizes the gang and the completion count every workgroup agrees on:

@@ -38,6 +38,9 @@ for n in (0, 1, 2, 4, 8):
 CONFIGS["gangrec"] = {"OCM_SERVICE_PROTO": "3"}  # write-through + gang requests in their own host record
 CONFIGS["wcreq"] = {"OCM_SERVICE_PROTO": "5"}  # write-through + the record in write-combined host memory
 CONFIGS["wcgang"] = {"OCM_SERVICE_PROTO": "7"}  # both
+for sh in (12, 13, 14):
+    CONFIGS[f"htile{sh}"] = {"OCM_SERVICE_HOST_TILE_SHIFT_GET": str(sh)}
+    CONFIGS[f"htile{sh}p"] = {"OCM_SERVICE_HOST_TILE_SHIFT_GET": str(sh), "OCM_SERVICE_HOST_TILE_SHIFT_PUT": str(sh)}
 CONFIGS["relay"] = {"OCM_SERVICE_PROTO": "1"}  # round-2 v4 default: one coherent record, WG0 relays every gang
 for g in (4, 8, 16):
     CONFIGS[f"wcgang_g{g}"] = {"OCM_SERVICE_PROTO": "7", "OCM_SERVICE_BLOCKS": str(g)}
