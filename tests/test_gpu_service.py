@@ -79,3 +79,28 @@ def test_service_restarts_after_idle_exit(mesh_factory):
         ops = api.service_stats()["ops"]
         assert ops >= 24
         a.free()
+
+
+def test_service_direct_and_relayed_gangs_interleave(mesh_factory):
+    # Gangs of up to 16 workgroups poll their own host record; wider ones (HBM
+    # ops above 1 MiB, host-tier ops above 4 MiB) are relayed by workgroup 0.
+    # Interleave solo ops, direct gangs (16 KiB host-get tiles included) and
+    # relayed gangs on both tiers, with idle exits in between.
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 8 << 20
+        hbm = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_LOOPBACK)
+        host = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_HOST_TIER)
+        plan = [(host, 8192), (host, 96 << 10), (hbm, 2 << 20), (host, 256 << 10), (hbm, 1 << 20),
+                (host, 3 << 20), (hbm, 4096), (host, 6 << 20), (hbm, (2 << 20) + 4096), (host, 64 << 10)]
+        for i in range(3 * len(plan)):
+            a, size = plan[i % len(plan)]
+            a.fill(seed=300 + i, nbytes=size)
+            a.put(0, 0, size)
+            a.fill(seed=0, nbytes=size)
+            a.get(0, 0, size)
+            assert a.check(seed=300 + i, nbytes=size) == 0, f"op pair {i} ({size} B)"
+            if i % 4 == 3:
+                time.sleep(0.004)  # past the 2 ms idle exit
+        hbm.free()
+        host.free()
