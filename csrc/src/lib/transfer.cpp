@@ -163,6 +163,8 @@ int service_start(unsigned long long first_seq) {
             if (hipHostMalloc(reinterpret_cast<void **>(&s.svc_rec_pages), 8192, flags) != hipSuccess) {
                 (void)hipGetLastError();
                 s.svc_rec_pages = nullptr;  // one coherent record, relay protocol
+                OCM_WARN("copy service: no %s record pages; using one coherent record and the relay protocol",
+                         wc ? "write-combined" : "gang");
             } else {
                 for (int i = 0; i < 8192 / 8; i++) __atomic_store_n(reinterpret_cast<unsigned long long *>(s.svc_rec_pages) + i, 0ull, __ATOMIC_RELAXED);
                 __builtin_ia32_sfence();
