@@ -41,6 +41,8 @@ CONFIGS["wcgang"] = {"OCM_SERVICE_PROTO": "7"}  # both
 for sh in (12, 13, 14):
     CONFIGS[f"htile{sh}"] = {"OCM_SERVICE_HOST_TILE_SHIFT_GET": str(sh)}
     CONFIGS[f"htile{sh}p"] = {"OCM_SERVICE_HOST_TILE_SHIFT_GET": str(sh), "OCM_SERVICE_HOST_TILE_SHIFT_PUT": str(sh)}
+for d in (8, 12, 24, 32):
+    CONFIGS[f"direct{d}"] = {"OCM_SERVICE_DIRECT": str(d)}
 CONFIGS["relay"] = {"OCM_SERVICE_PROTO": "1"}  # round-2 v4 default: one coherent record, WG0 relays every gang
 for g in (4, 8, 16):
     CONFIGS[f"wcgang_g{g}"] = {"OCM_SERVICE_PROTO": "7", "OCM_SERVICE_BLOCKS": str(g)}
