@@ -93,6 +93,7 @@ class Mesh:
         self.watch = watch  # daemons exit when this process does (no orphans after a crash)
         self.workdir = workdir or tempfile.mkdtemp(prefix=f"ocm_{self.ns}_")
         self.ports = list(ports) if ports is not None else free_ports(n)
+        self._own_ports = ports is None  # picked here: free to pick again if one was taken meanwhile
         self.data_ports = list(data_ports) if data_ports is not None else None
         self.ranks = list(ranks) if ranks is not None else list(range(n))  # which ranks THIS process launches
         self.nodefile = os.path.join(self.workdir, "nodefile")
@@ -130,24 +131,42 @@ class Mesh:
         return Daemon(r, proc, ready, log)
 
     def _wait_ready(self, daemons, timeout: float) -> None:
+        # Every daemon is checked on every pass: one that died (e.g. its port was
+        # taken between free_ports and its bind) fails the start at once instead
+        # of leaving the others waiting for it until the deadline.
         deadline = time.time() + timeout
-        for d in daemons:
-            while not os.path.exists(d.ready_file):
-                if not d.alive():
+        pending = list(daemons)
+        while pending:
+            for d in daemons:
+                if not os.path.exists(d.ready_file) and not d.alive():
                     raise RuntimeError(f"ocmd rank {d.rank} exited ({d.proc.returncode}):\n{d.log()}")
-                if time.time() > deadline:
-                    logs = "".join(f"--- ocmd rank {x.rank} ---\n{x.log()[-2000:]}\n" for x in self.daemons)
-                    self.stop()
-                    raise TimeoutError(f"ocmd rank {d.rank} not ready after {timeout}s:\n{logs}")
-                time.sleep(0.02)
+            pending = [d for d in pending if not os.path.exists(d.ready_file)]
+            if not pending:
+                return
+            if time.time() > deadline:
+                logs = "".join(f"--- ocmd rank {x.rank} ---\n{x.log()[-2000:]}\n" for x in self.daemons)
+                self.stop()
+                raise TimeoutError(f"ocmd rank {pending[0].rank} not ready after {timeout}s:\n{logs}")
+            time.sleep(0.02)
 
     def start(self, timeout: float = 60.0) -> "Mesh":
-        write_nodefile(self.nodefile, self.ports, self.gpus, data_ports=self.data_ports)
-        for r in self.ranks:
-            log = os.path.join(self.workdir, f"ocmd.{r}.log")
-            open(log, "w").close()
-            self.daemons.append(self._spawn(r))
-        self._wait_ready(self.daemons, timeout)
+        for attempt in range(3):
+            write_nodefile(self.nodefile, self.ports, self.gpus, data_ports=self.data_ports)
+            for r in self.ranks:
+                log = os.path.join(self.workdir, f"ocmd.{r}.log")
+                open(log, "w").close()
+                self.daemons.append(self._spawn(r))
+            try:
+                self._wait_ready(self.daemons, timeout)
+                return self
+            except RuntimeError as e:
+                # Ports from free_ports are only probably free: another process
+                # can bind one before the daemon does. Pick new ones and retry.
+                if not (self._own_ports and "Address already in use" in str(e) and attempt < 2):
+                    raise
+                self.stop()
+                self.daemons = []
+                self.ports = free_ports(self.n)
         return self
 
     def restart(self, rank: int, timeout: float = 60.0) -> None:

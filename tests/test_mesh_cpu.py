@@ -217,3 +217,42 @@ def test_host_tier_slab_passed_by_fd_from_non_dumpable_owner(mesh_factory):
         assert after["n_slab_path"] == before["n_slab_path"]
         for a in allocs:
             a.free()
+
+
+def test_mesh_start_retries_a_port_taken_after_it_was_picked(native, monkeypatch):
+    # free_ports only finds ports that are free *now*; another process can bind
+    # one before the daemon does. The mesh must notice the dead daemon at once
+    # and start again on fresh ports instead of timing out.
+    import socket
+
+    from oncilla_amd.parallel import mesh as meshmod
+
+    squatter = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    squatter.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    squatter.bind(("127.0.0.1", 0))
+    squatter.listen(1)
+    taken = squatter.getsockname()[1]
+    real = meshmod.free_ports
+    calls = []
+
+    def first_call_hands_out_a_taken_port(n):
+        calls.append(n)
+        ports = real(n)
+        if len(calls) == 1:
+            ports[-1] = taken
+        return ports
+
+    monkeypatch.setattr(meshmod, "free_ports", first_call_hands_out_a_taken_port)
+    try:
+        t0 = time.time()
+        m = meshmod.Mesh(2).start(timeout=60)
+        try:
+            assert len(calls) == 2 and taken not in m.ports
+            assert time.time() - t0 < 30
+            with api.Client(daemon_rank=0, ns=m.ns) as c:
+                a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=4096)
+                a.free()
+        finally:
+            m.stop()
+    finally:
+        squatter.close()
