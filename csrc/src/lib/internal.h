@@ -49,7 +49,16 @@ constexpr uint64_t kServiceMaxDefault = 4ull << 20;
 // engines up to 16 MiB (8 MiB 152/155 us against 164/164, 16 MiB 300/303 against
 // 312/312 put/get; profiles/svc_max_ab_r02.json). OCM_SERVICE_MAX_HOST.
 constexpr uint64_t kServiceMaxHostDefault = 16ull << 20;
-constexpr int kServiceBlocksDefault = 32;
+// 128 workgroups: with the direct gang record only 16 of them poll host memory,
+// so the width costs small ops nothing, and HBM gangs of 4-64 MiB run 1.5-7 us
+// faster than 32 (or a launch); host-tier gangs stay at 32, since wider ones
+// lose at 8-16 MiB (188 vs 153 us; profiles/svc_blocks_r02.json).
+constexpr int kServiceBlocksDefault = 128;
+constexpr unsigned kServiceGangHostDefault = 32;
+// Pairs wholly in this GPU's HBM keep blocking ops up to 64 MiB on the service
+// (64 MiB: 23.5-24 vs 30.5 us for launch + completion); peer HBM over xGMI
+// keeps kServiceMaxDefault, above which the autotuned launches take over.
+constexpr uint64_t kServiceMaxLocalDefault = 64ull << 20;
 constexpr int kServiceSoloTilesDefault = 2;
 // Write-through hand-offs, the records in write-combined memory, and gang
 // requests polled directly by the first 16 workgroups: small ops -0.1/-0.2 us,
@@ -103,6 +112,7 @@ struct lib_alloc {
     bool any_gpu = false;
     bool all_dev_ok = false;  // every extent reachable by a kernel on this GPU
     bool any_net = false;     // some extent lives on another node
+    bool same_gpu = false;    // every extent in this process's own GPU's HBM (another daemon on it, via IPC)
     bool async_pending = false;
     bool pooled = false;      // local half from the stream-ordered pool
     int lane = -1;            // async ops: index into State::lanes (per-allocation ordering)
@@ -201,7 +211,13 @@ struct State {
     uint64_t svc_max = kServiceMaxDefault;           // 0: the service is off (or failed)
     uint64_t svc_max_host = kServiceMaxHostDefault;  // the same bound for host-tier-only pairs
     // Largest blocking op the service takes for a pair with (`hbm`) or without HBM extents.
-    uint64_t svc_limit(bool hbm) const { return svc_max == 0 ? 0 : (hbm ? svc_max : svc_max_host); }
+    uint64_t svc_max_local = kServiceMaxLocalDefault;  // ... for pairs wholly in this GPU's HBM (OCM_SERVICE_MAX_LOCAL)
+    unsigned svc_gang_host = kServiceGangHostDefault;  // widest gang for host-tier ops (OCM_SERVICE_GANG_HOST)
+    uint64_t svc_limit(const lib_alloc *a) const {
+        if (svc_max == 0) return 0;
+        if (!a->any_gpu) return svc_max_host;
+        return a->same_gpu ? std::max(svc_max, svc_max_local) : svc_max;
+    }
     unsigned long long svc_idle_ticks = 200000ull;  // 2 ms at 100 MHz: live only during bursts of small ops
     // network tier
     std::map<std::string, NetConn> net_conns;  // "ip:port#stream" -> connection

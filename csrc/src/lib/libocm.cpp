@@ -112,6 +112,8 @@ int ocm_init(void) {
     s.svc_solo_tiles = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES", kServiceSoloTilesDefault));
     s.svc_solo_tiles_host_get = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES_HOST_GET", 1));
     s.svc_proto = (unsigned)env_int("OCM_SERVICE_PROTO", (int)kServiceProtoDefault) & 31u;
+    if (const char *v = std::getenv("OCM_SERVICE_MAX_LOCAL"); v && *v) s.svc_max_local = std::strtoull(v, nullptr, 0);
+    s.svc_gang_host = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_GANG_HOST", (int)s.svc_gang_host), 1024));
     s.svc_direct = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_DIRECT", kServiceDirectDefault), 1024));
     if (const char *v = std::getenv("OCM_SERVICE_DIRECT_MAX_HOST"); v && *v) s.svc_direct_max_host = std::strtoull(v, nullptr, 0);
     if (const char *v = std::getenv("OCM_SERVICE_DIRECT_MAX_HBM"); v && *v) s.svc_direct_max_hbm = std::strtoull(v, nullptr, 0);
@@ -276,6 +278,8 @@ static ocm_alloc_t alloc_impl(ocm_alloc_param_t p, const struct ocm_alloc_ex_par
                 if (e.net) a->all_gpu = false;
             }
             a->any_gpu = a->any_gpu && !a->any_net;
+            a->same_gpu = a->all_gpu && s.device >= 0;
+            for (auto &e : a->ext) a->same_gpu &= e.r.owner_gpu == s.device;
             Loc want = kind == OCM_REMOTE_GPU ? LOC_DEVICE : LOC_PINNED;
             ok = alloc_local_half(a, p->local_alloc_bytes, want) == 0;
         }
@@ -428,7 +432,7 @@ static int onesided_impl(ocm_alloc_t a, ocm_param_t p, bool async) {
         // Large blocking ops: launch on the allocation's lane under the lock, wait
         // outside it, so other threads' ops proceed meanwhile. Small ones keep the
         // copy service (no launch) and the network tier its own blocking path.
-        const bool service = a->loc == LOC_DEVICE && a->all_dev_ok && p->bytes <= s.svc_limit(a->any_gpu);
+        const bool service = a->loc == LOC_DEVICE && a->all_dev_ok && p->bytes <= s.svc_limit(a);
         if (async || s.device < 0 || service || a->any_net)
             return xfer(a, put, lin, a->loc, p->dest_offset, p->bytes, async);
         if (xfer(a, put, lin, a->loc, p->dest_offset, p->bytes, true, &wait_done_flag) != 0) return -1;

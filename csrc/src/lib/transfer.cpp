@@ -234,8 +234,9 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm) {
     // The host sizes the gang and the completion count every workgroup agrees on:
     // up to the direct pollers (no relay) for ops they copy fast enough.
     const bool direct = s.svc_greq && x.len <= (hbm ? s.svc_direct_max_hbm : s.svc_direct_max_host);
-    const unsigned long long active =
-        service_gang_size(x, direct ? std::min(s.svc_direct, s.svc_blocks) : s.svc_blocks, solo_tiles);
+    const unsigned width = direct ? std::min(s.svc_direct, s.svc_blocks)
+                                  : (hbm ? s.svc_blocks : std::min(s.svc_gang_host, s.svc_blocks));
+    const unsigned long long active = service_gang_size(x, width, solo_tiles);
     auto gang_word = [&]() {
         unsigned long long target = 0;
         if (active > 1) {
@@ -343,7 +344,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         lin_dev && !dma_pick && (a->any_gpu || s.host_engine_kernel || len <= s.host_kernel_max);
     hipError_t err = hipSuccess;
     // Small blocking ops go to the resident copy service (no launch, no stream sync).
-    if (lin_dev && a->all_dev_ok && !async && len <= s.svc_limit(a->any_gpu) && !dma_pick) {
+    if (lin_dev && a->all_dev_ok && !async && len <= s.svc_limit(a) && !dma_pick) {
         XferArgs x;
         std::memset(&x, 0, sizeof(x));
         x.lin = lin;
@@ -370,7 +371,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     hipStream_t st = async ? lane_stream(a) : s.stream;
     if (honor_dep(a, st, false) != 0) return -1;
     if (use_kernel) {
-        if (s.svc_park_kernel && len > s.svc_limit(a->any_gpu)) service_park();  // A/B: no resident poller during the copy
+        if (s.svc_park_kernel && len > s.svc_limit(a)) service_park();  // A/B: no resident poller during the copy
         XferArgs x;
         std::memset(&x, 0, sizeof(x));
         x.lin = lin;

@@ -43,6 +43,11 @@ for sh in (12, 13, 14):
     CONFIGS[f"htile{sh}p"] = {"OCM_SERVICE_HOST_TILE_SHIFT_GET": str(sh), "OCM_SERVICE_HOST_TILE_SHIFT_PUT": str(sh)}
 for d in (8, 12, 24, 32):
     CONFIGS[f"direct{d}"] = {"OCM_SERVICE_DIRECT": str(d)}
+for g in (64, 128, 256):
+    CONFIGS[f"blocks{g}"] = {"OCM_SERVICE_BLOCKS": str(g)}  # service bounds left at their defaults
+    CONFIGS[f"blocks{g}_max64"] = {"OCM_SERVICE_BLOCKS": str(g), "OCM_SERVICE_MAX": str(64 << 20),
+                                   "OCM_SERVICE_MAX_HOST": str(16 << 20)}
+CONFIGS["prev32"] = {"OCM_SERVICE_BLOCKS": "32", "OCM_SERVICE_MAX_LOCAL": str(4 << 20)}  # before the 128-wide gang
 CONFIGS["relay"] = {"OCM_SERVICE_PROTO": "1"}  # round-2 v4 default: one coherent record, WG0 relays every gang
 for g in (4, 8, 16):
     CONFIGS[f"wcgang_g{g}"] = {"OCM_SERVICE_PROTO": "7", "OCM_SERVICE_BLOCKS": str(g)}
