@@ -491,6 +491,9 @@ def main() -> int:
 
         def sync():
             if use_gpu:
+                # the copy service is a persistent kernel: park it, or a device-wide
+                # synchronize waits for its 2 ms idle exit (inside the timed region)
+                api.quiesce()
                 torch.cuda.synchronize(local_rank)
 
         # ---- timed region: barrier + sync on both sides; the phase's all-gather is the closing barrier ----

@@ -123,6 +123,7 @@ int ocm_init(void) {
     if (const char *v = std::getenv("OCM_SERVICE_HOST_TILE_MIN"); v && *v) s.svc_host_tile_min = std::strtoull(v, nullptr, 0);
     s.launch_flags = env_int("OCM_LAUNCH_FLAG", 1) != 0;
     s.svc_park_kernel = env_int("OCM_SERVICE_PARK_KERNEL", 0) != 0;
+    s.svc_idle_ticks = 100ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_IDLE_US", 2000));  // 100 MHz clock
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");
     s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
     s.tuning = xfer_tuning_from_env();
@@ -777,6 +778,16 @@ static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64
     const hipError_t e = adam_remote_launch(x, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) OCM_FAIL(-1, "ocm_x_adam launch: %s", hipGetErrorString(e));
     return 0;
+}
+
+// Park the resident copy service now. A device-wide synchronize
+// (hipDeviceSynchronize, torch.cuda.synchronize) waits for every stream,
+// including the service's persistent kernel, which otherwise leaves only after
+// OCM_SERVICE_IDLE_US (2 ms) without work; the next small op relaunches it.
+void ocm_x_quiesce(void) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    service_park();
 }
 
 // Copy-service diagnostics: {ops, ns posting requests, ns waiting for done,

@@ -175,6 +175,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
             "ocm_x_service_stats": (None, [ctypes.POINTER(u64)]),
+            "ocm_x_quiesce": (None, []),
             "ocm_x_service_trace": (i32, [ctypes.POINTER(u64), i32]),
             "ocm_x_adam": (i32, [vp, vp, vp, u64, u64, u64, ctypes.POINTER(ctypes.c_float), vp]),
             "ocm_x_adam_multi": (i32, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(u64),
@@ -315,6 +316,15 @@ def counters() -> dict:
     out = (ctypes.c_uint64 * len(COUNTER_KEYS))()
     load().ocm_x_counters(out)
     return dict(zip(COUNTER_KEYS, [int(v) for v in out]))
+
+
+def quiesce() -> None:
+    """Park this process's resident copy service, so that a device-wide
+    synchronize (torch.cuda.synchronize) does not wait for the service's idle
+    exit (OCM_SERVICE_IDLE_US, 2 ms by default). Call it before such a sync when
+    the last library op was a small blocking one; the next op relaunches the
+    service. No-op without a GPU or before any op."""
+    load().ocm_x_quiesce()
 
 
 def service_stats() -> dict:

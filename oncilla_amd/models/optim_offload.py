@@ -220,6 +220,7 @@ class OffloadedAdam:
         if self.mode == "fused":
             import torch
 
+            api.quiesce()  # a resident copy service would hold the device-wide sync for its idle exit
             torch.cuda.synchronize(self.params[0].device)
         for a in self.allocs:
             a.wait()

@@ -104,3 +104,27 @@ def test_service_direct_and_relayed_gangs_interleave(mesh_factory):
                 time.sleep(0.004)  # past the 2 ms idle exit
         hbm.free()
         host.free()
+
+
+def test_quiesce_lets_a_device_sync_return_at_once(mesh_factory):
+    # The service is a persistent kernel: torch.cuda.synchronize() waits for it.
+    # api.quiesce() parks it, so the sync returns without waiting for the idle
+    # exit; the next op relaunches the service and still moves the right bytes.
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 64 << 10
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_LOOPBACK)
+        best = 1.0
+        for i in range(5):
+            a.fill(seed=70 + i, nbytes=n)
+            torch.cuda.synchronize()
+            a.put(0, 0, n)  # small blocking op: the service stays resident after it
+            t0 = time.perf_counter()
+            api.quiesce()
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+            a.fill(seed=0, nbytes=n)
+            a.get(0, 0, n)
+            assert a.check(seed=70 + i, nbytes=n) == 0, f"round {i}"
+        assert best < 1e-3, f"quiesce + device sync took {best * 1e3:.2f} ms (idle exit is 2 ms)"
+        a.free()
