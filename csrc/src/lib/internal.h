@@ -188,6 +188,7 @@ struct State {
     char *svc_rec_pages = nullptr;   // separately allocated record pages (GANGREC / WCREQ), freed at stop
     unsigned long long svc_gang_total = 0;  // gang completions this instance counts to (device counter mirror)
     ServiceBox *svc_box = nullptr;   // device-memory mailbox of the gang
+    unsigned long long *pattern_bad = nullptr;  // device counter of ocm_x_pattern checks
     hipStream_t svc_stream = nullptr;
     unsigned svc_blocks = kServiceBlocksDefault;          // gang size (OCM_SERVICE_BLOCKS)
     unsigned svc_solo_tiles = kServiceSoloTilesDefault;  // requests of <= this many tiles stay on workgroup 0

@@ -172,6 +172,11 @@ int ocm_tini(void) {
         s.lane_flag_seq.clear();
     }
     release_dev_cache();
+    if (s.pattern_bad) {
+        DeviceGuard g(s.device);
+        (void)hipFree(s.pattern_bad);
+        s.pattern_bad = nullptr;
+    }
     if (s.stream) {
         DeviceGuard g(s.device);
         (void)hipStreamSynchronize(s.stream);
@@ -1016,13 +1021,17 @@ long long ocm_x_pattern(void *p, uint64_t words, uint64_t first, uint32_t seed, 
         if (pattern_fill(p, words, first, seed, s.stream) != hipSuccess) return -1;
         return sync_stream() == 0 ? 0 : -1;
     }
-    unsigned long long *bad_dev = nullptr, bad = 0;
-    if (hipMalloc(&bad_dev, sizeof(bad)) != hipSuccess) return -1;
-    (void)hipMemsetAsync(bad_dev, 0, sizeof(bad), s.stream);
-    hipError_t e = pattern_check(p, words, first, seed, bad_dev, s.stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(&bad, bad_dev, sizeof(bad), hipMemcpyDeviceToHost, s.stream);
+    // One counter kept for the process: hipFree synchronizes the whole device,
+    // which would also wait for the resident copy service's idle exit.
+    if (!s.pattern_bad && hipMalloc(reinterpret_cast<void **>(&s.pattern_bad), sizeof(unsigned long long)) != hipSuccess) {
+        s.pattern_bad = nullptr;
+        return -1;
+    }
+    unsigned long long bad = 0;
+    (void)hipMemsetAsync(s.pattern_bad, 0, sizeof(bad), s.stream);
+    hipError_t e = pattern_check(p, words, first, seed, s.pattern_bad, s.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&bad, s.pattern_bad, sizeof(bad), hipMemcpyDeviceToHost, s.stream);
     int rc = sync_stream();
-    (void)hipFree(bad_dev);
     return (e == hipSuccess && rc == 0) ? (long long)bad : -1;
 }
 

@@ -150,10 +150,23 @@ int service_start(unsigned long long first_seq) {
             s.svc_max = 0;
             OCM_FAIL(-1, "copy service: no device mailbox");
         }
-        if (hipStreamCreateWithFlags(&s.svc_stream, hipStreamNonBlocking) != hipSuccess) {
+        // A stream of its own priority: HIP shares its few hardware queues
+        // (GPU_MAX_HW_QUEUES) among a process's streams, and a launch on a stream
+        // that shares the service's queue waits behind the persistent kernel until
+        // its idle exit (2 ms per large op in bench.py with torch's streams around).
+        // Queues are pooled per priority, so the service's is not shared with the
+        // normal-priority streams of the library and the application.
+        int lo = 0, hi = 0;
+        hipError_t pe = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (pe != hipSuccess || lo == hi ||
+            hipStreamCreateWithPriority(&s.svc_stream, hipStreamNonBlocking, env_int("OCM_SERVICE_STREAM_PRIO", hi)) !=
+                hipSuccess) {
             (void)hipGetLastError();
-            s.svc_max = 0;
-            OCM_FAIL(-1, "copy service: no stream");
+            if (hipStreamCreateWithFlags(&s.svc_stream, hipStreamNonBlocking) != hipSuccess) {
+                (void)hipGetLastError();
+                s.svc_max = 0;
+                OCM_FAIL(-1, "copy service: no stream");
+            }
         }
         const bool gangrec = (s.svc_proto & kServiceProtoGangRec) && s.svc_blocks > 1;
         const bool wc = (s.svc_proto & kServiceProtoWCReq) != 0;
