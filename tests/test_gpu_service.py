@@ -128,3 +128,29 @@ def test_quiesce_lets_a_device_sync_return_at_once(mesh_factory):
             assert a.check(seed=70 + i, nbytes=n) == 0, f"round {i}"
         assert best < 1e-3, f"quiesce + device sync took {best * 1e3:.2f} ms (idle exit is 2 ms)"
         a.free()
+
+
+def test_launch_after_service_ops_does_not_wait_for_the_service(mesh_factory):
+    # The persistent service must not share a hardware queue with the launch
+    # streams: a launch queued behind it waits for its 2 ms idle exit. Here torch
+    # owns streams too (as in bench.py), small ops keep the service resident, and
+    # each following large op (a launch, above the 64 MiB same-GPU bound) must
+    # take its own time only.
+    torch.cuda.synchronize()
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 160 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_LOOPBACK)
+        a.fill(seed=9, nbytes=n)
+        a.put(0, 0, n)
+        a.fill(seed=0, nbytes=n)
+        a.get(0, 0, n)
+        assert a.check(seed=9, nbytes=n) == 0
+        worst = 0.0
+        for _ in range(6):
+            a.put(0, 0, 4096)  # the service is resident after this
+            t0 = time.perf_counter()
+            a.get(0, 0, 128 << 20)  # ~50 us of copying on MI355X
+            worst = max(worst, time.perf_counter() - t0)
+        assert worst < 1e-3, f"a 128 MiB launch after a service op took {worst * 1e3:.2f} ms"
+        a.free()
