@@ -206,6 +206,7 @@ struct State {
     uint64_t svc_host_tile_min = 64ull << 10;                             // OCM_SERVICE_HOST_TILE_MIN
     uint64_t svc_host_tile_max = 256ull << 10;                            // OCM_SERVICE_HOST_TILE_MAX
     bool svc_running = false;
+    bool svc_shared_queue = false;  // no priority stream for the service: it may share a launch stream's hardware queue
     bool svc_park_kernel = false;  // park the service during kernel transfers above svc_max (OCM_SERVICE_PARK_KERNEL)
     unsigned long long svc_seq = 0;
     uint64_t svc_ops = 0, svc_ns_post = 0, svc_ns_wait = 0;  // service diagnostics (ocm_x_service_stats)

@@ -162,6 +162,7 @@ int service_start(unsigned long long first_seq) {
             hipStreamCreateWithPriority(&s.svc_stream, hipStreamNonBlocking, env_int("OCM_SERVICE_STREAM_PRIO", hi)) !=
                 hipSuccess) {
             (void)hipGetLastError();
+            s.svc_shared_queue = true;  // launches park the service first (see xfer)
             if (hipStreamCreateWithFlags(&s.svc_stream, hipStreamNonBlocking) != hipSuccess) {
                 (void)hipGetLastError();
                 s.svc_max = 0;
@@ -384,7 +385,9 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     hipStream_t st = async ? lane_stream(a) : s.stream;
     if (honor_dep(a, st, false) != 0) return -1;
     if (use_kernel) {
-        if (s.svc_park_kernel && len > s.svc_limit(a)) service_park();  // A/B: no resident poller during the copy
+        // A/B: no resident poller during the copy; and without a queue of its own
+        // the service would hold this launch until its idle exit.
+        if ((s.svc_park_kernel || s.svc_shared_queue) && len > s.svc_limit(a)) service_park();
         XferArgs x;
         std::memset(&x, 0, sizeof(x));
         x.lin = lin;
