@@ -7,7 +7,8 @@
 // cache line moves between them in tens of ns instead of hundreds. The daemon
 // of GPU g and the apps that copy on GPU g both restrict themselves to the
 // same CCD of g's NUMA node (chosen by g's ordinal, so the GPUs of one node get
-// different CCDs), the daemon to a core of its own; OCM_PIN=0 turns it off. No reference counterpart: the
+// different CCDs), the daemon to a core of its own; OCM_PIN=0 turns it off
+// (apps opt in with OCM_PIN=1: see pin_near_gpu). No reference counterpart: the
 // reference's daemon and apps ran wherever the scheduler put them.
 #pragma once
 #include <string>
@@ -26,12 +27,21 @@ std::vector<int> ccd_cpus(int node, int slot);
 // Returns the number of CPUs it may now run on (0: unchanged, nothing in common).
 int pin_thread(const std::vector<int> &cpus);
 
+// The CPUs the calling thread may run on now (empty if unknown).
+std::vector<int> thread_cpus();
+// Set the calling thread's mask to exactly `cpus` (e.g. restore a saved mask
+// for a thread that must not share the pinned event loop's core). 0 on success.
+int set_thread_cpus(const std::vector<int> &cpus);
+
 // Hardware threads sharing `cpu`'s core (itself included).
 std::vector<int> core_siblings(int cpu);
 
-// Unless OCM_PIN=0: the event loop of daemon `daemon_rank` on one core of the
-// GPU's L3 complex (one hardware thread; core = rank modulo the complex's
-// cores), an app thread of that daemon on the complex's other cores.
+// Daemon (unless OCM_PIN=0): the event loop of daemon `daemon_rank` on one core
+// of the GPU's L3 complex (one hardware thread; core = rank modulo the complex's
+// cores). App (only when OCM_PIN is set, e.g. OCM_PIN=1): the calling thread on
+// the complex's other cores. Apps are not pinned by default, because the mask
+// of the calling thread (usually the application's main thread) is inherited by
+// every thread and process it creates later (intra-op pools, data loaders).
 // Returns the CPUs pinned to (empty: not pinned); logs the choice under OCM_VERBOSE.
 enum class PinRole { Daemon, App };
 std::vector<int> pin_near_gpu(const std::string &bus_id, int gpu_ordinal, PinRole role, int daemon_rank);

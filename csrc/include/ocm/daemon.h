@@ -20,6 +20,7 @@
 #include <set>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "ocm/arena.h"
@@ -156,6 +157,18 @@ private:
     // dispatch
     void handle_app_msg(Msg &m);
     void handle_mesh_msg(Msg &m, int from_fd);
+    // Once a tick transport exists, the allocation protocol's records are
+    // remembered by content: when the transport fails, a sender re-sends over TCP
+    // every record it cannot prove delivered (TickTransport::take_unsent), and a
+    // copy of one that did arrive (by the tick, or by TCP first) is dropped here
+    // instead of being handled twice (a second DO_ALLOC would leak the first
+    // extent; a second DO_ALLOC response would free a live one). Those records
+    // are unique by construction (seq, alloc_id, extent index), so a repeat is
+    // always such a copy.
+    bool mesh_duplicate(const Msg &m);
+    std::unordered_set<uint64_t> mesh_seen_;    // content hashes (bounded window)
+    std::deque<uint64_t> mesh_seen_order_;      // the same, oldest first
+    uint64_t mesh_dups_dropped_ = 0;
     void send_rank(int r, Msg &m);      // to a daemon (self = local queue)
     void send_app(pid_t pid, const Msg &m);
 
@@ -187,6 +200,12 @@ private:
     int preferred_owner() const;
     bool cross_host(int a, int b) const;
     void start_tick(const uint8_t *id);
+    // Leave the tick transport (it failed here, a peer died, or a peer left it):
+    // abort it, re-send over TCP every record it cannot prove delivered, and tell
+    // the peers once (MSG_TICK_STOP) so the whole mesh leaves it together instead
+    // of an idle rank posting into a collective nobody else runs any more.
+    void leave_tick(const char *why);
+    bool tick_left_ = false;
     void on_tick();
     void send_tcp(int r, Msg &m);
 
@@ -228,6 +247,7 @@ private:
     uint64_t n_alloc_ = 0, n_free_ = 0, n_reclaimed_ = 0, n_spilled_ = 0;
     // checkpoint / resume
     uint64_t boot_id_ = 0;               // this process lifetime
+    std::vector<int> orig_cpus_;         // the process's mask before the event loop was pinned (tick thread)
     size_t pinned_cpus_ = 0;             // event loop restricted to this many CPUs near the GPU (0: not pinned)
     SipKey mesh_key_{};                  // HELLO MAC key (namespace + OCM_MESH_KEY)
     std::unordered_map<uint64_t, uint64_t> hello_seen_;  // nonce -> ts_ms of HELLOs accepted in the window

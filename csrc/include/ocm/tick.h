@@ -113,6 +113,8 @@ public:
     // until every rank joined).
     TickTransport(int rank, int nranks, CollectiveFactory factory);
     ~TickTransport();
+    // CPUs the tick thread runs on (set before start(); empty: inherit the caller's).
+    void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
     void start();
     void stop();
     void abort();          // a peer died: stop ticking, fall back to TCP
@@ -153,6 +155,11 @@ private:
     void flush_ring();
     uint64_t unsent() const;
     int efd_ = -1;
+    std::vector<int> cpus_;
+    // Host-filled collectives: records of issued ticks not yet completed here
+    // (and how many each tick took), re-sent by take_unsent if the tick fails.
+    std::deque<TickRecord> inflight_;
+    std::deque<uint32_t> inflight_n_;
 };
 
 }  // namespace ocm

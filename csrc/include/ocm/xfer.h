@@ -140,7 +140,12 @@ hipError_t xfer_batch_graph_node(hipGraph_t graph, hipGraphNode_t dep, const Xfe
 // svc_doorbell_r01.json (a BAR-mapped HBM record was slower than host memory).
 constexpr unsigned long long kServiceStop = ~0ull;
 constexpr int kServiceArgWords = (int)((sizeof(XferArgs) + 7) / 8);
-constexpr int kServiceReqGang = 13;  // record word: active | target << 16
+constexpr int kServiceReqGang = 13;  // record word: active | target << 16 | STRICT
+// Gang word bit 63 (STRICT): some extent is in another GPU's HBM, so this request
+// takes the fenced hand-off (system acquire before the copy, release before
+// `done`) whatever the protocol bits say.
+constexpr unsigned long long kServiceGangStrict = 1ull << 63;
+constexpr unsigned long long kServiceGangTargetMask = (1ull << 47) - 1;  // bits 16..62
 static_assert(kServiceArgWords <= kServiceReqGang, "service request record holds 13 argument words");
 
 struct alignas(128) ServiceReq {
@@ -186,6 +191,7 @@ void service_store_seq(ServiceReq *req, unsigned long long seq);
 //             every wave drains its stores: neither an acquire after the
 //             doorbell nor a system-scope release (buffer_wbl2) before `done`.
 //             Without WT: plain loads and stores, system acquire and release.
+//             STRICT requests (peer HBM) always take the fenced path.
 //   GANGREC   gang requests go to a second host record on a page of their own
 //             (`gang_req`), which the first `direct_wgs` workgroups poll
 //             themselves: no relay through device memory (1.3 us across XCD

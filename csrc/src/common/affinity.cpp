@@ -92,6 +92,29 @@ int pin_thread(const std::vector<int> &cpus) {
     return n;
 }
 
+std::vector<int> thread_cpus() {
+    cpu_set_t cur;
+    CPU_ZERO(&cur);
+    std::vector<int> out;
+    if (sched_getaffinity(0, sizeof(cur), &cur) != 0) return out;
+    for (int c = 0; c < CPU_SETSIZE; c++)
+        if (CPU_ISSET(c, &cur)) out.push_back(c);
+    return out;
+}
+
+int set_thread_cpus(const std::vector<int> &cpus) {
+    cpu_set_t want;
+    CPU_ZERO(&want);
+    int n = 0;
+    for (int c : cpus)
+        if (c >= 0 && c < CPU_SETSIZE) {
+            CPU_SET(c, &want);
+            n++;
+        }
+    if (n == 0) return -1;
+    return sched_setaffinity(0, sizeof(want), &want) == 0 ? 0 : -1;
+}
+
 std::vector<int> core_siblings(int cpu) {
     std::string list;
     if (!read_line("/sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/topology/thread_siblings_list", &list))
@@ -102,6 +125,9 @@ std::vector<int> core_siblings(int cpu) {
 std::vector<int> pin_near_gpu(const std::string &bus_id, int gpu_ordinal, PinRole role, int daemon_rank) {
     const char *e = std::getenv("OCM_PIN");
     if (e && std::strcmp(e, "0") == 0) return {};
+    // Apps opt in: their calling thread's mask would be inherited by everything
+    // the application starts later.
+    if (role == PinRole::App && (!e || !*e)) return {};
     const bool whole_ccd = e && std::strcmp(e, "ccd") == 0;  // everyone on the whole complex
     const int node = pci_numa_node(bus_id);
     std::vector<int> ccd = ccd_cpus(node, gpu_ordinal);

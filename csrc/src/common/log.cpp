@@ -75,6 +75,7 @@ const char *msg_type_str(uint32_t t) {
     case MSG_OWNED_DONE: return "MSG_OWNED_DONE";
     case MSG_NODE_LINKS: return "MSG_NODE_LINKS";
     case MSG_SLAB_FD: return "MSG_SLAB_FD";
+    case MSG_TICK_STOP: return "MSG_TICK_STOP";
     default: return "INVALID MSG TYPE";
     }
 }

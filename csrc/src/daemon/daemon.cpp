@@ -180,6 +180,7 @@ int Daemon::init() {
         // The event loop next to its GPU, on the L3 complex its apps use (ocm/affinity.h);
         // the data server's threads (started above) keep the full mask.
         char bus[64] = {0};
+        orig_cpus_ = thread_cpus();
         if (hipDeviceGetPCIBusId(bus, sizeof(bus), gpu_) == hipSuccess)
             pinned_cpus_ = pin_near_gpu(bus, gpu_, PinRole::Daemon, rank_).size();
         else

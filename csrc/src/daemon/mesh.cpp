@@ -34,7 +34,46 @@ using namespace dm;
 
 // ---------------------------------------------------------------- mesh messages
 
+namespace {
+uint64_t record_hash(const Msg &m) {
+    // FNV-1a over the whole 160-byte record
+    const unsigned char *p = reinterpret_cast<const unsigned char *>(&m);
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(Msg); i++) h = (h ^ p[i]) * 1099511628211ull;
+    return h;
+}
+constexpr size_t kMeshSeenMax = 8192;  // > every rank's unsent window (kTickRing records) together
+}  // namespace
+
+bool Daemon::mesh_duplicate(const Msg &m) {
+    switch (m.type) {
+    case MSG_REQ_ALLOC:
+    case MSG_DO_ALLOC:
+    case MSG_DO_FREE:
+    case MSG_PLACE_FAIL:
+    case MSG_FREED:
+    case MSG_STATS:
+        break;
+    default:
+        return false;
+    }
+    const uint64_t h = record_hash(m);
+    if (!mesh_seen_.insert(h).second) {
+        mesh_dups_dropped_++;
+        OCM_WARN("rank %d: dropping a second copy of %s/%s seq %llu from rank %d (tick fallback re-send)", rank_,
+                 msg_type_str(m.type), msg_status_str(m.status), (unsigned long long)m.seq, m.src_rank);
+        return true;
+    }
+    mesh_seen_order_.push_back(h);
+    if (mesh_seen_order_.size() > kMeshSeenMax) {
+        mesh_seen_.erase(mesh_seen_order_.front());
+        mesh_seen_order_.pop_front();
+    }
+    return false;
+}
+
 void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
+    if (tick_ && mesh_duplicate(m)) return;
     if (from_fd >= 0) {
         // An inbound link is anonymous until its HELLO carries a valid MAC.
         auto it = conns_.find(from_fd);
@@ -130,7 +169,10 @@ void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
         if (!tick_ && cfg_.ctrl != "tcp") start_tick(m.u.raw);
         break;
     case MSG_TICK_WAKE:
-        if (tick_) tick_->wake_at(m.u.req.bytes);
+        if (tick_ && !tick_left_) tick_->wake_at(m.u.req.bytes);
+        break;
+    case MSG_TICK_STOP:
+        if (tick_) leave_tick("a peer left it");
         break;
     case MSG_SHUTDOWN: stop_ = true; break;
     case MSG_PING:
@@ -646,7 +688,7 @@ void Daemon::peer_lost(int rank) {
     for (auto &l : leases_)
         if (l && l->owner == rank) l.reset();  // its memory died with it
     lease_inflight_.erase(rank);
-    if (tick_) tick_->abort();  // the dead rank will never join another tick
+    if (tick_) leave_tick("a peer died");  // the dead rank will never join another tick
     if (gov_) gov_->mark_dead(rank);
     fail_pending_on(rank);
     // Extents we own for allocations that originated at the dead daemon stay
@@ -719,6 +761,9 @@ void Daemon::start_tick(const uint8_t *id) {
         };
     }
     tick_ = std::make_unique<TickTransport>(rank_, n_, f);
+    // The tick thread busy-polls its collective during traffic, and RCCL's proxy
+    // threads inherit its mask: keep them off the event loop's pinned core.
+    if (pinned_cpus_) tick_->set_cpus(orig_cpus_);
     ep_add(tick_->event_fd(), EPOLLIN, tag(T_TICK, 0));
     tick_->start();
     OCM_INFO("rank %d: control records will ride the %s tick transport", rank_, cfg_.ctrl.c_str());
@@ -739,10 +784,25 @@ void Daemon::on_tick() {
         for (int r = 0; r < n_; r++)
             if (r != rank_) send_tcp(r, w);
     }
-    if (tick_->failed()) {
-        // send_rank: records to ourselves (OCM_TICK_SELF) go back to the local queue
-        for (TickRecord &rec : tick_->take_unsent()) send_rank(rec.dest, rec.msg);
-    }
+    if (tick_->failed()) leave_tick("the collective failed here");
+}
+
+void Daemon::leave_tick(const char *why) {
+    if (!tick_) return;
+    if (!tick_->failed()) tick_->abort();
+    // send_rank: records to ourselves (OCM_TICK_SELF) go back to the local queue
+    for (TickRecord &rec : tick_->take_unsent()) send_rank(rec.dest, rec.msg);
+    if (tick_left_) return;
+    tick_left_ = true;
+    OCM_WARN("rank %d: leaving the %s tick transport (%s); control records ride TCP", rank_,
+             tick_->collective_name(), why);
+    Msg s;
+    std::memset(&s, 0, sizeof(s));
+    s.type = MSG_TICK_STOP;
+    s.status = MSG_REQUEST;
+    s.rank = rank_;
+    for (int r = 0; r < n_; r++)
+        if (r != rank_ && peer_fd_[r] >= 0) send_tcp(r, s);
 }
 
 bool Daemon::cross_host(int a, int b) const {

@@ -4,6 +4,8 @@
 // SURVEY K11); the MI355X design carries the records over RCCL on xGMI.
 #include "ocm/tick.h"
 
+#include "ocm/affinity.h"
+
 #include <hip/hip_runtime_api.h>
 #include <poll.h>
 #include <rccl/rccl.h>
@@ -257,6 +259,8 @@ public:
         bytes_ = bytes;
         send_.assign(bytes, 0);
         recv_.assign(bytes * (size_t)n, 0);
+        const char *tf = std::getenv("OCM_TICK_FAULT");
+        fault_do_alloc_ = tf && std::strcmp(tf, "fail_after_do_alloc") == 0 && bytes == sizeof(TickSlot);
         const char *sl = std::getenv("OCM_TICK_SOCKET_SEAL");
         if (sl && std::strcmp(sl, "1") == 0 && bytes == sizeof(TickSlot)) {
             outbox_.reset(new TickRing());
@@ -310,7 +314,24 @@ public:
         }
         return 0;
     }
-    int test(int) override { return aborted_ ? -1 : 1; }
+    int test(int) override {
+        if (aborted_) return -1;
+        if (fault_do_alloc_ && !fault_fired_) {
+            // OCM_TICK_FAULT=fail_after_do_alloc (tests): the tick that carried one of
+            // our DO_ALLOC requests reached every peer, then fails here, so the
+            // fallback re-sends a record the owner already has.
+            const TickSlot *slot = reinterpret_cast<const TickSlot *>(send_.data());
+            for (uint32_t r = 0; r < slot->count && r < (uint32_t)kTickMsgs; r++)
+                if (slot->rec[r].msg.type == MSG_DO_ALLOC && slot->rec[r].msg.status == MSG_REQUEST) {
+                    fault_fired_ = true;
+                    error_ = "injected failure after a DO_ALLOC tick (OCM_TICK_FAULT)";
+                    abort();
+                    return -1;
+                }
+        }
+        return 1;
+    }
+    std::string error() const override { return error_; }
     void abort() override {
         aborted_ = true;
         if (left_ >= 0) shutdown(left_, SHUT_RDWR);
@@ -343,6 +364,8 @@ private:
     std::unique_ptr<TickRing> outbox_;  // OCM_TICK_SOCKET_SEAL
     uint64_t consumed_ = 0;
     std::atomic<bool> aborted_{false};
+    bool fault_do_alloc_ = false, fault_fired_ = false;
+    std::string error_;
 };
 
 }  // namespace
@@ -481,12 +504,17 @@ bool TickTransport::take_announce(uint64_t *tick) {
 
 std::vector<TickRecord> TickTransport::take_unsent() {
     std::lock_guard<std::mutex> lk(mu_);
-    // Ring records past the last completed tick of ours (one sealed into a tick
-    // that then failed may also have reached its peer: the fallback may repeat it).
+    // Ring records past the last completed tick of ours, or (host-filled) the
+    // records of ticks issued but not completed here, then the queue. A record of
+    // a tick that failed here may still have reached its peer: the fallback may
+    // repeat it, and the receiver drops the copy (Daemon::mesh_duplicate).
     std::vector<TickRecord> v;
     if (ring_)
         for (uint64_t j = ring_sent_; j < ring_pub_; j++) v.push_back(ring_->rec[j & (kTickRing - 1)]);
+    v.insert(v.end(), inflight_.begin(), inflight_.end());
     v.insert(v.end(), out_.begin(), out_.end());
+    inflight_.clear();
+    inflight_n_.clear();
     out_.clear();
     ring_sent_ = ring_pub_;
     return v;
@@ -500,6 +528,7 @@ void TickTransport::run() {
     // wake-up. Up to depth() ticks are queued at once; tick k's records are
     // read from ring slot (k - 1) % depth.
     constexpr uint64_t kBusyTicks = 64;
+    if (!cpus_.empty()) (void)set_thread_cpus(cpus_);
     std::string err;
     std::unique_ptr<Collective> c = factory_(&err, &stop_);
     auto signal = [this] {
@@ -558,8 +587,10 @@ void TickTransport::run() {
                     slot->first = 0;
                     while (!out_.empty() && slot->count < (uint32_t)kTickMsgs) {
                         slot->rec[slot->count++] = out_.front();
+                        inflight_.push_back(out_.front());  // until the tick completes here
                         out_.pop_front();
                     }
+                    inflight_n_.push_back(slot->count);
                     slot->busy = out_.empty() ? 0 : 1;
                 }
                 if (announce_.load()) signal();  // let the event loop wake the peers first
@@ -600,6 +631,9 @@ void TickTransport::run() {
                 const TickSlot &mine = got[rank_];
                 ring_sent_ = std::max<uint64_t>(ring_sent_, mine.first + std::min<uint32_t>(mine.count, kTickMsgs));
                 flush_ring();
+            } else if (!inflight_n_.empty()) {
+                for (uint32_t r = 0; r < inflight_n_.front() && !inflight_.empty(); r++) inflight_.pop_front();
+                inflight_n_.pop_front();
             }
             for (int k = 0; k < n_; k++) {
                 const TickSlot &sl = got[k];

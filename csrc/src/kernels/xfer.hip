@@ -597,14 +597,20 @@ __device__ __forceinline__ void service_stamp(ServiceBox *box, unsigned proto, i
 __device__ __forceinline__ void service_serve(const unsigned long long *sh, unsigned long long s, ServiceSlot *slot,
                                               ServiceBox *box, unsigned proto) {
     const unsigned long long gang = sh[1];
-    const unsigned long long active = gang & 0xFFFFull, target = gang >> 16;
+    const unsigned long long active = gang & 0xFFFFull, target = (gang >> 16) & kServiceGangTargetMask;
     if (blockIdx.x >= active) return;  // block-uniform: workgroups past `active` sit this one out
+    // STRICT requests (extents in another GPU's HBM) take the fenced hand-off even
+    // under the WT protocol: sc1 accesses keep this GPU's caches coherent with host
+    // memory and its own HBM, but a resident instance may hold L2 lines of peer
+    // memory from an earlier request, and nothing else invalidates them.
+    const bool wt = (proto & kServiceProtoWT) && !(gang & kServiceGangStrict);
     service_stamp(box, proto, 1);
-    if (proto & kServiceProtoWT) {
+    if (wt) {
         service_copy<ST_WT>(sh, blockIdx.x, active);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its sc1 stores
         __syncthreads();
     } else {
+        if (proto & kServiceProtoWT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the poll skipped it
         service_copy<ST_PLAIN>(sh, blockIdx.x, active);
         block_release_system();
     }
@@ -613,13 +619,12 @@ __device__ __forceinline__ void service_serve(const unsigned long long *sh, unsi
         bool last = active == 1;
         if (!last) {
             const unsigned long long old =
-                (proto & kServiceProtoWT)
-                    ? __hip_atomic_fetch_add(&box->cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                    : __hip_atomic_fetch_add(&box->cnt, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                wt ? __hip_atomic_fetch_add(&box->cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : __hip_atomic_fetch_add(&box->cnt, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
             last = old == target - 1;
         }
         if (last) {
-            if (proto & kServiceProtoWT)
+            if (wt)
                 __hip_atomic_store(&slot->done, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // after the drain
             else
                 __hip_atomic_store(&slot->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -98,6 +98,7 @@ int run_batch(lib_alloc *a, XferBatchArgs &args, std::vector<XferBatchOp> &v, bo
         args.ops = static_cast<const XferBatchOp *>(a->batch_dev);
         args.wave_op = reinterpret_cast<const uint32_t *>(static_cast<char *>(a->batch_dev) + dbytes);
     }
+    before_launch();
     err = xfer_batch_launch(args, s.tuning, st);
     if (err != hipSuccess) OCM_FAIL(-1, "batch launch failed: %s", hipGetErrorString(err));
     s.ctr.n_batch_launches++;
@@ -301,6 +302,7 @@ int ocm_plan_launch(ocm_plan_t p, void *stream) {
         if (a->async_pending && a->ev) (void)hipStreamWaitEvent(st, a->ev, 0);
         if (honor_dep(a, st, false) != 0) return -1;
     }
+    before_launch();
     e = hipGraphLaunch(p->exec, st);
     if (e != hipSuccess) OCM_FAIL(-1, "ocm_plan_launch: %s", hipGetErrorString(e));
     int rc = stream ? 0 : sync_stream();

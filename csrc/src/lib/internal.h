@@ -60,6 +60,7 @@ constexpr unsigned kServiceGangHostDefault = 32;
 // keeps kServiceMaxDefault, above which the autotuned launches take over.
 constexpr uint64_t kServiceMaxLocalDefault = 64ull << 20;
 constexpr int kServiceSoloTilesDefault = 2;
+constexpr int kServiceIdleUsDefault = 50;
 // Write-through hand-offs, the records in write-combined memory, and gang
 // requests polled directly by the first 16 workgroups: small ops -0.1/-0.2 us,
 // host-tier 128 KiB-4 MiB and HBM 256 KiB-1 MiB gangs 1-1.5 us faster than the
@@ -113,6 +114,7 @@ struct lib_alloc {
     bool all_dev_ok = false;  // every extent reachable by a kernel on this GPU
     bool any_net = false;     // some extent lives on another node
     bool same_gpu = false;    // every extent in this process's own GPU's HBM (another daemon on it, via IPC)
+    bool any_peer = false;    // some extent in ANOTHER GPU's HBM (xGMI): the copy service's fenced hand-off
     bool async_pending = false;
     bool pooled = false;      // local half from the stream-ordered pool
     int lane = -1;            // async ops: index into State::lanes (per-allocation ordering)
@@ -220,7 +222,12 @@ struct State {
         if (!a->any_gpu) return svc_max_host;
         return a->same_gpu ? std::max(svc_max, svc_max_local) : svc_max;
     }
-    unsigned long long svc_idle_ticks = 200000ull;  // 2 ms at 100 MHz: live only during bursts of small ops
+    // Idle exit after OCM_SERVICE_IDLE_US (50 us; 100 MHz ticks): long enough to
+    // stay resident through a burst of blocking ops, short enough that a
+    // device-wide synchronize right after one (torch.cuda.synchronize) does not
+    // wait long for the persistent kernel to leave.
+    unsigned long long svc_idle_ticks = 100ull * kServiceIdleUsDefault;
+    uint64_t svc_relaunches = 0;    // instances started after an idle exit (ocm_x_service_stats)
     // network tier
     std::map<std::string, NetConn> net_conns;  // "ip:port#stream" -> connection
     std::map<int, int> fd_chans;               // owner rank -> mailbox connection for slab fds (MSG_SLAB_FD)
@@ -338,7 +345,10 @@ int sync_stream();
 int service_start(unsigned long long first_seq);
 void service_park();
 void service_stop();
-int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm);
+// strict: an extent is in another GPU's HBM (kServiceGangStrict).
+int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict);
+// Before a library launch: park the service when it may share the launch's hardware queue.
+void before_launch();
 // `done` (optional, async launches on a lane): receives the kernel-published
 // completion flag of the launch, or flag == nullptr when the op has none.
 int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t len, bool async,

@@ -123,7 +123,7 @@ int ocm_init(void) {
     if (const char *v = std::getenv("OCM_SERVICE_HOST_TILE_MIN"); v && *v) s.svc_host_tile_min = std::strtoull(v, nullptr, 0);
     s.launch_flags = env_int("OCM_LAUNCH_FLAG", 1) != 0;
     s.svc_park_kernel = env_int("OCM_SERVICE_PARK_KERNEL", 0) != 0;
-    s.svc_idle_ticks = 100ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_IDLE_US", 2000));  // 100 MHz clock
+    s.svc_idle_ticks = 100ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_IDLE_US", kServiceIdleUsDefault));  // 100 MHz clock
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");
     s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
     s.tuning = xfer_tuning_from_env();
@@ -286,6 +286,8 @@ static ocm_alloc_t alloc_impl(ocm_alloc_param_t p, const struct ocm_alloc_ex_par
             a->any_gpu = a->any_gpu && !a->any_net;
             a->same_gpu = a->all_gpu && s.device >= 0;
             for (auto &e : a->ext) a->same_gpu &= e.r.owner_gpu == s.device;
+            a->any_peer = false;
+            for (auto &e : a->ext) a->any_peer |= !e.net && e.r.tier == TIER_GPU && e.r.owner_gpu != s.device;
             Loc want = kind == OCM_REMOTE_GPU ? LOC_DEVICE : LOC_PINNED;
             ok = alloc_local_half(a, p->local_alloc_bytes, want) == 0;
         }
@@ -729,6 +731,7 @@ int ocm_x_adam_multi(ocm_alloc_t a, int count, void *const *p, const void *const
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (wait_alloc(a) != 0) return -1;
     DeviceGuard dg(s.device);
+    before_launch();
     for (int k0 = 0; k0 < count; k0 += kAdamMaxTensors) {
         x.count = (uint32_t)std::min(count - k0, kAdamMaxTensors);
         for (uint32_t j = 0; j < x.count; j++) {
@@ -780,6 +783,7 @@ static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (wait_alloc(a) != 0) return -1;  // queued async ops on this allocation come first
     DeviceGuard dg(s.device);
+    before_launch();
     const hipError_t e = adam_remote_launch(x, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) OCM_FAIL(-1, "ocm_x_adam launch: %s", hipGetErrorString(e));
     return 0;
@@ -787,8 +791,9 @@ static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64
 
 // Park the resident copy service now. A device-wide synchronize
 // (hipDeviceSynchronize, torch.cuda.synchronize) waits for every stream,
-// including the service's persistent kernel, which otherwise leaves only after
-// OCM_SERVICE_IDLE_US (2 ms) without work; the next small op relaunches it.
+// including the service's persistent kernel, which otherwise leaves by itself
+// after OCM_SERVICE_IDLE_US (50 us) without work; the next small op relaunches it.
+// Optional: only callers that cannot afford those microseconds need it.
 void ocm_x_quiesce(void) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
@@ -796,7 +801,9 @@ void ocm_x_quiesce(void) {
 }
 
 // Copy-service diagnostics: {ops, ns posting requests, ns waiting for done,
-// GPU ticks (100 MHz) from doorbell seen to done published, doorbell in HBM}.
+// GPU ticks (100 MHz) from doorbell seen to done published, relaunches after an
+// idle exit}. The doorbell record stays in host memory (a BAR-mapped HBM record
+// measured slower: profiles/svc_doorbell_hbm_ab_r02.json).
 void ocm_x_service_stats(uint64_t out[5]) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
@@ -804,7 +811,7 @@ void ocm_x_service_stats(uint64_t out[5]) {
     out[1] = s.svc_ns_post;
     out[2] = s.svc_ns_wait;
     out[3] = s.svc ? __atomic_load_n(&s.svc->gpu_ticks, __ATOMIC_ACQUIRE) : 0;
-    out[4] = 0;  // doorbell record in host memory (a BAR-mapped HBM record measured slower: profiles/svc_doorbell_hbm_ab_r02.json)
+    out[4] = s.svc_relaunches;  // instances started because the previous one left idle
 }
 
 // Copy-service phase stamps of the last request (OCM_SERVICE_PROTO with the
@@ -1110,6 +1117,10 @@ void ocm_torch_free(void *ptr, ssize_t size, int device, void *stream) {
     {
         // hipFree semantics: kernels still reading or writing the block finish
         // before its bytes go back to the owner (which may hand them out again).
+        // Park the copy service first and hold the lock across the sync, so no
+        // other thread relaunches it in between and the wait stays bounded.
+        std::lock_guard<std::recursive_mutex> lk(s.mu);
+        service_park();
         DeviceGuard g(s.device);
         if (hipDeviceSynchronize() != hipSuccess) (void)hipGetLastError();
     }

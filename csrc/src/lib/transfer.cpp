@@ -201,6 +201,15 @@ int service_start(unsigned long long first_seq) {
     return 0;
 }
 
+// Without a stream priority of its own (svc_shared_queue) the service may share
+// a hardware queue with the library's launch streams, and a launch queued behind
+// the persistent kernel would wait for its idle exit: park it first. Application
+// kernels on such a queue still wait up to OCM_SERVICE_IDLE_US.
+void before_launch() {
+    State &s = S();
+    if (s.svc_shared_queue) service_park();
+}
+
 // Park the resident kernel: its doorbell polls cross PCIe and slow down
 // large DMA-engine transfers (measured: 53 -> 34 GiB/s on host-tier sweeps).
 void service_park() {
@@ -236,7 +245,7 @@ void service_stop() {
 }
 
 // Run one normalized transfer through the resident kernel and wait for it.
-int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm) {
+int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
     State &s = S();
     if (xfer_normalize(x) != hipSuccess) OCM_FAIL(-1, "invalid transfer");
     if (!hbm && x.len >= s.svc_host_tile_min && x.len <= s.svc_host_tile_max) {
@@ -244,6 +253,14 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm) {
         if (sh >= 12 && sh < x.tile_shift) x.tile_shift = sh;
     }
     const unsigned long long seq = ++s.svc_seq;
+    if (s.svc_running && __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE) != 0) {
+        // The instance left on its idle timeout (OCM_SERVICE_IDLE_US): reap it and
+        // start the next one right away instead of posting to nobody.
+        DeviceGuard g(s.device);
+        (void)hipStreamSynchronize(s.svc_stream);
+        s.svc_running = false;
+        s.svc_relaunches++;
+    }
     if (!s.svc_running && service_start(seq) != 0) return -1;
     // The host sizes the gang and the completion count every workgroup agrees on:
     // up to the direct pollers (no relay) for ops they copy fast enough.
@@ -257,7 +274,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm) {
             s.svc_gang_total += active;
             target = s.svc_gang_total;
         }
-        return active | (target << 16);
+        return active | (target << 16) | (strict ? kServiceGangStrict : 0ull);
     };
     unsigned long long gang = gang_word();
     // GANGREC: gang requests go to the record the whole gang polls.
@@ -280,6 +297,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm) {
                 DeviceGuard g(s.device);
                 (void)hipStreamSynchronize(s.svc_stream);
                 s.svc_running = false;
+                s.svc_relaunches++;
                 if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
                 if (service_start(seq) != 0) return -1;
                 gang = gang_word();              // counted afresh by the new instance
@@ -375,7 +393,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         // HBM owners keep small requests on workgroup 0 (profiles/svc_v4_r02.json).
         const unsigned solo = (!put && !a->any_gpu) ? std::min(s.svc_solo_tiles, s.svc_solo_tiles_host_get)
                                                     : s.svc_solo_tiles;
-        if (service_xfer(x, solo, a->any_gpu) == 0) return 0;
+        if (service_xfer(x, solo, a->any_gpu, a->any_peer) == 0) return 0;
         OCM_WARN("copy service failed (%s); falling back to launches", last_error());
         s.svc_max = 0;
     }
@@ -387,7 +405,8 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     if (use_kernel) {
         // A/B: no resident poller during the copy; and without a queue of its own
         // the service would hold this launch until its idle exit.
-        if ((s.svc_park_kernel || s.svc_shared_queue) && len > s.svc_limit(a)) service_park();
+        if (s.svc_park_kernel && len > s.svc_limit(a)) service_park();
+        before_launch();
         XferArgs x;
         std::memset(&x, 0, sizeof(x));
         x.lin = lin;
@@ -470,6 +489,7 @@ int copy_local(void *dst, Loc dl, const void *src, Loc sl, size_t n) {
     }
     DeviceGuard g(s.device);
     hipError_t e;
+    before_launch();
     if (dl == LOC_DEVICE && sl == LOC_DEVICE) {
         XferTuning t = s.tuning;
         if (t.variant == XFER_AUTO) t.variant = n <= (256ull << 20) ? XFER_LDS : XFER_REG;

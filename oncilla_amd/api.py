@@ -319,23 +319,24 @@ def counters() -> dict:
 
 
 def quiesce() -> None:
-    """Park this process's resident copy service, so that a device-wide
-    synchronize (torch.cuda.synchronize) does not wait for the service's idle
-    exit (OCM_SERVICE_IDLE_US, 2 ms by default). Call it before such a sync when
-    the last library op was a small blocking one; the next op relaunches the
-    service. No-op without a GPU or before any op."""
+    """Park this process's resident copy service now. Optional: the service
+    leaves by itself OCM_SERVICE_IDLE_US (50 us) after its last op, so a
+    device-wide synchronize (torch.cuda.synchronize) right after a small blocking
+    op waits at most that long; quiesce() removes even that wait. The next op
+    relaunches the service. No-op without a GPU or before any op."""
     load().ocm_x_quiesce()
 
 
 def service_stats() -> dict:
     """Copy-service diagnostics of this process: ops served, mean host time to post a
     request, mean host wait for its completion, mean GPU time from doorbell seen to
-    completion published (microseconds), and where the doorbell record lives."""
+    completion published (microseconds), and how many times it was relaunched after
+    leaving on its idle timeout (OCM_SERVICE_IDLE_US)."""
     out = (ctypes.c_uint64 * 5)()
     load().ocm_x_service_stats(out)
     n = int(out[0])
     return {"ops": n, "post_us": out[1] / n / 1e3 if n else None, "wait_us": out[2] / n / 1e3 if n else None,
-            "gpu_us": out[3] / 100.0 / n if n else None, "doorbell": "hbm" if out[4] else "host"}
+            "gpu_us": out[3] / 100.0 / n if n else None, "relaunches": int(out[4])}
 
 
 def service_trace(n_wgs: int = 32) -> list:

@@ -123,7 +123,7 @@ class OffloadedAdam:
                                     stripe_unit=stripe_unit)]
         a = self.allocs[0]
         a.local_tensor(torch.uint8).zero_()
-        torch.cuda.synchronize(client.device)
+        torch.cuda.current_stream(client.device).synchronize()
         for off in range(0, remote, self.stage):
             a.put(0, off, min(self.stage, remote - off))
         if self.bf16:
@@ -135,7 +135,7 @@ class OffloadedAdam:
                 for e0 in range(0, p.numel(), step):
                     e1 = min(p.numel(), e0 + step)
                     buf[:e1 - e0].copy_(flat[e0:e1].float())
-                    torch.cuda.synchronize(client.device)
+                    torch.cuda.current_stream(client.device).synchronize()  # the copy, before the put reads buf
                     a.put(0, 4 * (2 * self.padded + start + e0), 4 * (e1 - e0))
 
     def _step_fused(self) -> None:
@@ -220,8 +220,9 @@ class OffloadedAdam:
         if self.mode == "fused":
             import torch
 
-            api.quiesce()  # a resident copy service would hold the device-wide sync for its idle exit
-            torch.cuda.synchronize(self.params[0].device)
+            # the update kernels run on torch's current stream (the copy service's
+            # persistent kernel is on a stream of its own and is not waited for)
+            torch.cuda.current_stream(self.params[0].device).synchronize()
         for a in self.allocs:
             a.wait()
 

@@ -90,6 +90,46 @@ def test_tick_peer_death_falls_back_to_tcp(mesh_factory, sealed):
         a.free()
 
 
+@pytest.mark.parametrize("sealed", ["0", "1"])
+def test_tick_failure_after_do_alloc_does_not_duplicate_it(mesh_factory, sealed):
+    """when the tick transport fails, the sender re-sends over TCP
+    every record it cannot prove delivered. Here rank0's tick fails right after
+    the tick that carried its DO_ALLOC reached the owner (OCM_TICK_FAULT), so the
+    owner receives that DO_ALLOC twice; it must allocate once (a second extent
+    would leak, and a second response would free a live one)."""
+    import time
+
+    m = mesh_factory(3, extra_args=["--ctrl", "socket"],
+                     env={"OCM_TICK_SOCKET_SEAL": sealed, "OCM_TICK_FAULT": "fail_after_do_alloc",
+                          "OCM_LEASE_BYTES": "0"})
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        deadline = time.time() + 20  # STATS records ride the ticks too: wait until every rank ticked
+        while not all([c.stats(r)["ctrl_ticks"] > 0 for r in range(3)]):  # every rank asked: remote STATS tick
+            assert time.time() < deadline, "tick transport never came up"
+            time.sleep(0.05)
+        held = []
+        for i in range(6):  # the first DO_ALLOC trips the fault; the rest ride TCP
+            a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)
+            a.fill(seed=60 + i)
+            a.put(0, 0, 1 << 20)
+            a.fill(seed=0)
+            a.get(0, 0, 1 << 20)
+            assert a.check(seed=60 + i) == 0
+            held.append(a)
+        used = sum(c.stats(r)["host_used"] for r in range(3))
+        assert used == 6 << 20, f"{used} bytes placed for 6 x 1 MiB (a re-sent DO_ALLOC was served twice)"
+        for a in held:
+            a.free()
+        deadline = time.time() + 5
+        while sum(c.stats(r)["host_used"] for r in range(3)) and time.time() < deadline:
+            time.sleep(0.05)
+        assert all(c.stats(r)["host_used"] == 0 for r in range(3))
+    logs = m.logs()
+    assert "injected failure after a DO_ALLOC tick" in logs, logs
+    assert "dropping a second copy of MSG_DO_ALLOC" in logs, logs
+    assert logs.count("leaving the socket tick transport") == 3, logs  # the whole mesh left it together
+
+
 def test_socket_tick_self_loop(mesh_factory):
     # OCM_TICK_SELF routes a daemon's self-addressed records through the collective too.
     m = mesh_factory(1, extra_args=["--ctrl", "socket"], env={"OCM_TICK_SELF": "1"})

@@ -62,8 +62,8 @@ def test_service_never_reads_stale_bytes(mesh_factory, rounds):
 
 
 def test_service_restarts_after_idle_exit(mesh_factory):
-    # The service leaves after 2 ms without work (workgroup 0 stores STOP for the
-    # gang); the next op relaunches it. Alternate gang-sized and solo ops across exits.
+    # The service leaves after OCM_SERVICE_IDLE_US without work (workgroup 0 stores
+    # STOP for the gang); the next op relaunches it. Alternate gang-sized and solo ops across exits.
     m = mesh_factory(1, gpus=[0])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         n = 1 << 20
@@ -76,8 +76,9 @@ def test_service_restarts_after_idle_exit(mesh_factory):
             a.get(0, 0, size)
             assert a.check(seed=50 + i, nbytes=size) == 0, f"op pair {i}"
             time.sleep(0.005)
-        ops = api.service_stats()["ops"]
-        assert ops >= 24
+        st = api.service_stats()
+        assert st["ops"] >= 24
+        assert st["relaunches"] >= 10, st  # every 5 ms sleep outlasted the idle exit
         a.free()
 
 
@@ -101,7 +102,7 @@ def test_service_direct_and_relayed_gangs_interleave(mesh_factory):
             a.get(0, 0, size)
             assert a.check(seed=300 + i, nbytes=size) == 0, f"op pair {i} ({size} B)"
             if i % 4 == 3:
-                time.sleep(0.004)  # past the 2 ms idle exit
+                time.sleep(0.004)  # past the idle exit
         hbm.free()
         host.free()
 
@@ -130,13 +131,76 @@ def test_quiesce_lets_a_device_sync_return_at_once(mesh_factory):
         a.free()
 
 
-def test_launch_after_service_ops_does_not_wait_for_the_service(mesh_factory):
+@pytest.mark.parametrize("tier", ["host", "hbm"])
+def test_device_sync_right_after_a_small_op_needs_no_quiesce(mesh_factory, tier):
+    # torch.cuda.synchronize() right after a blocking 4 KiB op
+    # waits for the persistent service's idle exit (OCM_SERVICE_IDLE_US). Without
+    # any quiesce() it must return in < 100 us, and the next op (which relaunches
+    # the service) must still move the right bytes.
+    m = mesh_factory(1, gpus=[0])
+    flags = api.OCM_ALLOC_HOST_TIER if tier == "host" else api.OCM_ALLOC_LOOPBACK
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 4096
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=flags)
+        times = []
+        for i in range(25):
+            a.fill(seed=90 + i, nbytes=n)
+            a.put(0, 0, n)
+            a.put(0, 0, n)  # the service is resident: the second op is served by it
+            t0 = time.perf_counter()
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+            a.fill(seed=0, nbytes=n)
+            a.get(0, 0, n)
+            assert a.check(seed=90 + i, nbytes=n) == 0, f"round {i}"
+        times.sort()
+        med = times[len(times) // 2]
+        print(f"sync after a 4 KiB {tier} put: median {med * 1e6:.1f} us, max {times[-1] * 1e6:.1f} us")
+        assert med < 100e-6, f"device sync after a small op took {med * 1e6:.1f} us (median)"
+        a.free()
+
+
+def test_torch_pool_release_after_small_op_is_fast(mesh_factory):
+    # ocm_torch_free runs a device-wide sync inside torch's allocator;
+    # it parks the copy service first (under the library lock), so releasing a
+    # RemoteMemPool block right after a small blocking op does not wait for the
+    # service's idle exit.
+    import gc
+
+    from oncilla_amd.torch_pool import RemoteMemPool
+
+    m = mesh_factory(2, gpus=[0, 0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=4096, flags=api.OCM_ALLOC_HOST_TIER)
+        pool = RemoteMemPool(c, remote_rank=1)
+        best = 1.0
+        for i in range(5):
+            with pool:
+                t = torch.full((1 << 20,), float(i), device="cuda:0")
+            assert float(t[-1]) == float(i)
+            del t
+            gc.collect()
+            a.put(0, 0, 4096)
+            a.put(0, 0, 4096)  # served by the resident service
+            t0 = time.perf_counter()
+            torch.cuda.empty_cache()  # hands the block back: ocm_torch_free
+            best = min(best, time.perf_counter() - t0)
+        assert RemoteMemPool.stats()["blocks"] == 0
+        assert best < 1e-3, f"releasing a pool block after a small op took {best * 1e3:.2f} ms"
+        del pool
+        gc.collect()
+        a.free()
+
+
+def test_launch_after_service_ops_does_not_wait_for_the_service(mesh_factory, monkeypatch):
     # The persistent service must not share a hardware queue with the launch
-    # streams: a launch queued behind it waits for its 2 ms idle exit. Here torch
+    # streams: a launch queued behind it waits for its idle exit (2 ms here, so a
+    # shared queue would show). Here torch
     # owns streams too (as in bench.py), small ops keep the service resident, and
     # each following large op (a launch, above the 64 MiB same-GPU bound) must
     # take its own time only.
     torch.cuda.synchronize()
+    monkeypatch.setenv("OCM_SERVICE_IDLE_US", "2000")
     m = mesh_factory(1, gpus=[0])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         n = 160 << 20

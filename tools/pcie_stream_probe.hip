@@ -1,0 +1,185 @@
+// Probe: launched streaming copies between HBM and the pinned host tier over
+// PCIe, against the runtime's own copy (hipMemcpyAsync -> __amd_rocclr_copyBuffer).
+//
+// Question (VERDICT r02 "Next round" 1a): which launch shape lets OUR kernel match
+// or beat the runtime blit for host-tier ops of 32 MiB .. 1 GiB? Knobs:
+//   U        16-byte loads in flight per lane before the stores (1, 2, 4, 8)
+//   G        workgroups (256 threads each)
+//   layout   blk: 256*16*U-byte chunks per workgroup, grid-strided (the library's
+//                 tile layout); win: every unrolled load is a grid-wide contiguous
+//                 slice (each lane's U vectors are G*4 KiB apart)
+//   LA / SA  cache-policy bits of the buffer loads / stores (0, nt=2, sc0|sc1=17)
+// Host memory is a memfd MAP_SHARED mapping, hipHostRegister'ed like a host-tier
+// slab (csrc/src/daemon/arena.cpp, csrc/src/lib/runtime.cpp). Every kernel is
+// finite (a grid-stride loop over a fixed range); every config is verified once.
+//
+//   pcie_stream_probe [bytes=256M] [reps=4]   -> one JSON object on stdout
+#include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define CHECK(x)                                                                                      \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) {                                                                       \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));    \
+            std::exit(1);                                                                             \
+        }                                                                                             \
+    } while (0)
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
+}
+
+// LAYOUT 0 = blk, 1 = win. Range checks drop the past-the-end lanes of the last round.
+template <int LAYOUT, int U, int LA, int SA>
+__global__ __launch_bounds__(kThreads) void stream_kernel(char *dst, const char *src, uint32_t bytes) {
+    const __amdgpu_buffer_rsrc_t rs = rsrc(src, bytes), rd = rsrc(dst, bytes);
+    const uint32_t nv = bytes >> 4;
+    const uint32_t tid = threadIdx.x;
+    if constexpr (LAYOUT == 0) {
+        const uint32_t chunk = kThreads * U;  // vectors
+        for (uint32_t c = blockIdx.x * chunk; c < nv; c += gridDim.x * chunk) {
+            u32x4 v[U];
+#pragma unroll
+            for (int k = 0; k < U; k++)
+                v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((c + k * kThreads + tid) << 4), 0, LA);
+#pragma unroll
+            for (int k = 0; k < U; k++)
+                __builtin_amdgcn_raw_buffer_store_b128(v[k], rd, (int)((c + k * kThreads + tid) << 4), 0, SA);
+        }
+    } else {
+        const uint32_t T = gridDim.x * kThreads;
+        for (uint32_t i = blockIdx.x * kThreads + tid; i - tid < nv; i += U * T) {
+            u32x4 v[U];
+#pragma unroll
+            for (int k = 0; k < U; k++) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((i + k * T) << 4), 0, LA);
+#pragma unroll
+            for (int k = 0; k < U; k++) __builtin_amdgcn_raw_buffer_store_b128(v[k], rd, (int)((i + k * T) << 4), 0, SA);
+        }
+    }
+}
+
+typedef void (*KernFn)(char *, const char *, uint32_t);
+
+struct Variant {
+    const char *name;
+    KernFn fn;
+};
+
+#define V(L, U, LA, SA) {#L "/u" #U "/la" #LA "/sa" #SA, stream_kernel<L, U, LA, SA>}
+static const Variant kVariants[] = {
+    V(0, 1, 2, 2), V(0, 2, 2, 2), V(0, 4, 2, 2), V(0, 8, 2, 2),
+    V(0, 1, 0, 0), V(0, 2, 0, 0), V(0, 4, 0, 0), V(0, 8, 0, 0),
+    V(0, 4, 17, 2), V(0, 4, 2, 0), V(0, 4, 17, 0), V(0, 4, 0, 2),
+    V(1, 1, 2, 2), V(1, 2, 2, 2), V(1, 4, 2, 2), V(1, 8, 2, 2),
+    V(1, 1, 0, 0), V(1, 4, 0, 0), V(1, 4, 17, 2),
+};
+#undef V
+
+int main(int argc, char **argv) {
+    const uint64_t bytes = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : (256ull << 20);
+    const int reps = argc > 2 ? std::atoi(argv[2]) : 4;
+    if (bytes == 0 || bytes > (1ull << 30) || (bytes & 4095)) {
+        std::fprintf(stderr, "bytes must be a multiple of 4 KiB in (0, 1 GiB]\n");
+        return 2;
+    }
+    const int fd = memfd_create("pcie_probe", 0);
+    if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) return 1;
+    void *host = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (host == MAP_FAILED) return 1;
+    std::memset(host, 0x5a, bytes);
+    CHECK(hipHostRegister(host, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    void *hdev = nullptr;
+    CHECK(hipHostGetDevicePointer(&hdev, host, 0));
+    void *dev = nullptr;
+    CHECK(hipMalloc(&dev, bytes));
+    std::vector<unsigned> pattern(bytes / 4), back(bytes / 4);
+    for (size_t i = 0; i < pattern.size(); i++) pattern[i] = (unsigned)(i * 2654435761u) ^ 0x9e37u;
+    hipStream_t st;
+    CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    int cus = 0;
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+
+    auto prep = [&](int dir) {  // dir 0 get (host -> dev), 1 put (dev -> host)
+        if (dir == 0) {
+            std::memcpy(host, pattern.data(), bytes);
+            CHECK(hipMemset(dev, 0, bytes));
+        } else {
+            CHECK(hipMemcpy(dev, pattern.data(), bytes, hipMemcpyHostToDevice));
+            std::memset(host, 0, bytes);
+        }
+        CHECK(hipDeviceSynchronize());
+    };
+    auto verify = [&](int dir, const char *what) {
+        if (dir == 0)
+            CHECK(hipMemcpy(back.data(), dev, bytes, hipMemcpyDeviceToHost));
+        else
+            std::memcpy(back.data(), host, bytes);
+        if (std::memcmp(back.data(), pattern.data(), bytes) != 0) {
+            std::fprintf(stderr, "MISMATCH %s dir %d\n", what, dir);
+            std::exit(3);
+        }
+    };
+    // median GB/s of `reps` timed runs after one untimed
+    auto timeit = [&](auto &&launch) {
+        launch();
+        CHECK(hipStreamSynchronize(st));
+        std::vector<float> t;
+        for (int r = 0; r < reps; r++) {
+            CHECK(hipEventRecord(e0, st));
+            launch();
+            CHECK(hipEventRecord(e1, st));
+            CHECK(hipEventSynchronize(e1));
+            float ms = 0;
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        return bytes / (t[t.size() / 2] * 1e-3) / 1e9;
+    };
+
+    std::printf("{\"bytes\": %llu, \"cus\": %d", (unsigned long long)bytes, cus);
+    for (int dir = 0; dir < 2; dir++) {
+        char *dst = (char *)(dir ? hdev : dev);
+        const char *src = (const char *)(dir ? dev : hdev);
+        prep(dir);
+        const double blit = timeit([&] {
+            CHECK(hipMemcpyAsync(dir ? host : dev, dir ? dev : host, bytes, hipMemcpyDefault, st));
+        });
+        verify(dir, "blit");
+        std::printf(", \"%s/blit\": %.2f", dir ? "put" : "get", blit);
+        std::fflush(stdout);
+        const int grids[] = {cus / 2, cus, 2 * cus, 4 * cus, 8 * cus};
+        for (const Variant &v : kVariants) {
+            for (int g : grids) {
+                prep(dir);
+                const double gbs = timeit([&] {
+                    hipLaunchKernelGGL(v.fn, dim3(g), dim3(kThreads), 0, st, dst, src, (uint32_t)bytes);
+                    CHECK(hipGetLastError());
+                });
+                verify(dir, v.name);
+                std::printf(", \"%s/%s/g%d\": %.2f", dir ? "put" : "get", v.name, g, gbs);
+                std::fflush(stdout);
+            }
+        }
+    }
+    std::printf("}\n");
+    CHECK(hipHostUnregister(host));
+    munmap(host, bytes);
+    close(fd);
+    return 0;
+}

@@ -104,7 +104,7 @@ def child(tier: str, cpu: int | None = None) -> None:
 
                     out[f"breakdown_{s // 1024}k_{'put' if op else 'get'}"] = {
                         "call_us": round(t * 1e6, 3), "post_us": mean("post_us"), "wait_us": mean("wait_us"),
-                        "gpu_us": mean("gpu_us"), "doorbell": b1["doorbell"]}
+                        "gpu_us": mean("gpu_us"), "relaunches": b1["relaunches"]}
                     if int(os.environ.get("OCM_SERVICE_PROTO", "0")) & 16:
                         out[f"trace_{s // 1024}k_{'put' if op else 'get'}"] = [r for r in api.service_trace(32) if r]
             a.free()
