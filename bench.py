@@ -511,9 +511,19 @@ def main() -> int:
 
         elapsed, moved = ph.run("timed", timed)
 
+        # Self-diagnosis of the data path, per rank: peer access, IPC imports of
+        # other GPUs' HBM, and the transport that carried this rank's control records.
+        def rank_diag():
+            d = api.xgmi_diag() if use_gpu else {"device": -1, "peer_access": 0, "ipc_imports": 0, "ipc_failures": 0}
+            st, _ = _local(lambda: client.stats(rank))
+            d["ctrl"] = st["ctrl"] if st else None
+            d["remote_gpus"] = sorted({e["owner_gpu"] for e in info["extents"] if e["tier"] == api.OCM_TIER_GPU})
+            return d
+
+        diag, _ = _local(rank_diag)
         # max over ranks of elapsed, sum of bytes
         stats = gather_obj(dist, {"elapsed": elapsed, "moved": moved, "lat": lat_remote, "lat_local": lat_local,
-                                  "extents": info["extents"], "leases": leases}, world)
+                                  "extents": info["extents"], "leases": leases, "diag": diag}, world)
         t_max = max(s["elapsed"] for s in stats)
         total = sum(s["moved"] for s in stats)
 
@@ -545,6 +555,12 @@ def main() -> int:
 
         value = total / t_max / GiB
         tiers = sorted({e["tier"] for s in stats for e in s["extents"]})
+        diags = [s["diag"] or {} for s in stats]
+        # xGMI carried the sweep only if every rank's remote half sat in OTHER GPUs'
+        # HBM, imported over IPC with peer access: a fallback or a host tier is PCIe.
+        xgmi = bool(world > 1 and not fallback and tiers == [api.OCM_TIER_GPU] and all(
+            d.get("peer_access", 0) >= 1 and d.get("ipc_imports", 0) >= 1 and d.get("remote_gpus")
+            and d.get("device", -1) not in d["remote_gpus"] for d in diags))
         result = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -577,6 +593,8 @@ def main() -> int:
             "local_alloc_p50_us": round(max(s["lat_local"]["alloc_p50_us"] for s in stats), 2),
             "alloc_p50_us_per_rank": [round(s["lat"]["alloc_p50_us"], 2) for s in stats],
             "lease_allocs_per_rank": [s["leases"] for s in stats],
+            "xgmi": xgmi,
+            "ranks": diags,
             "sweep": sweep,
         }
         if tuned:

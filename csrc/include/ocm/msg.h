@@ -108,7 +108,7 @@ struct NodeConfig {
     uint16_t num_apps;
     uint8_t xgmi_peers;    // GPUs on the node this daemon's GPU reaches over xGMI
     uint8_t min_hops, max_hops;  // over those links (0 when none)
-    uint8_t pad0;
+    uint8_t ctrl;          // control transport (ocm_daemon_stats.ctrl_transport)
     uint32_t n_alloc, n_free, n_reclaimed, n_spilled, n_slabs;
     uint32_t ticks;        // allgather ticks of the control transport (0 on TCP)
     uint32_t n_leases;     // capacity leases this daemon holds on peers

@@ -133,6 +133,9 @@ struct ocm_daemon_stats {
     uint32_t xgmi_peers;   /* GPUs on the node this daemon's GPU reaches over xGMI */
     uint16_t min_hops;     /* xGMI hop count over those links (0 when none) */
     uint16_t max_hops;
+    uint32_t ctrl_transport; /* daemon<->daemon records: 0 TCP, 1 socket ticks, 2 RCCL ticks,
+                                3 TCP after leaving a tick transport, 4 tick transport starting */
+    uint32_t reserved;
 };
 
 ocm_alloc_t ocm_alloc_ex(ocm_alloc_param_t alloc_param, const struct ocm_alloc_ex_params *ex);

@@ -83,6 +83,7 @@ NodeConfig Daemon::my_config() const {
     c.n_spilled = (uint32_t)(gov_ ? gov_->spilled_count() : n_spilled_);
     c.n_slabs = (uint32_t)(arena_ ? arena_->num_slabs() : 0);
     c.ticks = (uint32_t)(tick_ ? tick_->ticks() : 0);
+    c.ctrl = !tick_ ? 0 : tick_left_ || tick_->failed() ? 3 : !tick_->up() ? 4 : std::strcmp(tick_->collective_name(), "rccl") == 0 ? 2 : 1;
     for (auto &l : leases_) c.n_leases += l != nullptr;
     c.lease_allocs = (uint32_t)n_lease_allocs_;
     return c;

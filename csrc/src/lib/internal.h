@@ -171,6 +171,10 @@ struct State {
     NodeConfig daemon{};
     int daemon_rank = 0;
     int device = -1;
+    // xGMI self-diagnosis (ocm_x_xgmi_diag): peers this device got access to at
+    // init, and slabs of OTHER GPUs' HBM imported / refused by hipIpcOpenMemHandle.
+    int peers_enabled = 0;
+    uint64_t ipc_peer_imports = 0, ipc_peer_failures = 0;
     hipStream_t stream = nullptr;
     uint64_t seq = 0;
     std::map<SlabKey, Mapping> imports;

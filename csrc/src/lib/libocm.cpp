@@ -70,6 +70,7 @@ int ocm_init(void) {
     int dev = g && *g ? std::atoi(g) : s.daemon.gpu;
     if (dev < 0 && ndev > 0 && s.daemon.gpu >= 0) dev = 0;
     s.device = (ndev > 0 && dev >= 0 && dev < ndev) ? dev : -1;
+    s.peers_enabled = 0;
     if (s.device >= 0) {
         DeviceGuard guard(s.device);
         if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) {
@@ -88,6 +89,8 @@ int ocm_init(void) {
             hipError_t pe = hipDeviceEnablePeerAccess(p, 0);
             if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
                 OCM_WARN("peer access %d -> %d: %s", s.device, p, hipGetErrorString(pe));
+            else
+                s.peers_enabled++;
             (void)hipGetLastError();
         }
     }
@@ -611,6 +614,70 @@ int ocm_x_extent_handle(ocm_alloc_t a, int i, uint8_t *out) {
     return 0;
 }
 
+// xGMI self-diagnosis of this process: {device, peers with access enabled,
+// other GPUs' HBM slabs imported, such imports refused}.
+void ocm_x_xgmi_diag(uint64_t out[4]) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    out[0] = (uint64_t)(int64_t)s.device;
+    out[1] = (uint64_t)s.peers_enabled;
+    out[2] = s.ipc_peer_imports;
+    out[3] = s.ipc_peer_failures;
+}
+
+// Where extent i lives inside its owner's slab: {offset in the slab, extent
+// bytes, slab bytes, owner GPU (-1: host tier)}. With ocm_x_extent_handle, a
+// process on the OWNER's GPU can map the same bytes (tests: owner-side kernels).
+int ocm_x_extent_region(ocm_alloc_t a, int i, uint64_t out[4]) {
+    if (!a || !out || i < 0 || (size_t)i >= a->ext.size()) return -1;
+    const Region &r = a->ext[(size_t)i].r;
+    out[0] = r.offset;
+    out[1] = r.bytes;
+    out[2] = r.slab_bytes;
+    out[3] = (uint64_t)(int64_t)r.owner_gpu;
+    return 0;
+}
+
+// Owner-side helpers that need no ocm_init (a verifier process on the owner's
+// GPU): open an exported HBM slab on `device`, and fill / check the word
+// pattern there with the same gfx950 kernels on that device's null stream.
+int ocm_x_ipc_open(int device, const uint8_t *handle, void **out) {
+    if (!handle || !out || hipSetDevice(device) != hipSuccess) return -1;
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, sizeof(h));
+    if (hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return 0;
+}
+
+int ocm_x_ipc_close(int device, void *p) {
+    if (hipSetDevice(device) != hipSuccess) return -1;
+    return hipIpcCloseMemHandle(p) == hipSuccess ? 0 : -1;
+}
+
+long long ocm_x_pattern_dev(int device, void *p, uint64_t words, uint64_t first, uint32_t seed, int check) {
+    if (!p || hipSetDevice(device) != hipSuccess) return -1;
+    unsigned long long *bad_dev = nullptr, bad = 0;
+    hipError_t e = hipSuccess;
+    if (check) {
+        e = hipMalloc(reinterpret_cast<void **>(&bad_dev), sizeof(bad));
+        if (e == hipSuccess) e = hipMemset(bad_dev, 0, sizeof(bad));
+        if (e == hipSuccess) e = pattern_check(p, words, first, seed, bad_dev, nullptr);
+        if (e == hipSuccess) e = hipMemcpy(&bad, bad_dev, sizeof(bad), hipMemcpyDeviceToHost);
+        if (bad_dev) (void)hipFree(bad_dev);
+    } else {
+        e = pattern_fill(p, words, first, seed, nullptr);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+    }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return (long long)bad;
+}
+
 void *ocm_remotebuf(ocm_alloc_t a) {
     if (!a || a->ext.size() != 1 || a->ext[0].net) return nullptr;
     return S().device >= 0 ? a->ext[0].dptr : a->ext[0].hptr;
@@ -646,6 +713,7 @@ int ocm_stats(int rank, struct ocm_daemon_stats *out) {
     out->xgmi_peers = c.xgmi_peers;
     out->min_hops = c.min_hops;
     out->max_hops = c.max_hops;
+    out->ctrl_transport = c.ctrl;
     return 0;
 }
 

@@ -152,7 +152,11 @@ int import_extent(Extent &e) {
             void *p = nullptr;
             // (the lazy-peer-access flag is mandatory: 0 is rejected as an invalid argument)
             hipError_t err = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-            if (err != hipSuccess) OCM_FAIL(-1, "hipIpcOpenMemHandle(owner %d slab %u): %s", r.owner_rank, r.slab_id, hipGetErrorString(err));
+            if (err != hipSuccess) {
+                if (r.owner_gpu != s.device) s.ipc_peer_failures++;
+                OCM_FAIL(-1, "hipIpcOpenMemHandle(owner %d slab %u): %s", r.owner_rank, r.slab_id, hipGetErrorString(err));
+            }
+            if (r.owner_gpu != s.device) s.ipc_peer_imports++;  // another GPU's HBM, reached over xGMI
             m.dbase = static_cast<char *>(p);
         } else {
             // The owner hands us the slab's memfd (SCM_RIGHTS); the /proc path in

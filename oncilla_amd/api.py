@@ -111,10 +111,18 @@ class OcmDaemonStats(ctypes.Structure):
         ("xgmi_peers", ctypes.c_uint32),
         ("min_hops", ctypes.c_uint16),
         ("max_hops", ctypes.c_uint16),
+        ("ctrl_transport", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
     ]
 
     def as_dict(self) -> dict:
-        return {name: getattr(self, name) for name, _ in self._fields_}
+        d = {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+        d["ctrl"] = CTRL_TRANSPORTS.get(d["ctrl_transport"], "unknown")
+        return d
+
+
+# ocm_daemon_stats.ctrl_transport
+CTRL_TRANSPORTS = {0: "tcp", 1: "socket", 2: "rccl", 3: "tcp (left ticks)", 4: "starting"}
 
 
 class OcmError(RuntimeError):
@@ -187,6 +195,11 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_batch": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, ctypes.POINTER(u64), i32, i32]),
             "ocm_x_link_info": (i32, [i32, i32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
             "ocm_x_extent_handle": (i32, [vp, i32, ctypes.c_char_p]),
+            "ocm_x_extent_region": (i32, [vp, i32, ctypes.POINTER(u64)]),
+            "ocm_x_xgmi_diag": (None, [ctypes.POINTER(u64)]),
+            "ocm_x_ipc_open": (i32, [i32, ctypes.c_char_p, ctypes.POINTER(vp)]),
+            "ocm_x_ipc_close": (i32, [i32, vp]),
+            "ocm_x_pattern_dev": (ctypes.c_longlong, [i32, vp, u64, u64, ctypes.c_uint32, i32]),
             "ocm_x_torch_pool_config": (None, [i32, ctypes.c_uint32]),
             "ocm_x_torch_pool_stats": (None, [ctypes.POINTER(u64)]),
         }
@@ -318,6 +331,15 @@ def counters() -> dict:
     return dict(zip(COUNTER_KEYS, [int(v) for v in out]))
 
 
+def xgmi_diag() -> dict:
+    """This process's xGMI self-diagnosis: its device, the peers it enabled access to,
+    and the other GPUs' HBM slabs it imported (or was refused) over IPC."""
+    out = (ctypes.c_uint64 * 4)()
+    load().ocm_x_xgmi_diag(out)
+    return {"device": ctypes.c_int64(out[0]).value, "peer_access": int(out[1]), "ipc_imports": int(out[2]),
+            "ipc_failures": int(out[3])}
+
+
 def quiesce() -> None:
     """Park this process's resident copy service now. Optional: the service
     leaves by itself OCM_SERVICE_IDLE_US (50 us) after its last op, so a
@@ -419,6 +441,15 @@ class Allocation:
         if self._c.lib.ocm_x_extent_handle(self.handle, i, buf) != 0:
             raise OcmError("ocm_x_extent_handle: no such extent")
         return buf.raw
+
+    def extent_region(self, i: int = 0) -> dict:
+        """Where extent i sits in its owner's slab (with extent_handle(i), a process on the
+        owner's GPU can map the same bytes: see owner_view())."""
+        out = (ctypes.c_uint64 * 4)()
+        if self._c.lib.ocm_x_extent_region(self.handle, i, out) != 0:
+            raise OcmError("ocm_x_extent_region: no such extent")
+        return {"offset": int(out[0]), "bytes": int(out[1]), "slab_bytes": int(out[2]),
+                "owner_gpu": ctypes.c_int64(out[3]).value}
 
     # --- data movement ---
     def onesided(self, op_flag: int, local_offset: int, remote_offset: int, nbytes: int, async_: bool = False) -> None:

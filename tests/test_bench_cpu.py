@@ -41,6 +41,10 @@ def test_bench_multi_rank(native, n):
     # the setup-time autotune ran its all-rank protocol and agreed on one pick per direction
     assert res["autotune"]["ranks"] == n and res["autotune"]["get"] in res["autotune"]["GiBps"], res["autotune"]
     assert len(res["alloc_p50_us_per_rank"]) == n
+    # self-diagnosis: every rank reports its data-path state and control transport;
+    # CPU ranks move no byte over xGMI, so the flag must say so
+    assert res["xgmi"] is False and len(res["ranks"]) == n, res.get("ranks")
+    assert all(d["ctrl"] in ("tcp", "socket", "rccl") and d["peer_access"] == 0 for d in res["ranks"]), res["ranks"]
     # control-plane extra: the same allocation path on TCP links and on socket-collective ticks
     cp = res["control_plane"]
     assert "alloc_p50_us" in cp["tcp"] and "alloc_p50_us" in cp["socket"], cp
@@ -135,3 +139,4 @@ def test_bench_falls_back_to_host_tier_when_peer_hbm_fails(native, phase):
     assert r.returncode == 0, r.stderr[-3000:]
     res = _last_json(r.stdout)
     assert res["value"] > 0 and res["fallback"]["phase"] == phase and list(res["fallback"]["rank_errors"]) == ["1"]
+    assert res["xgmi"] is False  # a fallback is never an xGMI number

@@ -82,6 +82,40 @@ def test_copy_service_small_ops_on_peer_hbm(mesh_factory, size):
         a.free()
 
 
+OWNER_SIZES = [4096, 256 << 10, 4 << 20, 16 << 20, 256 << 20]  # service (<= 4 MiB on peer HBM), then launches
+
+
+def owner_round_trips(c, owner_rank, size, rounds=3):
+    """a kernel on the OWNER's GPU verifies what the app put
+    (copy service for small ops, launches above), and writes what the app's next
+    get must return, with idle exits of the service in between."""
+    import time
+
+    from oncilla_amd.utils.owner_side import OwnerView
+
+    a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=size, remote_bytes=size, remote_rank=owner_rank)
+    try:
+        with OwnerView(a) as v:
+            for r in range(rounds):
+                a.fill(seed=500 + r, nbytes=size)
+                a.put(0, 0, size)
+                assert v.check(seed=500 + r, nbytes=size) == 0, f"owner GPU misses the app's put ({size} B, round {r})"
+                v.fill(seed=700 + r, nbytes=size)  # the owner's kernel rewrites the extent
+                a.get(0, 0, size)  # a resident service may hold lines of the old bytes: STRICT hand-off
+                assert a.check(seed=700 + r, nbytes=size) == 0, f"app get misses the owner's writes ({size} B, round {r})"
+                if r == 1:
+                    time.sleep(0.002)  # past the service's idle exit: the next op relaunches it
+    finally:
+        a.free()
+
+
+@pytest.mark.parametrize("size", OWNER_SIZES)
+def test_owner_gpu_sees_app_puts_and_app_gets_see_owner_writes(mesh_factory, size):
+    m = mesh_factory(2, gpus=[0, 1])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        owner_round_trips(c, 1, size)
+
+
 def test_fused_adam_with_state_in_peer_hbm(mesh_factory):
     """The fused remote-Adam kernel reads and writes the moments in another
     GPU's HBM over xGMI; results match torch.optim.Adam."""
@@ -139,25 +173,29 @@ def test_host_tier_of_another_gpus_daemon(mesh_factory):
 
 
 def test_bench_on_real_gpus():
-    """The driver's scaling launch on this box's GPUs (up to 4): one rank and one
-    daemon per physical GPU, striped over every peer, autotune over xGMI, the
-    per-peer table with link types, and the control-plane extra with RCCL
-    ticks between real ranks."""
+    """The driver's scaling launch on EVERY GPU of this box at the driver's config
+    (1 GiB max transfer): one rank and one daemon per physical GPU, striped over
+    every peer, autotune over xGMI, the per-peer table with link types, the
+    self-diagnosis fields (xgmi, peer access / IPC import per rank, control
+    transport per rank) and the control-plane extra with RCCL ticks."""
     import json
     import os
     import subprocess
     import sys
 
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    k = min(NDEV, 4)
+    k = min(NDEV, 8)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(k),
                         "--master-addr", "127.0.0.1", "--master-port", "29671", os.path.join(repo, "bench.py"),
-                        "--gpus", str(k), "--steps", "1", "--warmup", "1", "--max-bytes", str(64 << 20),
+                        "--gpus", str(k), "--steps", "1", "--warmup", "1", "--max-bytes", str(1 << 30),
                         "--alloc-samples", "50", "--no-characterize"],
-                       capture_output=True, text=True, timeout=600, cwd="/tmp")
+                       capture_output=True, text=True, timeout=900, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-4000:]
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert res["n_gpus"] == k and res["value"] > 0 and res["config"]["remote_tier"] == "hbm", res
+    assert res["xgmi"] is True and "fallback" not in res, res
+    diag = res["ranks"]
+    assert len(diag) == k and all(d["peer_access"] == k - 1 and d["ipc_imports"] >= k - 1 for d in diag), diag
     assert res["config"]["extents_per_pair"] == k - 1
     peers = res["peers_from_rank0"]
     assert sorted(peers) == [str(p) for p in range(1, k)], peers

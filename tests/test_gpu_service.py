@@ -192,6 +192,18 @@ def test_torch_pool_release_after_small_op_is_fast(mesh_factory):
         a.free()
 
 
+@pytest.mark.parametrize("size", [4096, 256 << 10, 4 << 20, 16 << 20, 128 << 20])
+def test_owner_side_kernel_round_trips_same_gpu(mesh_factory, size):
+    # The owner-side protocol of test_gpu_multi.py on the same-GPU stand-in (the
+    # owner daemon on this GPU, the owner view in a process of its own): a kernel
+    # there checks the app's puts and writes what the app's next get returns.
+    from test_gpu_multi import owner_round_trips
+
+    m = mesh_factory(2, gpus=[0, 0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        owner_round_trips(c, 1, size)
+
+
 def test_launch_after_service_ops_does_not_wait_for_the_service(mesh_factory, monkeypatch):
     # The persistent service must not share a hardware queue with the launch
     # streams: a launch queued behind it waits for its idle exit (2 ms here, so a
