@@ -529,13 +529,17 @@ def main() -> int:
 
         sweep = {}
         if not args.no_characterize:
-            ch = ph.run("characterize", lambda: wl.characterize(pair, sizes))
+            ch = ph.run("characterize", lambda: wl.characterize(pair, sizes, breakdown_max=(4 << 20) if use_gpu else 0))
             chs = gather_obj(dist, ch, world)
             for s in sizes:
                 g = max(c[s]["get_s"] for c in chs)
                 p = max(c[s]["put_s"] for c in chs)
                 sweep[str(s)] = {"get_GiBps": round(world * s / g / GiB, 3), "put_GiBps": round(world * s / p / GiB, 3),
                                  "get_us": round(g * 1e6, 2), "put_us": round(p * 1e6, 2)}
+                if chs[0][s].get("service"):
+                    # rank 0's copy-service breakdown per op (us): host post, GPU doorbell-seen
+                    # -> done, and the crossings (doorbell read + completion write over PCIe)
+                    sweep[str(s)]["service_rank0"] = chs[0][s]["service"]
         # ---- extras, after the timed region (never affect the metric) ----
         # Every rank reaches every collective below even when its local part
         # fails, so a failure is recorded instead of deadlocking the job.

@@ -51,7 +51,7 @@ struct DaemonConfig {
     bool zero_on_alloc = false;
     std::string ready_file;
     std::string bind_ip;             // default: 0.0.0.0
-    std::string ctrl = "tcp";        // daemon<->daemon records: tcp | rccl | socket (tick transports)
+    std::string ctrl = "auto";       // daemon<->daemon records: auto | tcp | rccl | socket (tick transports)
     int watch_pid = 0;               // exit when this process (the launcher) exits
     uint64_t lease_bytes = 1ull << 30;  // HBM leased per owner for local sub-allocation (0 = off)
     int lease_after = 2;             // normal placements on an owner before leasing there
@@ -199,13 +199,29 @@ private:
     void return_idle_leases();
     int preferred_owner() const;
     bool cross_host(int a, int b) const;
-    void start_tick(const uint8_t *id);
+    void start_tick(const uint8_t *id, bool rccl);
     // Leave the tick transport (it failed here, a peer died, or a peer left it):
     // abort it, re-send over TCP every record it cannot prove delivered, and tell
     // the peers once (MSG_TICK_STOP) so the whole mesh leaves it together instead
     // of an idle rank posting into a collective nobody else runs any more.
     void leave_tick(const char *why);
     bool tick_left_ = false;
+    // Control-plane bootstrap (n > 1). rank0 resolves --ctrl (auto: RCCL when the
+    // nodefile gives every rank a GPU of its own, else TCP) and tells each peer as
+    // soon as its link is up: MSG_TICK_START (u.raw = the ncclUniqueId, seq = the
+    // collective: 1 RCCL, 2 socket) or MSG_TICK_STOP (TCP). A peer defers its join
+    // (ADD_NODE, NODE_LINKS, OWNED) until its tick transport is up, so the join is
+    // the transport's first traffic, or until it is told TCP / gives up after
+    // OCM_TICK_UP_MS: then the join rides TCP.
+    std::string ctrl_mode_ = "tcp";     // rank0's resolved transport: tcp | rccl | socket
+    uint8_t tick_uid_[128] = {};
+    bool join_deferred_ = false;        // our join waits for the transport decision / the tick
+    long tick_deadline_ms_ = 0;         // bootstrap bound (0: none pending)
+    int tick_up_ms_ = 20000;            // OCM_TICK_UP_MS
+    void resolve_ctrl();                // rank0, at init
+    void send_ctrl_decision(int r);     // rank0 -> rank r, once its link is up
+    void join_now(const char *why);     // the deferred join, over whatever transport is up
+    void check_tick_bootstrap();        // deadlines, from the event loop
     void on_tick();
     void send_tcp(int r, Msg &m);
 

@@ -35,6 +35,9 @@ enum XferVariant : int {
     XFER_REG = 1,    // register-staged, 8 x 16 B loads in flight per lane
     XFER_LDS = 2,    // LDS-DMA (global_load_lds_dwordx4) staged, wave-private double buffer
     XFER_DMA = 3,    // no kernel: the runtime's copy engines, one hipMemcpyAsync per stripe segment
+                     // (a measured baseline: autotune reports it, never installs it)
+    XFER_PCIE = 4,   // PCIe streaming: 8 KiB tiles on a small grid (128), write-through stores to the
+                     // host tier; the default for pairs whose remote half is in the pinned host tier
 };
 
 struct XferTuning {

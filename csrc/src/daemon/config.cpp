@@ -35,7 +35,8 @@ static const char *kUsage =
     "  --slab-bytes B           HBM slab size (default 4G)                       [OCM_SLAB_BYTES]\n"
     "  --gpu-capacity B         HBM this daemon may hand out (default 75% free) [OCM_GPU_CAPACITY]\n"
     "  --host-capacity B        host-tier bytes (default 25% MemAvailable)      [OCM_HOST_CAPACITY]\n"
-    "  --ctrl tcp|rccl|socket   daemon<->daemon record transport               [OCM_CTRL]\n"
+    "  --ctrl auto|tcp|rccl|socket  daemon<->daemon record transport (auto: RCCL when every\n"
+    "                           rank has a GPU of its own, else TCP)            [OCM_CTRL]\n"
     "  --lease-bytes B          capacity lease chunk (0 = off, default 1G)      [OCM_LEASE_BYTES]\n"
     "  --state-file PATH        rank0 directory checkpoint (resume)            [OCM_STATE_FILE]\n"
     "  --host-alias NAME        node name to report (emulate several nodes)    [OCM_HOST_ALIAS]\n"
@@ -119,8 +120,8 @@ int parse_daemon_args(int argc, char **argv, DaemonConfig *cfg, std::string *err
             if (!val(&cfg->bind_ip)) return -1;
         } else if (a == "--ctrl") {
             if (!val(&cfg->ctrl)) return -1;
-            if (cfg->ctrl != "tcp" && cfg->ctrl != "rccl" && cfg->ctrl != "socket") {
-                *err = "--ctrl must be tcp, rccl or socket";
+            if (cfg->ctrl != "auto" && cfg->ctrl != "tcp" && cfg->ctrl != "rccl" && cfg->ctrl != "socket") {
+                *err = "--ctrl must be auto, tcp, rccl or socket";
                 return -1;
             }
         } else if (a == "--host-alias") {

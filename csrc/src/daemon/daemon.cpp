@@ -300,8 +300,17 @@ int Daemon::init() {
         conns_[fd] = std::move(c);
     }
     probe_links();
+    if (const char *v = std::getenv("OCM_TICK_UP_MS"); v && *v) tick_up_ms_ = std::max(1, std::atoi(v));
+    if (rank_ == 0) resolve_ctrl();
     // Join: report our configuration to rank0 (reference notify_rank0, src/main.c:143-160).
-    join_rank0();
+    // With a tick transport possible, a peer first waits for rank0's decision so that
+    // the join is the transport's first traffic (bounded by OCM_TICK_UP_MS).
+    if (n_ > 1 && rank_ != 0 && cfg_.ctrl != "tcp") {
+        join_deferred_ = true;
+        tick_deadline_ms_ = now_ms() + tick_up_ms_;
+    } else {
+        join_rank0();
+    }
     OCM_INFO("ocmd rank %d/%d up: gpu %d (%d visible, host tier on NUMA node %d), hbm capacity %.1f GiB, host tier %.1f GiB, policy %s, ns %s",
              rank_, n_, gpu_, num_gpu_, arena_->config().numa_node, (double)arena_->capacity(TIER_GPU) / (1 << 30),
              (double)arena_->capacity(TIER_HOST) / (1 << 30), policy_name(cfg_.policy), ns_.c_str());
@@ -314,20 +323,15 @@ void Daemon::check_ready() {
         if (!joined_[r]) return;
     ready_ = true;
     OCM_LOG("rank %d: mesh complete (%d nodes)", rank_, n_);
-    if (rank_ == 0 && cfg_.ctrl != "tcp" && !resumed_) {
-        // Bootstrap the tick transport (not after a resume: survivors stay on TCP): rank0 picks the RCCL id and tells everybody over TCP.
-        Msg t;
-        std::memset(&t, 0, sizeof(t));
-        t.type = MSG_TICK_START;
-        t.status = MSG_REQUEST;
-        t.rank = 0;
+    if (rank_ == 0 && n_ == 1 && (cfg_.ctrl == "rccl" || cfg_.ctrl == "socket") && !resumed_) {
+        // A single daemon only ticks when asked to (OCM_TICK_SELF tests: its own
+        // records through a 1-rank communicator); meshes bootstrap at link-up.
+        uint8_t uid[128] = {};
         std::string err;
-        if (cfg_.ctrl == "rccl" && rccl_unique_id(t.u.raw, &err) != 0) {
+        if (cfg_.ctrl == "rccl" && rccl_unique_id(uid, &err) != 0)
             OCM_WARN("rccl control plane unavailable (%s); staying on TCP", err.c_str());
-        } else {
-            for (int r = 1; r < n_; r++) send_tcp(r, t);
-            start_tick(t.u.raw);
-        }
+        else
+            start_tick(uid, cfg_.ctrl == "rccl");
     }
     if (!cfg_.ready_file.empty()) {
         std::string tmp = cfg_.ready_file + ".tmp";
@@ -406,6 +410,7 @@ int Daemon::loop() {
         int n = epoll_wait(ep_, evs, 64, (self_q_.empty() && !spinning) ? timeout : 0);
         if (n > 0 && spin_ns) last_event_ns = now_ns();
         sweep_timeouts();
+        check_tick_bootstrap();
         return_idle_leases();
         if (n < 0) {
             if (errno == EINTR) continue;

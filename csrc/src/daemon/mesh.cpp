@@ -94,6 +94,7 @@ void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
             it->second->peer_rank = m.src_rank;
             if (peer_fd_[m.src_rank] >= 0 && peer_fd_[m.src_rank] != from_fd) drop_conn(peer_fd_[m.src_rank]);
             peer_fd_[m.src_rank] = from_fd;
+            if (rank_ == 0 && m.src_rank != 0) send_ctrl_decision(m.src_rank);
         }
         break;
     }
@@ -166,13 +167,21 @@ void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
         }
         break;
     case MSG_TICK_START:
-        if (!tick_ && cfg_.ctrl != "tcp") start_tick(m.u.raw);
+        if (!tick_ && !tick_left_ && cfg_.ctrl != "tcp") {
+            start_tick(m.u.raw, m.seq == 1);
+            if (!tick_ && join_deferred_) join_now("this rank cannot run the chosen tick transport");
+        }
         break;
     case MSG_TICK_WAKE:
         if (tick_ && !tick_left_) tick_->wake_at(m.u.req.bytes);
         break;
     case MSG_TICK_STOP:
-        if (tick_) leave_tick("a peer left it");
+        if (tick_) {
+            leave_tick("a peer left it");
+        } else {
+            tick_left_ = true;  // rank0 chose TCP: ignore any later start
+            if (join_deferred_) join_now("rank0 chose TCP");
+        }
         break;
     case MSG_SHUTDOWN: stop_ = true; break;
     case MSG_PING:
@@ -740,12 +749,86 @@ void Daemon::sweep_timeouts() {
     }
 }
 
-void Daemon::start_tick(const uint8_t *id) {
+void Daemon::resolve_ctrl() {
+    ctrl_mode_ = "tcp";
+    if (n_ <= 1 || resumed_ || cfg_.ctrl == "tcp") {
+        if (resumed_ && cfg_.ctrl != "tcp") OCM_INFO("rank 0: resumed directory: control records stay on TCP");
+        return;
+    }
+    if (cfg_.ctrl == "rccl" || cfg_.ctrl == "socket") {
+        ctrl_mode_ = cfg_.ctrl;
+    } else {
+        // auto: RCCL when every rank has a GPU of its own (one rank per GPU, the
+        // layout RCCL requires). GPUs come from the nodefile's gpu= column; a
+        // rank without one on this host uses rank % visible GPUs, as it will.
+        std::set<std::pair<std::string, int>> seen;
+        bool own = gpu_ >= 0;
+        const std::string &my_ip = nf_.nodes[rank_].ip;
+        for (const NodeEntry &ne : nf_.nodes) {
+            int g = ne.gpu;
+            if (g < 0 && ne.ip == my_ip && num_gpu_ > 0) g = ne.rank % num_gpu_;
+            if (g < 0 || !seen.insert({ne.ip, g}).second) {
+                own = false;
+                break;
+            }
+        }
+        const char *sock = std::getenv("OCM_CTRL_AUTO_SOCKET");  // CPU meshes in tests: the socket ring instead
+        ctrl_mode_ = own ? "rccl" : (sock && std::strcmp(sock, "1") == 0) ? "socket" : "tcp";
+    }
+    if (ctrl_mode_ == "rccl") {
+        std::string err;
+        if (rccl_unique_id(tick_uid_, &err) != 0) {
+            OCM_WARN("rank 0: rccl control plane unavailable (%s); control records stay on TCP", err.c_str());
+            ctrl_mode_ = "tcp";
+        }
+    }
+    if (ctrl_mode_ != "tcp") tick_deadline_ms_ = now_ms() + tick_up_ms_;
+    OCM_INFO("rank 0: daemon<->daemon records: %s (--ctrl %s)", ctrl_mode_.c_str(), cfg_.ctrl.c_str());
+}
+
+void Daemon::send_ctrl_decision(int r) {
+    if (r <= 0 || r >= n_) return;
+    Msg t;
+    std::memset(&t, 0, sizeof(t));
+    t.status = MSG_REQUEST;
+    t.rank = 0;
+    if (ctrl_mode_ == "tcp" || tick_left_) {
+        t.type = MSG_TICK_STOP;
+    } else {
+        t.type = MSG_TICK_START;
+        t.seq = ctrl_mode_ == "rccl" ? 1 : 2;
+        std::memcpy(t.u.raw, tick_uid_, sizeof(tick_uid_));
+    }
+    send_tcp(r, t);
+    if (t.type == MSG_TICK_START && !tick_) start_tick(tick_uid_, ctrl_mode_ == "rccl");
+}
+
+void Daemon::join_now(const char *why) {
+    if (!join_deferred_) return;
+    join_deferred_ = false;
+    OCM_INFO("rank %d: joining rank0 (%s)", rank_, why);
+    join_rank0();
+}
+
+void Daemon::check_tick_bootstrap() {
+    if (!tick_deadline_ms_ || now_ms() < tick_deadline_ms_) return;
+    tick_deadline_ms_ = 0;
+    char why[96];
+    std::snprintf(why, sizeof(why), "not up within OCM_TICK_UP_MS=%d ms", tick_up_ms_);
+    if (tick_ && !tick_->up() && !tick_left_) {
+        leave_tick(why);  // the whole mesh falls back to TCP (MSG_TICK_STOP); a deferred join follows
+    } else if (!tick_ && join_deferred_) {
+        tick_left_ = true;  // no decision from rank0 in time: join over TCP, ignore a late start
+        join_now("no control-plane decision from rank0 in time");
+    }
+}
+
+void Daemon::start_tick(const uint8_t *id, bool rccl) {
     if (tick_) return;
     CollectiveFactory f;
-    if (cfg_.ctrl == "rccl") {
+    if (rccl) {
         if (gpu_ < 0) {
-            OCM_WARN("rank %d: --ctrl rccl needs a GPU; staying on TCP", rank_);
+            OCM_WARN("rank %d: the RCCL control plane needs a GPU; staying on TCP", rank_);
             return;
         }
         std::vector<uint8_t> uid(id, id + 128);
@@ -766,12 +849,16 @@ void Daemon::start_tick(const uint8_t *id) {
     if (pinned_cpus_) tick_->set_cpus(orig_cpus_);
     ep_add(tick_->event_fd(), EPOLLIN, tag(T_TICK, 0));
     tick_->start();
-    OCM_INFO("rank %d: control records will ride the %s tick transport", rank_, cfg_.ctrl.c_str());
+    OCM_INFO("rank %d: control records will ride the %s tick transport", rank_, rccl ? "rccl" : "socket");
 }
 
 void Daemon::on_tick() {
     if (!tick_) return;
     for (Msg &m : tick_->drain()) handle_mesh_msg(m, -1);
+    if (tick_->up() && tick_deadline_ms_) {
+        tick_deadline_ms_ = 0;
+        if (join_deferred_) join_now("tick transport up: the join is its first traffic");
+    }
     uint64_t t = 0;
     if (tick_->take_announce(&t)) {
         // Wake the peers for the tick this rank is starting from idle.
@@ -792,6 +879,8 @@ void Daemon::leave_tick(const char *why) {
     if (!tick_->failed()) tick_->abort();
     // send_rank: records to ourselves (OCM_TICK_SELF) go back to the local queue
     for (TickRecord &rec : tick_->take_unsent()) send_rank(rec.dest, rec.msg);
+    tick_deadline_ms_ = 0;
+    if (join_deferred_) join_now(why);
     if (tick_left_) return;
     tick_left_ = true;
     OCM_WARN("rank %d: leaving the %s tick transport (%s); control records ride TCP", rank_,

@@ -404,7 +404,14 @@ std::unique_ptr<Collective> make_rccl_collective(int gpu, int rank, int nranks, 
 }
 
 std::unique_ptr<Collective> make_socket_collective(const std::string &ns, int rank, int nranks, size_t slot_bytes,
-                                                   std::string *err, const std::atomic<bool> *) {
+                                                   std::string *err, const std::atomic<bool> *cancel) {
+    const char *tf = std::getenv("OCM_TICK_FAULT");
+    if (tf && std::strcmp(tf, "init_hang") == 0) {
+        // Test hook: a communicator that never comes up (a rank that never joins).
+        while (cancel && !cancel->load()) usleep(1000);
+        *err = "injected: the collective never came up (OCM_TICK_FAULT=init_hang)";
+        return nullptr;
+    }
     auto c = std::make_unique<SocketCollective>();
     if (c->init(ns, rank, nranks, slot_bytes, err) != 0) return nullptr;
     return c;

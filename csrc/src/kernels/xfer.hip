@@ -336,6 +336,65 @@ __global__ __launch_bounds__(kThreads) void xfer_lds_kernel(XferArgs a, XferDone
     xfer_publish(d);
 }
 
+// ---- PCIe streaming variant (host-tier extents) ----
+// Large ops between this GPU's HBM and the pinned host tier are bound by PCIe,
+// not by the CUs, and the 32 KiB-tile register kernel on a full-chip grid
+// stays at 54-55 GB/s. Measured over shapes (tools/pcie_stream_probe.hip,
+// profiles/pcie_stream_r03.json, 256 MiB, against hipMemcpyAsync at 56.8-57.1):
+//   get (host -> HBM): 2 loads in flight per lane and 128 workgroups reach
+//       57.4 GB/s; cache bits of either side change nothing; full-chip grids
+//       lose up to 2 GB/s (too many streams scatter the read window);
+//   put (HBM -> host): write-through (sc1) stores are the whole difference,
+//       57.0 against 55.5 GB/s with plain or nontemporal stores, flat from 48
+//       to 256 workgroups.
+// So: 8 KiB tiles (256 lanes x 16 B x 2), grid-strided over a small grid, and
+// sc1 stores when the destination is the host tier.
+constexpr int kPcieUnroll = 2;
+constexpr uint32_t kPcieTileShift = 13;  // 256 x 16 B x kPcieUnroll
+constexpr unsigned kPcieBlocksDefault = 128;
+
+template <int LA, int SA>
+__device__ __forceinline__ void span_copy_pcie(char *__restrict__ dst, const char *__restrict__ src, uint64_t n) {
+    const int tid = threadIdx.x;
+    uint64_t head = (16u - ((uintptr_t)dst & 15u)) & 15u;
+    if (head > n) head = n;
+    if ((uint64_t)tid < head) dst[tid] = src[tid];
+    dst += head;
+    src += head;
+    n -= head;
+    if (((uintptr_t)src & 15u) == 0) {
+        const uint32_t nv = (uint32_t)(n >> 4);  // a span is at most one tile
+        const __amdgpu_buffer_rsrc_t rs = span_rsrc(src, nv << 4);
+        const __amdgpu_buffer_rsrc_t rd = span_rsrc(dst, nv << 4);
+        for (uint32_t base = 0; base < nv; base += kThreads * kPcieUnroll) {
+            u32x4 v[kPcieUnroll];
+#pragma unroll
+            for (int k = 0; k < kPcieUnroll; k++)
+                v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((base + k * kThreads + tid) << 4), 0, LA);
+#pragma unroll
+            for (int k = 0; k < kPcieUnroll; k++)
+                __builtin_amdgcn_raw_buffer_store_b128(v[k], rd, (int)((base + k * kThreads + tid) << 4), 0, SA);
+        }
+        const uint64_t tail = n & 15u;
+        if ((uint64_t)tid < tail) dst[((uint64_t)nv << 4) + tid] = src[((uint64_t)nv << 4) + tid];
+    } else {
+        for (uint64_t i = tid; i < n; i += kThreads) dst[i] = src[i];
+    }
+}
+
+// SA: store bits (kAuxSC1 when the destination is the host tier).
+template <int SA>
+__global__ __launch_bounds__(kThreads) void xfer_pcie_kernel(XferArgs a, XferDone d) {
+    const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
+    const uint64_t first = a.rem_off & ~tile_mask;
+    const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;
+    for (uint64_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
+        TileSpan s = tile_span(a, ti, first);
+        span_copy_pcie<kAuxNT, SA>(s.dst, s.src, s.n);
+    }
+    xfer_publish(d);
+}
+
 int env_int(const char *k, int dflt) {
     const char *v = std::getenv(k);
     return (v && *v) ? std::atoi(v) : dflt;
@@ -360,6 +419,7 @@ XferTuning xfer_tuning_from_env() {
     const char *v = std::getenv("OCM_XFER_VARIANT");
     if (v && (!std::strcmp(v, "lds") || !std::strcmp(v, "2"))) t.variant = XFER_LDS;
     if (v && (!std::strcmp(v, "reg") || !std::strcmp(v, "1"))) t.variant = XFER_REG;
+    if (v && (!std::strcmp(v, "pcie") || !std::strcmp(v, "4"))) t.variant = XFER_PCIE;
     t.max_blocks = env_int("OCM_XFER_BLOCKS", 0);
     t.nontemporal = env_int("OCM_XFER_NT", 1) != 0;
     return t;
@@ -383,13 +443,27 @@ hipError_t xfer_launch(const XferArgs &in, const XferTuning &t, hipStream_t stre
     const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - (a.rem_off & ~tile_mask)) >> a.tile_shift;
     int variant = t.variant;
     if (variant == XFER_AUTO) variant = XFER_REG;
+    const XferDone d0 = done ? *done : XferDone{};
+    if (variant == XFER_PCIE) {
+        if (a.tile_shift > kPcieTileShift) a.tile_shift = kPcieTileShift;
+        const uint64_t mask = (1ull << a.tile_shift) - 1;
+        const uint64_t tiles = (((a.rem_off + a.len + mask) & ~mask) - (a.rem_off & ~mask)) >> a.tile_shift;
+        const uint64_t cap = t.max_blocks > 0 ? (uint64_t)t.max_blocks : (uint64_t)kPcieBlocksDefault;
+        const unsigned g = (unsigned)(tiles < cap ? tiles : cap);
+        // sc1 (write-through) stores into the host tier, plain ones into HBM
+        if (a.put && t.nontemporal)
+            hipLaunchKernelGGL(xfer_pcie_kernel<kAuxSC1>, dim3(g), dim3(kThreads), 0, stream, a, d0);
+        else
+            hipLaunchKernelGGL(xfer_pcie_kernel<0>, dim3(g), dim3(kThreads), 0, stream, a, d0);
+        return hipGetLastError();
+    }
     if (a.tile_shift != kTileShift) variant = XFER_REG;  // LDS path is built for 32 KiB tiles
     // Grid caps from the round-1 sweep (profiles/ksweep_r01.json): LDS-DMA
     // peaks at 4 blocks per CU (2 resident, 64 KiB LDS each), the register
     // path at 2 per CU; never more blocks than tiles.
     int cap = t.max_blocks > 0 ? t.max_blocks : num_cus() * (variant == XFER_LDS ? 4 : 2);
     const unsigned grid = (unsigned)(ntiles < (uint64_t)cap ? ntiles : (uint64_t)cap);
-    const XferDone d = done ? *done : XferDone{};
+    const XferDone d = d0;
     if (variant == XFER_LDS) {
         if (t.nontemporal)
             hipLaunchKernelGGL(xfer_lds_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a, d);

@@ -183,8 +183,10 @@ struct State {
     // Per-direction override ([0] get, [1] put) for one-sided kernel ops,
     // set by an autotune (variant XFER_AUTO: use `tuning`).
     XferTuning dir_tuning[2];
-    bool host_engine_kernel = false;
-    uint64_t host_kernel_max = 0;  // measured: SDMA beats the kernel on registered host slabs
+    // Host-tier pairs: the PCIe streaming kernel (default), or with OCM_HOST_ENGINE=sdma
+    // the runtime's copy engines above host_kernel_max (the measured baseline).
+    bool host_engine_kernel = true;
+    uint64_t host_kernel_max = 0;
     int sync_mode = 0;             // 0 stream sync, 1 spin on an event, 2 blocking event sync
     OpCounters ctr;
     // persistent copy service (small blocking one-sided ops)

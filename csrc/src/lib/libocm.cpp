@@ -131,7 +131,7 @@ int ocm_init(void) {
     s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
     s.tuning = xfer_tuning_from_env();
     const char *he = std::getenv("OCM_HOST_ENGINE");
-    s.host_engine_kernel = he && !std::strcmp(he, "kernel");
+    s.host_engine_kernel = !(he && !std::strcmp(he, "sdma"));  // the PCIe streaming kernel unless asked for SDMA
     if (he && !std::strcmp(he, "sdma")) s.host_kernel_max = 0;
     if (const char *hk = std::getenv("OCM_HOST_KERNEL_MAX")) s.host_kernel_max = std::strtoull(hk, nullptr, 0);
     s.inited = true;

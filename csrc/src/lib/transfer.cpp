@@ -368,8 +368,11 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     }
     DeviceGuard guard(s.device);
     const bool lin_dev = lloc == LOC_DEVICE;
-    // HBM extents: always the kernel. Host-tier extents: the kernel below
-    // host_kernel_max (lower latency), the DMA engines above (higher peak).
+    // Every extent kind goes through the repo's own kernels: HBM extents the
+    // register / LDS-DMA kernels, host-tier extents the PCIe streaming kernel
+    // (57.0-57.4 GB/s, at or above the runtime's copy at 56.8-57.1:
+    // profiles/pcie_stream_r03.json). OCM_HOST_ENGINE=sdma keeps the runtime's
+    // copy engines for host-tier pairs as a measured baseline.
     const XferTuning &dt = s.dir_tuning[put ? 1 : 0];
     const bool dma_pick = (dt.variant != XFER_AUTO ? dt.variant : s.tuning.variant) == XFER_DMA;
     const bool use_kernel =
@@ -403,9 +406,10 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     hipStream_t st = async ? lane_stream(a) : s.stream;
     if (honor_dep(a, st, false) != 0) return -1;
     if (use_kernel) {
-        // A/B: no resident poller during the copy; and without a queue of its own
-        // the service would hold this launch until its idle exit.
-        if (s.svc_park_kernel && len > s.svc_limit(a)) service_park();
+        // No resident poller during a large copy over PCIe (its doorbell reads share
+        // the link) or when asked (A/B); without a queue of its own the service
+        // would also hold this launch until its idle exit.
+        if ((s.svc_park_kernel || !a->any_gpu) && len > s.svc_limit(a)) service_park();
         before_launch();
         XferArgs x;
         std::memset(&x, 0, sizeof(x));
@@ -427,7 +431,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
             // over xGMI, host-mapped memory, huge copies) uses the register path.
             bool same_gpu = lloc == LOC_DEVICE;
             for (auto &e : a->ext) same_gpu &= e.r.tier == TIER_GPU && e.r.owner_gpu == s.device;
-            t.variant = (same_gpu && len <= (256ull << 20)) ? XFER_LDS : XFER_REG;
+            t.variant = !a->any_gpu ? XFER_PCIE : (same_gpu && len <= (256ull << 20)) ? XFER_LDS : XFER_REG;
         }
         XferDone dn;
         if (done && async && len <= s.launch_flag_max && s.launch_flags && s.lane_flags && st != s.stream &&

@@ -361,6 +361,28 @@ def service_stats() -> dict:
             "gpu_us": out[3] / 100.0 / n if n else None, "relaunches": int(out[4])}
 
 
+def service_totals() -> dict:
+    """Raw cumulative copy-service counters (diff two snapshots for a breakdown)."""
+    out = (ctypes.c_uint64 * 5)()
+    load().ocm_x_service_stats(out)
+    return {"ops": int(out[0]), "ns_post": int(out[1]), "ns_wait": int(out[2]), "gpu_ticks": int(out[3]),
+            "relaunches": int(out[4])}
+
+
+def service_breakdown(before: dict, after: dict) -> Optional[dict]:
+    """Per-op means between two service_totals() snapshots: host time to post the
+    request, GPU time from doorbell seen to completion published, and the rest of
+    the host's wait (the two PCIe crossings: doorbell read, completion write)."""
+    n = after["ops"] - before["ops"]
+    if n <= 0:
+        return None
+    post = (after["ns_post"] - before["ns_post"]) / n / 1e3
+    wait = (after["ns_wait"] - before["ns_wait"]) / n / 1e3
+    gpu = (after["gpu_ticks"] - before["gpu_ticks"]) / n / 100.0
+    return {"ops": n, "post_us": round(post, 3), "gpu_us": round(gpu, 3), "crossings_us": round(wait - gpu, 3),
+            "relaunches": after["relaunches"] - before["relaunches"]}
+
+
 def service_trace(n_wgs: int = 32) -> list:
     """Copy-service phase stamps of the last request, per workgroup (needs the TRACE bit,
     16, in OCM_SERVICE_PROTO): microseconds of [seen, copy start, drained, counted/done]

@@ -59,24 +59,36 @@ def rw_sweep_step(alloc: api.Allocation, sizes: Iterable[int]) -> int:
     return moved
 
 
-def characterize(alloc: api.Allocation, sizes: Iterable[int], target_s: float = 0.02, max_iters: int = 200) -> dict:
-    """Per-size put/get seconds per op (timed in C, no Python in the loop)."""
+def characterize(alloc: api.Allocation, sizes: Iterable[int], target_s: float = 0.02, max_iters: int = 200,
+                 breakdown_max: int = 0) -> dict:
+    """Per-size put/get seconds per op (timed in C, no Python in the loop). For sizes up
+    to `breakdown_max` on a GPU, also the copy service's per-op breakdown of each
+    direction (api.service_breakdown: host post, GPU doorbell-seen -> done, crossings)."""
     out = {}
     for s in sizes:
         probe = alloc.time_onesided(1, s, 1)
         iters = max(1, min(max_iters, int(target_s / max(probe, 1e-7))))
+        bd = s <= breakdown_max
+        b0 = api.service_totals() if bd else None
         t_get = alloc.time_onesided(0, s, iters)
+        b1 = api.service_totals() if bd else None
         t_put = alloc.time_onesided(1, s, iters)
         out[s] = {"get_s": t_get, "put_s": t_put, "iters": iters}
+        if bd:
+            b2 = api.service_totals()
+            out[s]["service"] = {"get": api.service_breakdown(b0, b1), "put": api.service_breakdown(b1, b2)}
     return out
 
 
 # Configurations an autotune chooses from: (variant 0 auto / 1 register kernel /
-# 2 LDS-DMA kernel / 3 the runtime's copy engines, grid cap 0 = default,
-# nontemporal destination stores).
+# 2 LDS-DMA kernel / 3 the runtime's copy engines / 4 PCIe streaming kernel,
+# grid cap 0 = default, nontemporal destination stores).
 TUNING_CANDIDATES = {"auto": (0, 0, 1), "reg_b256": (1, 256, 1), "reg_b1024": (1, 1024, 1),
                      "reg_b2048": (1, 2048, 1), "reg_nt0": (1, 0, 0), "lds_default": (2, 0, 1),
                      "lds_b512": (2, 512, 1), "dma": (3, 0, 1)}
+# Measured and reported, never installed: the runtime's copy engines are the
+# comparison baseline for the repo's own kernels (SURVEY §7.2), not a data path.
+BASELINE_ONLY = frozenset({"dma"})
 
 
 def autotune(alloc: api.Allocation, nbytes: int, reps: int = 3, gather=None, candidates: dict | None = None) -> dict:
@@ -89,11 +101,13 @@ def autotune(alloc: api.Allocation, nbytes: int, reps: int = 3, gather=None, can
     links, and a candidate's time is the slowest rank's. A candidate that
     fails on any rank is out. The fastest per direction is installed with
     `api.set_tuning_dir`; "auto" (the library default) is always a candidate,
-    so the choice is never slower than the default as measured. Overwrites the
-    first `nbytes` of both halves.
+    so the choice is never slower than the default as measured. Baseline
+    candidates (BASELINE_ONLY: the runtime's copy engines) are timed and
+    reported but never installed. Overwrites the first `nbytes` of both halves.
     """
     cands = dict(candidates or TUNING_CANDIDATES)
     cands.setdefault("auto", (0, 0, 1))
+    baselines = {n for n in cands if n in BASELINE_ONLY}
     gather = gather or (lambda obj: [obj])
     table = {}
     for name, (variant, blocks, nt) in cands.items():
@@ -117,13 +131,13 @@ def autotune(alloc: api.Allocation, nbytes: int, reps: int = 3, gather=None, can
         table[name] = row
     best = {}
     for op, key in ((0, "get"), (1, "put")):
-        ok = {n: r[key]["s"] for n, r in table.items() if "s" in r[key]}
+        ok = {n: r[key]["s"] for n, r in table.items() if "s" in r[key] and n not in baselines}
         pick = min(ok, key=ok.get) if ok else "auto"
         variant, blocks, nt = cands[pick]
         api.set_tuning_dir(op, variant, blocks, bool(nt))
         best[key] = pick
     ranks = len(gather(None))
-    return {"get": best["get"], "put": best["put"], "bytes": nbytes, "ranks": ranks,
+    return {"get": best["get"], "put": best["put"], "bytes": nbytes, "ranks": ranks, "baselines": sorted(baselines),
             "GiBps": {n: {k: (round(ranks * nbytes / v["s"] / (1 << 30), 2) if "s" in v else v)
                           for k, v in r.items()} for n, r in table.items()}}
 

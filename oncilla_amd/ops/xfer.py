@@ -10,7 +10,7 @@ import ctypes
 
 from .. import api
 
-XFER_AUTO, XFER_REG, XFER_LDS = 0, 1, 2
+XFER_AUTO, XFER_REG, XFER_LDS, XFER_PCIE = 0, 1, 2, 4
 
 
 def _ptr(t) -> int:

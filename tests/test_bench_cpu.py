@@ -140,3 +140,24 @@ def test_bench_falls_back_to_host_tier_when_peer_hbm_fails(native, phase):
     res = _last_json(r.stdout)
     assert res["value"] > 0 and res["fallback"]["phase"] == phase and list(res["fallback"]["rank_errors"]) == ["1"]
     assert res["xgmi"] is False  # a fallback is never an xGMI number
+
+
+def test_autotune_never_installs_the_dma_baseline(native, monkeypatch):
+    """the runtime's copy engines stay a reported baseline. Even when
+    "dma" is the fastest candidate, a kernel configuration is installed."""
+    from oncilla_amd import api
+    from oncilla_amd.models import workloads as wl
+
+    cur = {}
+    monkeypatch.setattr(api, "set_tuning_dir", lambda op, v, b, nt: cur.__setitem__(op, (v, b, nt)))
+    cands = {"auto": (0, 0, 1), "reg_b256": (1, 256, 1), "dma": (3, 0, 1)}
+    secs = {(0, 0, 1): 2e-4, (1, 256, 1): 1.5e-4, (3, 0, 1): 1e-4}
+
+    class FakePair:
+        def time_onesided(self, op, n, iters):
+            return secs[cur[op]]
+
+    r = wl.autotune(FakePair(), 1 << 20, candidates=cands)
+    assert r["get"] == "reg_b256" and r["put"] == "reg_b256", r
+    assert r["baselines"] == ["dma"] and r["GiBps"]["dma"]["get"] > r["GiBps"]["reg_b256"]["get"], r
+    assert cur[0] == (1, 256, 1) and cur[1] == (1, 256, 1)

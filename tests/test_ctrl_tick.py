@@ -159,3 +159,68 @@ def test_rccl_tick_single_gpu(mesh_factory, monkeypatch):
             a.free()
         assert c.stats(0)["ctrl_ticks"] > before
     assert "rccl tick transport" in m.logs()
+
+
+def _ctrl(c, n):
+    return [c.stats(r)["ctrl"] for r in range(n)]
+
+
+def test_ctrl_auto_without_gpus_stays_on_tcp(mesh_factory):
+    """--ctrl auto (the default): RCCL needs a GPU per rank; CPU daemons keep TCP
+    and never start a tick transport."""
+    m = mesh_factory(3)
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20, flags=api.OCM_ALLOC_STRIPE)
+        a.free()
+        assert _ctrl(c, 3) == ["tcp"] * 3
+        assert all(c.stats(r)["ctrl_ticks"] == 0 for r in range(3))
+    assert "daemon<->daemon records: tcp (--ctrl auto)" in m.logs()
+
+
+@pytest.mark.parametrize("sealed", ["0", "1"])
+def test_ctrl_auto_eight_ranks_join_over_the_ticks(mesh_factory, sealed):
+    """--ctrl auto with the CPU stand-in for RCCL (OCM_CTRL_AUTO_SOCKET): rank0
+    starts the transport as each link comes up, every peer's join (ADD_NODE,
+    NODE_LINKS) is the transport's first traffic, and the 8-rank mesh then
+    carries striped allocations on it."""
+    m = mesh_factory(8, env={"OCM_CTRL_AUTO_SOCKET": "1", "OCM_TICK_SOCKET_SEAL": sealed})
+    with api.Client(daemon_rank=3, ns=m.ns) as c:
+        assert _ctrl(c, 8) == ["socket"] * 8
+        t0 = [c.stats(r)["ctrl_ticks"] for r in range(8)]
+        assert all(t > 0 for t in t0), t0  # the joins ticked before any app traffic
+        for i in range(4):
+            a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=(7 << 20) + 5, remote_bytes=(7 << 20) + 5,
+                        flags=api.OCM_ALLOC_STRIPE)
+            assert len(a.remote_info()["extents"]) == 7
+            a.fill(seed=80 + i)
+            a.put(0, 0, 7 << 20)
+            a.fill(seed=0)
+            a.get(0, 0, 7 << 20)
+            assert a.check(seed=80 + i, nbytes=7 << 20) == 0
+            a.free()
+    logs = m.logs()
+    assert logs.count("joining rank0 (tick transport up") == 7, logs
+    assert "falling back to TCP" not in logs and "leaving the" not in logs
+
+
+def test_ctrl_auto_falls_back_to_tcp_when_the_transport_never_comes_up(mesh_factory):
+    """A communicator that never forms (OCM_TICK_FAULT=init_hang): after
+    OCM_TICK_UP_MS every rank leaves the transport, the deferred joins ride TCP,
+    and the mesh serves allocations."""
+    import time
+
+    t0 = time.time()
+    m = mesh_factory(4, env={"OCM_CTRL_AUTO_SOCKET": "1", "OCM_TICK_FAULT": "init_hang", "OCM_TICK_UP_MS": "400"})
+    assert time.time() - t0 < 30
+    with api.Client(daemon_rank=2, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20, flags=api.OCM_ALLOC_STRIPE)
+        a.fill(seed=9)
+        a.put(0, 0, 1 << 20)
+        a.fill(seed=0)
+        a.get(0, 0, 1 << 20)
+        assert a.check(seed=9) == 0
+        a.free()
+        assert _ctrl(c, 4) == ["tcp (left ticks)"] * 4
+        assert all(c.stats(r)["ctrl_ticks"] == 0 for r in range(4))
+    logs = m.logs()
+    assert "not up within OCM_TICK_UP_MS=400 ms" in logs, logs

@@ -15,7 +15,7 @@ def _rand(n, seed):
     return torch.randint(0, 256, (n,), dtype=torch.uint8, generator=g).to(DEV)
 
 
-@pytest.mark.parametrize("variant", [ops.XFER_REG, ops.XFER_LDS])
+@pytest.mark.parametrize("variant", [ops.XFER_REG, ops.XFER_LDS, ops.XFER_PCIE])
 @pytest.mark.parametrize("n,soff,doff", [(1, 0, 0), (15, 1, 0), (16, 0, 0), (17, 3, 3), (4095, 0, 7),
                                          (32768, 0, 0), (32769, 16, 32), (1 << 20, 5, 9), ((8 << 20) + 48, 0, 0),
                                          ((64 << 20) + 4, 4, 4)])
@@ -29,7 +29,7 @@ def test_device_copy_matches_torch(variant, n, soff, doff):
     assert torch.equal(dst, ref)
 
 
-@pytest.mark.parametrize("variant", [ops.XFER_REG, ops.XFER_LDS])
+@pytest.mark.parametrize("variant", [ops.XFER_REG, ops.XFER_LDS, ops.XFER_PCIE])
 @pytest.mark.parametrize("n_ext,unit", [(2, 4096), (3, 65536), (7, 1 << 20), (8, 32768)])
 @pytest.mark.parametrize("put", [True, False])
 def test_striped_matches_reference(variant, n_ext, unit, put):
@@ -42,6 +42,26 @@ def test_striped_matches_reference(variant, n_ext, unit, put):
     lin_ref = lin.clone()
     ops.striped_reference(lin_ref, exts_ref, unit, rem_off, nbytes, put)
     ops.xfer(lin, exts, unit, rem_off, nbytes, put=put, variant=variant)
+    torch.cuda.synchronize()
+    assert torch.equal(lin, lin_ref)
+    for a, b in zip(exts, exts_ref):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("put", [True, False])
+@pytest.mark.parametrize("n_ext,unit", [(1, 0), (3, 4096), (2, 1 << 20)])
+def test_pcie_kernel_on_pinned_host_memory(put, n_ext, unit):
+    # The host-tier path: extents in pinned host memory, the linear side in HBM,
+    # write-through stores into the host on puts. Byte-exact against torch.
+    total = (n_ext * max(unit, 1 << 20) * 3) + 4099
+    rem_off, nbytes = 4096 + 5, total - 8192
+    ext_len = (rem_off + nbytes) // n_ext + 2 * max(unit, 4096) if n_ext > 1 else rem_off + nbytes + 64
+    exts = [_rand(ext_len, 300 + i).cpu().pin_memory() for i in range(n_ext)]
+    lin = _rand(nbytes + 64, 8)
+    exts_ref = [e.clone() for e in exts]
+    lin_ref = lin.clone()
+    ops.striped_reference(lin_ref, exts_ref, unit if n_ext > 1 else 1, rem_off, nbytes, put)
+    ops.xfer(lin, exts, unit, rem_off, nbytes, put=put, variant=ops.XFER_PCIE)
     torch.cuda.synchronize()
     assert torch.equal(lin, lin_ref)
     for a, b in zip(exts, exts_ref):

@@ -172,23 +172,21 @@ def test_torch_pool_release_after_small_op_is_fast(mesh_factory):
     m = mesh_factory(2, gpus=[0, 0])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=4096, flags=api.OCM_ALLOC_HOST_TIER)
-        pool = RemoteMemPool(c, remote_rank=1)
         best = 1.0
-        for i in range(5):
+        for i in range(3):
+            pool = RemoteMemPool(c, remote_rank=1)
             with pool:
                 t = torch.full((1 << 20,), float(i), device="cuda:0")
             assert float(t[-1]) == float(i)
-            del t
-            gc.collect()
+            del t, pool
+            gc.collect()  # torch now holds the pool's block only until empty_cache
             a.put(0, 0, 4096)
             a.put(0, 0, 4096)  # served by the resident service
             t0 = time.perf_counter()
             torch.cuda.empty_cache()  # hands the block back: ocm_torch_free
             best = min(best, time.perf_counter() - t0)
-        assert RemoteMemPool.stats()["blocks"] == 0
+            assert RemoteMemPool.stats()["blocks"] == 0
         assert best < 1e-3, f"releasing a pool block after a small op took {best * 1e3:.2f} ms"
-        del pool
-        gc.collect()
         a.free()
 
 

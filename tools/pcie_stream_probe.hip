@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -78,18 +79,40 @@ struct Variant {
 };
 
 #define V(L, U, LA, SA) {#L "/u" #U "/la" #LA "/sa" #SA, stream_kernel<L, U, LA, SA>}
-static const Variant kVariants[] = {
-    V(0, 1, 2, 2), V(0, 2, 2, 2), V(0, 4, 2, 2), V(0, 8, 2, 2),
-    V(0, 1, 0, 0), V(0, 2, 0, 0), V(0, 4, 0, 0), V(0, 8, 0, 0),
-    V(0, 4, 17, 2), V(0, 4, 2, 0), V(0, 4, 17, 0), V(0, 4, 0, 2),
-    V(1, 1, 2, 2), V(1, 2, 2, 2), V(1, 4, 2, 2), V(1, 8, 2, 2),
-    V(1, 1, 0, 0), V(1, 4, 0, 0), V(1, 4, 17, 2),
-};
+#define VSA(L, U, LA) V(L, U, LA, 0), V(L, U, LA, 1), V(L, U, LA, 2), V(L, U, LA, 3), V(L, U, LA, 16), V(L, U, LA, 17)
+#define VLA(L, U) VSA(L, U, 0), VSA(L, U, 2), VSA(L, U, 17)
+static const Variant kVariants[] = {VLA(0, 1), VLA(0, 2), VLA(0, 4), VLA(1, 1), VLA(1, 2), VLA(1, 4)};
+#undef VLA
+#undef VSA
 #undef V
 
 int main(int argc, char **argv) {
     const uint64_t bytes = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : (256ull << 20);
     const int reps = argc > 2 ? std::atoi(argv[2]) : 4;
+    // argv[3]: directions "get", "put" or "both"; argv[4]: comma-separated grids (default
+    // cus/2 .. 8 cus); argv[5]: comma-separated name filters (a variant runs if its name
+    // contains one of them; default all)
+    const std::string dirs = argc > 3 ? argv[3] : "both";
+    std::vector<int> grid_list;
+    std::vector<std::string> filters;
+    if (argc > 4) {
+        std::string g = argv[4];
+        for (size_t i = 0; i < g.size();) {
+            size_t j = g.find(',', i);
+            if (j == std::string::npos) j = g.size();
+            grid_list.push_back(std::atoi(g.substr(i, j - i).c_str()));
+            i = j + 1;
+        }
+    }
+    if (argc > 5) {
+        std::string f = argv[5];
+        for (size_t i = 0; i < f.size();) {
+            size_t j = f.find(',', i);
+            if (j == std::string::npos) j = f.size();
+            filters.push_back(f.substr(i, j - i));
+            i = j + 1;
+        }
+    }
     if (bytes == 0 || bytes > (1ull << 30) || (bytes & 4095)) {
         std::fprintf(stderr, "bytes must be a multiple of 4 KiB in (0, 1 GiB]\n");
         return 2;
@@ -154,6 +177,7 @@ int main(int argc, char **argv) {
 
     std::printf("{\"bytes\": %llu, \"cus\": %d", (unsigned long long)bytes, cus);
     for (int dir = 0; dir < 2; dir++) {
+        if ((dir == 0 && dirs == "put") || (dir == 1 && dirs == "get")) continue;
         char *dst = (char *)(dir ? hdev : dev);
         const char *src = (const char *)(dir ? dev : hdev);
         prep(dir);
@@ -163,9 +187,12 @@ int main(int argc, char **argv) {
         verify(dir, "blit");
         std::printf(", \"%s/blit\": %.2f", dir ? "put" : "get", blit);
         std::fflush(stdout);
-        const int grids[] = {cus / 2, cus, 2 * cus, 4 * cus, 8 * cus};
+        if (grid_list.empty()) grid_list = {cus / 2, cus, 2 * cus, 4 * cus, 8 * cus};
         for (const Variant &v : kVariants) {
-            for (int g : grids) {
+            bool want = filters.empty();
+            for (const std::string &f : filters) want |= std::string(v.name).find(f) != std::string::npos;
+            if (!want) continue;
+            for (int g : grid_list) {
                 prep(dir);
                 const double gbs = timeit([&] {
                     hipLaunchKernelGGL(v.fn, dim3(g), dim3(kThreads), 0, st, dst, src, (uint32_t)bytes);
