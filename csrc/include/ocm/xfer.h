@@ -38,6 +38,8 @@ enum XferVariant : int {
                      // (a measured baseline: autotune reports it, never installs it)
     XFER_PCIE = 4,   // PCIe streaming: 8 KiB tiles on a small grid (128), write-through stores to the
                      // host tier; the default for pairs whose remote half is in the pinned host tier
+    XFER_PUSH = 5,   // gets only: a kernel on each OWNER's GPU reads its extents (local HBM) and
+                     // writes the app's local half over xGMI (remote writes instead of remote reads)
 };
 
 struct XferTuning {
@@ -63,6 +65,11 @@ hipError_t xfer_normalize(XferArgs &a);
 
 // Launch one transfer on `stream`. Returns hipSuccess or the launch error.
 hipError_t xfer_launch(const XferArgs &a, const XferTuning &t, hipStream_t stream, const XferDone *done = nullptr);
+
+// Push-based get: the tiles of the extents in `ext_mask` (bit i: extent i), launched on
+// the current device (the owner of those extents); a.ext[i] must be addresses valid
+// there for the masked extents, a.lin an address of the app's buffer valid there too.
+hipError_t xfer_push_launch(const XferArgs &a, uint32_t ext_mask, int max_blocks, hipStream_t stream);
 
 // Plain device copy dst <- src (both device-accessible), via the same kernel.
 hipError_t xfer_copy(void *dst, const void *src, uint64_t bytes, const XferTuning &t, hipStream_t stream);

@@ -395,6 +395,27 @@ __global__ __launch_bounds__(kThreads) void xfer_pcie_kernel(XferArgs a, XferDon
     xfer_publish(d);
 }
 
+// ---- push-based get ----
+// Launched on an owner's GPU: tiles of the extents in `mask` only (the other
+// owners' launches take the rest); loads from this GPU's HBM, nontemporal
+// stores into the app's buffer on another GPU over xGMI.
+__global__ __launch_bounds__(kThreads) void xfer_push_kernel(XferArgs a, uint32_t mask) {
+    const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
+    const uint64_t first = a.rem_off & ~tile_mask;
+    const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;
+    const uint64_t r0 = a.rem_off;
+    for (uint64_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
+        if (a.n_ext > 1) {
+            const uint64_t lo = first + (ti << a.tile_shift);
+            const uint64_t ts = lo > r0 ? lo : r0;
+            const uint32_t e = (uint32_t)(ts >> a.unit_shift) % a.n_ext;
+            if (!((mask >> e) & 1u)) continue;  // workgroup-uniform
+        }
+        TileSpan s = tile_span(a, ti, first);
+        span_copy<ST_NT>(s.dst, s.src, s.n);
+    }
+}
+
 int env_int(const char *k, int dflt) {
     const char *v = std::getenv(k);
     return (v && *v) ? std::atoi(v) : dflt;
@@ -420,6 +441,7 @@ XferTuning xfer_tuning_from_env() {
     if (v && (!std::strcmp(v, "lds") || !std::strcmp(v, "2"))) t.variant = XFER_LDS;
     if (v && (!std::strcmp(v, "reg") || !std::strcmp(v, "1"))) t.variant = XFER_REG;
     if (v && (!std::strcmp(v, "pcie") || !std::strcmp(v, "4"))) t.variant = XFER_PCIE;
+    if (v && (!std::strcmp(v, "push") || !std::strcmp(v, "5"))) t.variant = XFER_PUSH;
     t.max_blocks = env_int("OCM_XFER_BLOCKS", 0);
     t.nontemporal = env_int("OCM_XFER_NT", 1) != 0;
     return t;
@@ -475,6 +497,20 @@ hipError_t xfer_launch(const XferArgs &in, const XferTuning &t, hipStream_t stre
         else
             hipLaunchKernelGGL(xfer_reg_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a, d);
     }
+    return hipGetLastError();
+}
+
+hipError_t xfer_push_launch(const XferArgs &in, uint32_t ext_mask, int max_blocks, hipStream_t stream) {
+    if (in.len == 0 || ext_mask == 0) return hipSuccess;
+    XferArgs a = in;
+    if (a.put || xfer_normalize(a) != hipSuccess) return hipErrorInvalidValue;
+    const uint64_t mask = (1ull << a.tile_shift) - 1;
+    const uint64_t tiles = (((a.rem_off + a.len + mask) & ~mask) - (a.rem_off & ~mask)) >> a.tile_shift;
+    const uint32_t mine = (uint32_t)__builtin_popcount(ext_mask & ((1u << a.n_ext) - 1));
+    const uint64_t own = a.n_ext > 1 ? (tiles * mine + a.n_ext - 1) / a.n_ext : tiles;
+    const uint64_t cap = max_blocks > 0 ? (uint64_t)max_blocks : (uint64_t)num_cus() * 2;
+    const unsigned g = (unsigned)(own < cap ? (own ? own : 1) : cap);
+    hipLaunchKernelGGL(xfer_push_kernel, dim3(g), dim3(kThreads), 0, stream, a, ext_mask);
     return hipGetLastError();
 }
 

@@ -160,6 +160,16 @@ struct Mapping {
     int refs = 0;
     bool dedicated = false;
     bool registered = false;
+    // HBM slabs: the same slab opened on OTHER devices of this process (push-based
+    // gets launch on the owner's GPU and need an address valid there).
+    std::map<int, char *> dev_views;
+};
+
+// Push-based gets: one stream per owner device this process launches on.
+struct PushDev {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    bool ready = false;
 };
 
 struct State {
@@ -266,6 +276,9 @@ struct State {
     uint64_t rpc_spin_ns = 50000;          // OCM_RPC_SPIN_US: poll for a reply this long before sleeping
     uint64_t pinned_keep = 2ull << 30;     // idle pinned chunks kept for reuse
     class PinnedArena *pinned = nullptr;   // created on first use
+    std::map<int, PushDev> push;           // XFER_PUSH: owner device -> its stream
+    hipEvent_t push_order = nullptr;       // the app stream's position the push launches wait for
+    uint64_t push_launches = 0;
 };
 
 State &S();
@@ -362,6 +375,12 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
 // Wait for a kernel-published flag (>= val), with the runtime event as the backstop.
 int wait_done(const XferDone &d, hipEvent_t ev);
 int copy_local(void *dst, Loc dl, const void *src, Loc sl, size_t n);
+// Push-based get (XFER_PUSH): launches on every owner's GPU, ordered after the work
+// queued on `st`; blocking ops wait on the host, async ones make `st` wait.
+int push_get(lib_alloc *a, char *lin, uint64_t rem_off, uint64_t len, hipStream_t st, bool async);
+void push_release();
+// An address of extent e valid on device `dev` (its owner's GPU), opening its slab there once.
+char *extent_view(const Extent &e, int dev);
 
 // ---- batches (batch.cpp)
 int run_batch(lib_alloc *a, XferBatchArgs &args, std::vector<XferBatchOp> &v, bool async);

@@ -148,8 +148,14 @@ int ocm_tini(void) {
     for (auto *a : left) ocm_free(a);
     Msg d = new_msg(MSG_DISCONNECT);
     s.chan.send(&d, kMsgBytes, 1000);
+    push_release();
     for (auto &kv : s.imports) {
         Mapping &m = kv.second;
+        for (auto &v : m.dev_views) {
+            DeviceGuard gv(v.first);
+            (void)hipIpcCloseMemHandle(v.second);
+        }
+        m.dev_views.clear();
         DeviceGuard g(s.device);
         if (kv.first.tier == TIER_GPU && m.dbase) (void)hipIpcCloseMemHandle(m.dbase);
         if (m.registered) (void)hipHostUnregister(m.hbase);
@@ -615,14 +621,15 @@ int ocm_x_extent_handle(ocm_alloc_t a, int i, uint8_t *out) {
 }
 
 // xGMI self-diagnosis of this process: {device, peers with access enabled,
-// other GPUs' HBM slabs imported, such imports refused}.
-void ocm_x_xgmi_diag(uint64_t out[4]) {
+// other GPUs' HBM slabs imported, such imports refused, push-get launches}.
+void ocm_x_xgmi_diag(uint64_t out[5]) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     out[0] = (uint64_t)(int64_t)s.device;
     out[1] = (uint64_t)s.peers_enabled;
     out[2] = s.ipc_peer_imports;
     out[3] = s.ipc_peer_failures;
+    out[4] = s.push_launches;
 }
 
 // Where extent i lives inside its owner's slab: {offset in the slab, extent
@@ -911,7 +918,7 @@ void ocm_x_set_tuning(int variant, int blocks, int nt) {
 // winner of an autotune over the xGMI links; variant 0 clears it.
 int ocm_x_set_tuning_dir(int dir, int variant, int blocks, int nt) {
     if (dir != 0 && dir != 1) return -1;
-    if (variant < XFER_AUTO || variant > XFER_DMA || blocks < 0) return -1;
+    if (variant < XFER_AUTO || variant > XFER_PUSH || blocks < 0) return -1;
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     XferTuning t;
@@ -963,7 +970,14 @@ int ocm_x_xfer(int device, void *lin, void **ext, int n_ext, uint64_t unit, uint
     XferTuning t = xfer_tuning_from_env();
     if (variant) t.variant = variant;
     if (blocks) t.max_blocks = blocks;
-    if (xfer_launch(x, t, nullptr) != hipSuccess) return -1;
+    if (t.variant == XFER_PUSH && !put) {
+        // the push-get kernel, every extent in the mask (numerics tests); the
+        // same kernel a push get launches on each owner's GPU
+        const uint32_t all = (uint32_t)((1ull << n_ext) - 1);
+        if (xfer_push_launch(x, all, blocks, nullptr) != hipSuccess) return -1;
+    } else if (xfer_launch(x, t, nullptr) != hipSuccess) {
+        return -1;
+    }
     if (!sync) return 0;  // caller orders it on the null stream
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }

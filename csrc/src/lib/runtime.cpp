@@ -113,6 +113,16 @@ void close_fd_chans() {
     s.fd_chans.clear();
 }
 
+namespace {
+void close_views(Mapping &m) {
+    for (auto &kv : m.dev_views) {
+        DeviceGuard g(kv.first);
+        (void)hipIpcCloseMemHandle(kv.second);
+    }
+    m.dev_views.clear();
+}
+}  // namespace
+
 int import_extent(Extent &e) {
     State &s = S();
     const Region &r = e.r;
@@ -133,6 +143,10 @@ int import_extent(Extent &e) {
     if (it != s.imports.end() && std::memcmp(it->second.handle, r.handle, kHandleBytes) != 0) {
         // Same id, different export: the owner restarted. Drop the stale mapping.
         Mapping &m = it->second;
+        if (!m.dev_views.empty()) {
+            push_release();
+            close_views(m);
+        }
         if (r.tier == TIER_GPU && m.dbase) (void)hipIpcCloseMemHandle(m.dbase);
         if (m.registered) (void)hipHostUnregister(m.hbase);
         if (m.hbase) munmap(m.hbase, m.bytes);
@@ -200,6 +214,33 @@ int import_extent(Extent &e) {
     return 0;
 }
 
+char *extent_view(const Extent &e, int dev) {
+    State &s = S();
+    if (e.net || e.r.tier != TIER_GPU) return nullptr;
+    if (dev == s.device) return e.dptr;
+    auto it = s.imports.find(SlabKey{e.r.owner_rank, e.r.tier, e.r.slab_id});
+    if (it == s.imports.end()) return nullptr;
+    Mapping &m = it->second;
+    auto v = m.dev_views.find(dev);
+    if (v == m.dev_views.end()) {
+        // A second import of the slab, by this process's context on `dev`: HIP allows
+        // one open per device context, and it maps the slab into that device's
+        // address space (the first import mapped it for s.device only).
+        DeviceGuard g(dev);
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, m.handle, sizeof(h));
+        void *p = nullptr;
+        const hipError_t err = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (err != hipSuccess) {
+            (void)hipGetLastError();
+            OCM_FAIL(nullptr, "hipIpcOpenMemHandle on device %d (owner %d slab %u): %s", dev, e.r.owner_rank,
+                     e.r.slab_id, hipGetErrorString(err));
+        }
+        v = m.dev_views.emplace(dev, static_cast<char *>(p)).first;
+    }
+    return v->second + e.r.offset;
+}
+
 void release_extent(const Extent &e, bool force) {
     State &s = S();
     if (e.net) return;
@@ -209,6 +250,10 @@ void release_extent(const Extent &e, bool force) {
     Mapping &m = it->second;
     if (--m.refs > 0 && !force) return;
     if (!m.dedicated && !force) return;  // shared slabs stay mapped for reuse
+    if (!m.dev_views.empty()) {
+        push_release();  // no push launch may still read a view we close
+        close_views(m);
+    }
     DeviceGuard g(s.device);
     if (e.r.tier == TIER_GPU && m.dbase) (void)hipIpcCloseMemHandle(m.dbase);
     if (m.registered) (void)hipHostUnregister(m.hbase);

@@ -405,6 +405,22 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
     if (!async && wait_alloc(a) != 0) return -1;
     hipStream_t st = async ? lane_stream(a) : s.stream;
     if (honor_dep(a, st, false) != 0) return -1;
+    const XferTuning &getdt = s.dir_tuning[0];
+    if (use_kernel && !put && a->all_gpu && !a->any_net &&
+        (getdt.variant != XFER_AUTO ? getdt.variant : s.tuning.variant) == XFER_PUSH) {
+        before_launch();
+        if (push_get(a, lin, rem_off, len, st, async) != 0) return -1;
+        if (async) {
+            if (st != s.stream && a->ev) {
+                err = hipEventRecord(a->ev, st);
+                if (err != hipSuccess) OCM_FAIL(-1, "event record failed: %s", hipGetErrorString(err));
+            } else if (a->ev == nullptr && sync_stream() != 0) {
+                return -1;
+            }
+            a->async_pending = a->ev != nullptr;
+        }
+        return 0;
+    }
     if (use_kernel) {
         // No resident poller during a large copy over PCIe (its doorbell reads share
         // the link) or when asked (A/B); without a queue of its own the service
@@ -481,6 +497,92 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         return 0;
     }
     return sync_stream();
+}
+
+// ---- push-based get (XFER_PUSH) ----
+// RDMA READ vs WRITE (reference src/rdma.c:240-263): over xGMI a remote write is
+// usually cheaper than a remote read, so a get can be turned into pushes. For
+// every owner GPU d of the pair's extents, this process launches a kernel on d
+// (a stream of its own there) that reads d's extents from d's HBM and stores
+// them into the local half over xGMI. The owner's CPU and daemon take no part.
+// Needs: the slab mapped on d (extent_view: a second IPC open by d's context),
+// peer access d -> this GPU and, for a pool-allocated local half, pool access
+// for d (local_pool() grants it to every peer at creation).
+
+void push_release() {
+    State &s = S();
+    for (auto &kv : s.push) {
+        DeviceGuard g(kv.first);
+        if (kv.second.stream) (void)hipStreamSynchronize(kv.second.stream);
+    }
+}
+
+static PushDev *push_dev(int d) {
+    State &s = S();
+    PushDev &p = s.push[d];
+    if (p.ready) return &p;
+    DeviceGuard g(d);
+    if (d != s.device) {
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, d, s.device) != hipSuccess || !can)
+            OCM_FAIL(nullptr, "push get: GPU %d cannot reach GPU %d", d, s.device);
+        const hipError_t pe = hipDeviceEnablePeerAccess(s.device, 0);
+        if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
+            OCM_FAIL(nullptr, "push get: peer access %d -> %d: %s", d, s.device, hipGetErrorString(pe));
+        (void)hipGetLastError();
+    }
+    if (!p.stream && hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking) != hipSuccess)
+        OCM_FAIL(nullptr, "push get: no stream on GPU %d", d);
+    if (!p.done && hipEventCreateWithFlags(&p.done, hipEventDisableTiming) != hipSuccess)
+        OCM_FAIL(nullptr, "push get: no event on GPU %d", d);
+    p.ready = true;
+    return &p;
+}
+
+int push_get(lib_alloc *a, char *lin, uint64_t rem_off, uint64_t len, hipStream_t st, bool async) {
+    State &s = S();
+    if (!a->all_gpu || a->any_net) OCM_FAIL(-1, "push get needs every extent in a GPU's HBM");
+    std::map<int, uint32_t> owners;  // device -> extent mask
+    for (size_t i = 0; i < a->ext.size(); i++) {
+        const int d = a->ext[i].r.owner_gpu;
+        if (d < 0) OCM_FAIL(-1, "push get: extent %zu has no owner GPU", i);
+        owners[d] |= 1u << i;
+    }
+    DeviceGuard g(s.device);
+    if (!s.push_order && hipEventCreateWithFlags(&s.push_order, hipEventDisableTiming) != hipSuccess)
+        OCM_FAIL(-1, "push get: no event");
+    if (hipEventRecord(s.push_order, st) != hipSuccess) OCM_FAIL(-1, "push get: ordering event");
+    std::vector<PushDev *> used;
+    for (auto &kv : owners) {
+        const int d = kv.first;
+        PushDev *p = push_dev(d);
+        if (!p) return -1;
+        XferArgs x;
+        std::memset(&x, 0, sizeof(x));
+        x.lin = lin;  // the local half: peer-accessible from d (peer access + pool access)
+        for (size_t i = 0; i < a->ext.size(); i++) {
+            if (!((kv.second >> i) & 1u)) continue;
+            x.ext[i] = extent_view(a->ext[i], d);
+            if (!x.ext[i]) return -1;
+        }
+        x.n_ext = (uint32_t)a->ext.size();
+        x.rem_off = rem_off;
+        x.len = len;
+        x.put = 0;
+        if (x.n_ext > 1) x.unit_shift = (uint32_t)log2_exact(a->stripe_unit);
+        DeviceGuard gd(d);
+        hipError_t e = hipStreamWaitEvent(p->stream, s.push_order, 0);  // after the work queued before this op
+        if (e == hipSuccess) e = xfer_push_launch(x, kv.second, s.dir_tuning[0].max_blocks, p->stream);
+        if (e == hipSuccess) e = hipEventRecord(p->done, p->stream);
+        if (e != hipSuccess) OCM_FAIL(-1, "push get on GPU %d: %s", d, hipGetErrorString(e));
+        used.push_back(p);
+        s.push_launches++;
+    }
+    for (PushDev *p : used) {
+        const hipError_t e = async ? hipStreamWaitEvent(st, p->done, 0) : hipEventSynchronize(p->done);
+        if (e != hipSuccess) OCM_FAIL(-1, "push get completion: %s", hipGetErrorString(e));
+    }
+    return 0;
 }
 
 // Copy between two process-local buffers.

@@ -333,11 +333,12 @@ def counters() -> dict:
 
 def xgmi_diag() -> dict:
     """This process's xGMI self-diagnosis: its device, the peers it enabled access to,
-    and the other GPUs' HBM slabs it imported (or was refused) over IPC."""
-    out = (ctypes.c_uint64 * 4)()
+    and the other GPUs' HBM slabs it imported (or was refused) over IPC, and how many
+    push-get kernels it launched on owners' GPUs."""
+    out = (ctypes.c_uint64 * 5)()
     load().ocm_x_xgmi_diag(out)
     return {"device": ctypes.c_int64(out[0]).value, "peer_access": int(out[1]), "ipc_imports": int(out[2]),
-            "ipc_failures": int(out[3])}
+            "ipc_failures": int(out[3]), "push_launches": int(out[4])}
 
 
 def quiesce() -> None:

@@ -81,11 +81,12 @@ def characterize(alloc: api.Allocation, sizes: Iterable[int], target_s: float = 
 
 
 # Configurations an autotune chooses from: (variant 0 auto / 1 register kernel /
-# 2 LDS-DMA kernel / 3 the runtime's copy engines / 4 PCIe streaming kernel,
-# grid cap 0 = default, nontemporal destination stores).
+# 2 LDS-DMA kernel / 3 the runtime's copy engines / 4 PCIe streaming kernel /
+# 5 push-based get (kernels on the owners' GPUs write into the local half; puts
+# fall back to auto), grid cap 0 = default, nontemporal destination stores).
 TUNING_CANDIDATES = {"auto": (0, 0, 1), "reg_b256": (1, 256, 1), "reg_b1024": (1, 1024, 1),
                      "reg_b2048": (1, 2048, 1), "reg_nt0": (1, 0, 0), "lds_default": (2, 0, 1),
-                     "lds_b512": (2, 512, 1), "dma": (3, 0, 1)}
+                     "lds_b512": (2, 512, 1), "push": (5, 0, 1), "push_b1024": (5, 1024, 1), "dma": (3, 0, 1)}
 # Measured and reported, never installed: the runtime's copy engines are the
 # comparison baseline for the repo's own kernels, not a data path.
 BASELINE_ONLY = frozenset({"dma"})

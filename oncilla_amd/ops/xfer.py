@@ -10,7 +10,7 @@ import ctypes
 
 from .. import api
 
-XFER_AUTO, XFER_REG, XFER_LDS, XFER_PCIE = 0, 1, 2, 4
+XFER_AUTO, XFER_REG, XFER_LDS, XFER_PCIE, XFER_PUSH = 0, 1, 2, 4, 5
 
 
 def _ptr(t) -> int:

@@ -48,6 +48,23 @@ def test_striped_matches_reference(variant, n_ext, unit, put):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("n_ext,unit", [(1, 0), (2, 4096), (3, 65536), (7, 1 << 20), (8, 32768)])
+def test_push_get_kernel_matches_reference(n_ext, unit):
+    # The push-get kernel (XFER_PUSH) with every extent in its mask: byte-exact
+    # against the torch oracle, striped or not, unaligned offsets included.
+    total = max(n_ext, 1) * max(unit, 65536) * 5 + 12345
+    rem_off, nbytes = (unit // 2 + 3) if n_ext > 1 else 5, total - max(unit, 4096) - 100
+    ext_len = ((rem_off + nbytes) // max(unit, 1) // n_ext + 2) * unit if n_ext > 1 else rem_off + nbytes + 64
+    exts = [_rand(ext_len, 500 + i) for i in range(n_ext)]
+    lin = _rand(nbytes + 64, 9)
+    exts_ref = [e.clone() for e in exts]
+    lin_ref = lin.clone()
+    ops.striped_reference(lin_ref, exts_ref, unit if n_ext > 1 else 1, rem_off, nbytes, False)
+    ops.xfer(lin, exts, unit, rem_off, nbytes, put=False, variant=ops.XFER_PUSH)
+    torch.cuda.synchronize()
+    assert torch.equal(lin, lin_ref)
+
+
 @pytest.mark.parametrize("put", [True, False])
 @pytest.mark.parametrize("n_ext,unit", [(1, 0), (3, 4096), (2, 1 << 20)])
 def test_pcie_kernel_on_pinned_host_memory(put, n_ext, unit):

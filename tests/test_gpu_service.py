@@ -190,6 +190,37 @@ def test_torch_pool_release_after_small_op_is_fast(mesh_factory):
         a.free()
 
 
+def test_push_get_through_the_library_same_gpu(mesh_factory):
+    # XFER_PUSH installed for gets (what autotune can pick on a multi-GPU node):
+    # blocking and async gets above the service size launch on the owner's GPU
+    # (here the same one) and still return the right bytes, ordered after the
+    # puts queued before them; puts keep the default path.
+    m = mesh_factory(3, gpus=[0, 0, 0], policy="stripe")
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 192 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_STRIPE)
+        assert len(a.remote_info()["extents"]) == 2
+        api.set_tuning_dir(0, 5, 0, True)
+        try:
+            before = api.xgmi_diag()["push_launches"]
+            for i in range(3):
+                a.fill(seed=900 + i)
+                a.put(0, 0, n)
+                a.fill(seed=0)
+                a.get(0, 0, n)
+                assert a.check(seed=900 + i) == 0, f"blocking push get, round {i}"
+                a.fill(seed=950 + i)
+                a.put(0, 0, n, async_=True)
+                a.fill(seed=0)
+                a.get(0, 0, n, async_=True)  # queued behind the async put on the allocation's lane
+                a.wait()
+                assert a.check(seed=950 + i) == 0, f"async push get, round {i}"
+            assert api.xgmi_diag()["push_launches"] - before >= 6  # one launch per owner GPU and get
+        finally:
+            api.set_tuning_dir(0, 0, 0, True)
+        a.free()
+
+
 @pytest.mark.parametrize("size", [4096, 256 << 10, 4 << 20, 16 << 20, 128 << 20])
 def test_owner_side_kernel_round_trips_same_gpu(mesh_factory, size):
     # The owner-side protocol of test_gpu_multi.py on the same-GPU stand-in (the
