@@ -420,10 +420,17 @@ def main() -> int:
         # ---- p50 ocm_alloc latency (remote pair, and the local malloc path) ----
         def latency(flags):
             def run():
+                st0, _ = _local(lambda: client.stats(rank))
                 lat_remote = wl.alloc_latency(client, remote_kind, args.alloc_samples, local_bytes=64 << 10,
                                               remote_bytes=1 << 20, flags=flags)
+                st1, _ = _local(lambda: client.stats(rank))
                 lat_local = wl.alloc_latency(client, api.OCM_LOCAL_HOST, args.alloc_samples, local_bytes=1 << 20)
-                leases, _ = _local(lambda: client.stats()["lease_allocs"])
+                leases = st1["lease_allocs"] if st1 else None
+                if st0 and st1:
+                    # How the remote allocations were served: carved from a capacity lease
+                    # (no daemon<->daemon record) or through the mesh on the control transport.
+                    lat_remote["via"] = {"lease": st1["lease_allocs"] - st0["lease_allocs"],
+                                         "ctrl": st1["ctrl"], "ctrl_ticks": st1["ctrl_ticks"] - st0["ctrl_ticks"]}
                 return lat_remote, lat_local, leases
 
             return run
@@ -597,6 +604,7 @@ def main() -> int:
             "local_alloc_p50_us": round(max(s["lat_local"]["alloc_p50_us"] for s in stats), 2),
             "alloc_p50_us_per_rank": [round(s["lat"]["alloc_p50_us"], 2) for s in stats],
             "lease_allocs_per_rank": [s["leases"] for s in stats],
+            "alloc_via_per_rank": [s["lat"].get("via") for s in stats],
             "xgmi": xgmi,
             "ranks": diags,
             "sweep": sweep,
