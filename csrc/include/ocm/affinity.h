@@ -45,5 +45,8 @@ std::vector<int> core_siblings(int cpu);
 // Returns the CPUs pinned to (empty: not pinned); logs the choice under OCM_VERBOSE.
 enum class PinRole { Daemon, App };
 std::vector<int> pin_near_gpu(const std::string &bus_id, int gpu_ordinal, PinRole role, int daemon_rank);
+// The CPUs pin_near_gpu would pick for `role` (App: the complex's cores other than
+// the daemon's), without pinning anything; empty if the topology is unknown.
+std::vector<int> near_gpu_cpus(const std::string &bus_id, int gpu_ordinal, PinRole role, int daemon_rank);
 
 }  // namespace ocm

@@ -263,7 +263,8 @@ private:
     uint64_t n_alloc_ = 0, n_free_ = 0, n_reclaimed_ = 0, n_spilled_ = 0;
     // checkpoint / resume
     uint64_t boot_id_ = 0;               // this process lifetime
-    std::vector<int> orig_cpus_;         // the process's mask before the event loop was pinned (tick thread)
+    std::vector<int> orig_cpus_;         // the process's mask before the event loop was pinned
+    std::vector<int> near_cpus_;         // the GPU's L3 complex minus the event loop's core (tick thread)
     size_t pinned_cpus_ = 0;             // event loop restricted to this many CPUs near the GPU (0: not pinned)
     SipKey mesh_key_{};                  // HELLO MAC key (namespace + OCM_MESH_KEY)
     std::unordered_map<uint64_t, uint64_t> hello_seen_;  // nonce -> ts_ms of HELLOs accepted in the window

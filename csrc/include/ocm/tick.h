@@ -65,7 +65,27 @@ struct TickRing {
     uint64_t published;               // records appended so far (host, release)
     uint64_t pad[15];
     TickRecord rec[kTickRing];        // record j lives at rec[j % kTickRing]
+    uint64_t tag[kTickRing];          // tick_record_tag(rec j, j), stored after the record
 };
+constexpr int kTickRecordWords = (int)(sizeof(TickRecord) / sizeof(uint64_t));  // 21
+static_assert(sizeof(TickRecord) % sizeof(uint64_t) == 0, "tick records are whole words");
+
+// Hash of record j's words and its ring index. The seal kernel loads `published`,
+// the next records and their tags in ONE round trip over PCIe; a record read
+// before the host finished writing it (or left from an earlier lap of the ring)
+// fails this check, and the kernel reads it again once `published` is known.
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint64_t tick_record_tag(const uint64_t *w, uint64_t j) {
+    uint64_t h = (j + 1) * 0x9E3779B97F4A7C15ull;
+    for (int k = 0; k < kTickRecordWords; k++) {
+        h ^= w[k] + 0x632BE59BD9B4E019ull * (uint64_t)(k + 1);
+        h *= 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 29;
+    }
+    return h;
+}
 
 // Queue the seal of one tick on `stream`: *consumed (device memory, only this
 // stream touches it) -> slot->first, up to kTickMsgs records of `ring` -> slot.

@@ -122,12 +122,8 @@ std::vector<int> core_siblings(int cpu) {
     return parse_cpulist(list);
 }
 
-std::vector<int> pin_near_gpu(const std::string &bus_id, int gpu_ordinal, PinRole role, int daemon_rank) {
+std::vector<int> near_gpu_cpus(const std::string &bus_id, int gpu_ordinal, PinRole role, int daemon_rank) {
     const char *e = std::getenv("OCM_PIN");
-    if (e && std::strcmp(e, "0") == 0) return {};
-    // Apps opt in: their calling thread's mask would be inherited by everything
-    // the application starts later (ADVICE r02).
-    if (role == PinRole::App && (!e || !*e)) return {};
     const bool whole_ccd = e && std::strcmp(e, "ccd") == 0;  // everyone on the whole complex
     const int node = pci_numa_node(bus_id);
     std::vector<int> ccd = ccd_cpus(node, gpu_ordinal);
@@ -154,10 +150,22 @@ std::vector<int> pin_near_gpu(const std::string &bus_id, int gpu_ordinal, PinRol
             if (std::find(dsib.begin(), dsib.end(), c) == dsib.end()) cpus.push_back(c);
         if (cpus.empty()) cpus = ccd;
     }
+    return cpus;
+}
+
+std::vector<int> pin_near_gpu(const std::string &bus_id, int gpu_ordinal, PinRole role, int daemon_rank) {
+    const char *e = std::getenv("OCM_PIN");
+    if (e && std::strcmp(e, "0") == 0) return {};
+    // Apps opt in: their calling thread's mask would be inherited by everything
+    // the application starts later (ADVICE r02).
+    if (role == PinRole::App && (!e || !*e)) return {};
+    std::vector<int> cpus = near_gpu_cpus(bus_id, gpu_ordinal, role, daemon_rank);
+    if (cpus.empty()) return {};
+    const int node = pci_numa_node(bus_id);
     const int n = pin_thread(cpus);
     if (n == 0) return {};
-    OCM_LOG("%s: pinned to %d CPU(s) from %d, L3 complex at CPU %d (NUMA node %d of GPU %s), daemon core %d",
-            role == PinRole::Daemon ? "ocmd" : "libocm", n, cpus.front(), ccd.front(), node, bus_id.c_str(), dcore);
+    OCM_LOG("%s: pinned to %d CPU(s) from %d (NUMA node %d of GPU %s)", role == PinRole::Daemon ? "ocmd" : "libocm", n,
+            cpus.front(), node, bus_id.c_str());
     return cpus;
 }
 

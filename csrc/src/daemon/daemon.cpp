@@ -182,8 +182,10 @@ int Daemon::init() {
         // the data server's threads (started above) keep the full mask.
         char bus[64] = {0};
         orig_cpus_ = thread_cpus();
-        if (hipDeviceGetPCIBusId(bus, sizeof(bus), gpu_) == hipSuccess)
+        if (hipDeviceGetPCIBusId(bus, sizeof(bus), gpu_) == hipSuccess) {
             pinned_cpus_ = pin_near_gpu(bus, gpu_, PinRole::Daemon, rank_).size();
+            if (pinned_cpus_) near_cpus_ = near_gpu_cpus(bus, gpu_, PinRole::App, rank_);
+        }
         else
             (void)hipGetLastError();
     }

@@ -845,8 +845,17 @@ void Daemon::start_tick(const uint8_t *id, bool rccl) {
     }
     tick_ = std::make_unique<TickTransport>(rank_, n_, f);
     // The tick thread busy-polls its collective during traffic, and RCCL's proxy
-    // threads inherit its mask: keep them off the event loop's pinned core.
-    if (pinned_cpus_) tick_->set_cpus(orig_cpus_);
+    // threads inherit its mask: keep them off the event loop's pinned core, on the
+    // rest of the GPU's L3 complex (OCM_TICK_CPUS=ccd, default), the process's whole
+    // mask (=all), or sharing the event loop's core as before round 3 (=loop).
+    if (pinned_cpus_) {
+        const char *tc = std::getenv("OCM_TICK_CPUS");
+        const std::string mode = tc && *tc ? tc : "ccd";
+        if (mode == "all")
+            tick_->set_cpus(orig_cpus_);
+        else if (mode != "loop")
+            tick_->set_cpus(near_cpus_.empty() ? orig_cpus_ : near_cpus_);
+    }
     ep_add(tick_->event_fd(), EPOLLIN, tag(T_TICK, 0));
     tick_->start();
     OCM_INFO("rank %d: control records will ride the %s tick transport", rank_, rccl ? "rccl" : "socket");

@@ -471,7 +471,9 @@ void TickTransport::flush_ring() {
     if (!ring_ || out_.empty()) return;
     uint64_t pub = ring_pub_;  // never read back: the ring may sit behind a write-combined BAR
     while (!out_.empty() && pub - ring_sent_ < kTickRing) {
-        ring_->rec[pub & (kTickRing - 1)] = out_.front();
+        TickRecord &r = ring_->rec[pub & (kTickRing - 1)];
+        r = out_.front();
+        ring_->tag[pub & (kTickRing - 1)] = tick_record_tag(reinterpret_cast<const uint64_t *>(&r), pub);
         out_.pop_front();
         pub++;
     }

@@ -10,23 +10,72 @@
 // stream reads the slot after this kernel ends.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "ocm/tick.h"
 
 namespace ocm {
 namespace {
 
+__device__ __forceinline__ uint64_t sys_load(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Two round trips: `published` first, then the records it covers (OCM_TICK_SEAL_SPEC=0).
+__global__ __launch_bounds__(64) void tick_seal2_kernel(const TickRing *ring, uint64_t *consumed, TickSlot *slot) {
+    const int lane = threadIdx.x;
+    const uint64_t c = *consumed;  // this stream's own counter: plain load
+    const uint64_t pub = sys_load(&ring->published);
+    const uint64_t pending = pub > c ? pub - c : 0;
+    const uint32_t n = pending < (uint64_t)kTickMsgs ? (uint32_t)pending : (uint32_t)kTickMsgs;
+    for (int w = lane; w < (int)n * kTickRecordWords; w += 64) {
+        const int r = w / kTickRecordWords, k = w % kTickRecordWords;
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(&ring->rec[(c + (uint64_t)r) & (kTickRing - 1)]) + k;
+        uint64_t *dst = reinterpret_cast<uint64_t *>(&slot->rec[r]) + k;
+        *dst = sys_load(src);
+    }
+    if (lane == 0) {
+        slot->count = n;
+        slot->busy = pending > n ? 1u : 0u;
+        slot->first = c;
+        *consumed = c + n;
+    }
+}
+
+// Speculative seal (one PCIe round trip instead of two): lanes 0..kTickMsgs-1
+// each load record c + lane (21 words) and its tag, lane 63 loads `published`,
+// all in flight together. A record whose tag does not match was read before the
+// host finished it (it cannot be a published one then): every record the tick
+// takes is read again after `published` is known, the two-round-trip path.
+// Measured: the seal was 2.6 us of a ~9 us tick (profiles/rocprof_tick_kernels_r02.json).
 __global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uint64_t *consumed, TickSlot *slot) {
     const int lane = threadIdx.x;
     const uint64_t c = *consumed;  // this stream's own counter: plain load
-    const uint64_t pub = __hip_atomic_load(&ring->published, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint64_t w[kTickRecordWords];
+    uint64_t tag = 0, pub_l = 0;
+    const uint64_t j = c + (uint64_t)lane;
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(&ring->rec[j & (kTickRing - 1)]);
+    if (lane < kTickMsgs) {
+#pragma unroll
+        for (int k = 0; k < kTickRecordWords; k++) w[k] = sys_load(src + k);
+        tag = sys_load(&ring->tag[j & (kTickRing - 1)]);
+    }
+    if (lane == 63) pub_l = sys_load(&ring->published);
+    const uint64_t pub = ((uint64_t)__builtin_amdgcn_readlane((int)(pub_l >> 32), 63) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pub_l, 63);
     const uint64_t pending = pub > c ? pub - c : 0;
     const uint32_t n = pending < (uint64_t)kTickMsgs ? (uint32_t)pending : (uint32_t)kTickMsgs;
-    constexpr int kWords = (int)(sizeof(TickRecord) / sizeof(uint64_t));  // 21
-    for (int w = lane; w < (int)n * kWords; w += 64) {
-        const int r = w / kWords, k = w % kWords;
-        const uint64_t *src = reinterpret_cast<const uint64_t *>(&ring->rec[(c + (uint64_t)r) & (kTickRing - 1)]) + k;
-        uint64_t *dst = reinterpret_cast<uint64_t *>(&slot->rec[r]) + k;
-        *dst = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const bool mine = (uint32_t)lane < n;
+    const bool torn = mine && tick_record_tag(w, j) != tag;
+    if (__builtin_amdgcn_ballot_w64(torn) != 0 && mine) {
+#pragma unroll
+        for (int k = 0; k < kTickRecordWords; k++) w[k] = sys_load(src + k);  // published: complete now
+    }
+    if (mine) {
+        uint64_t *dst = reinterpret_cast<uint64_t *>(&slot->rec[lane]);
+#pragma unroll
+        for (int k = 0; k < kTickRecordWords; k++) dst[k] = w[k];
     }
     if (lane == 0) {
         slot->count = n;
@@ -52,7 +101,14 @@ hipError_t tick_done_launch(uint64_t *flag, uint64_t seq, hipStream_t stream) {
 
 hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, hipStream_t stream) {
     (void)hipGetLastError();  // report this launch, not an earlier call's error
-    hipLaunchKernelGGL(tick_seal_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot);
+    static const bool spec = [] {
+        const char *v = std::getenv("OCM_TICK_SEAL_SPEC");
+        return !(v && std::strcmp(v, "0") == 0);
+    }();
+    if (spec)
+        hipLaunchKernelGGL(tick_seal_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot);
+    else
+        hipLaunchKernelGGL(tick_seal2_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot);
     return hipGetLastError();
 }
 

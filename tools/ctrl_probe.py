@@ -21,6 +21,22 @@ from oncilla_amd.parallel import Mesh  # noqa: E402
 
 def run(ctrl, tick_self, **extra_env):
     env = {"OCM_LEASE_BYTES": "0", **extra_env}
+    # OCM_PIN is read by the daemon (from env) and by this process's libocm (os.environ)
+    saved = os.environ.get("OCM_PIN")
+    mask = os.sched_getaffinity(0)  # a pinned variant must not leave this thread pinned for the next
+    if "OCM_PIN" in extra_env:
+        os.environ["OCM_PIN"] = extra_env["OCM_PIN"]
+    try:
+        return _run(ctrl, tick_self, env)
+    finally:
+        os.sched_setaffinity(0, mask)
+        if saved is None:
+            os.environ.pop("OCM_PIN", None)
+        else:
+            os.environ["OCM_PIN"] = saved
+
+
+def _run(ctrl, tick_self, env):
     if tick_self:
         env["OCM_TICK_SELF"] = "1"
     with Mesh(1, gpus=[0], extra_args=["--ctrl", ctrl], env=env) as m:
@@ -53,6 +69,18 @@ VARIANTS = {
     "rccl_tick_sealed_depth3": ("rccl", True, {"OCM_TICK_DEPTH": "3"}),
     "rccl_tick_host_filled": ("rccl", True, {"OCM_TICK_SEAL": "0"}),
     "socket_tick": ("socket", True, {}),
+    # round 3: one-round-trip seal (default) vs two round trips, and where the tick thread runs
+    "rccl_spec_ccd": ("rccl", True, {"OCM_TICK_CPUS": "ccd"}),
+    "rccl_spec_all": ("rccl", True, {"OCM_TICK_CPUS": "all"}),
+    "rccl_spec_loop": ("rccl", True, {"OCM_TICK_CPUS": "loop"}),
+    "rccl_seal2_loop": ("rccl", True, {"OCM_TICK_SEAL_SPEC": "0", "OCM_TICK_CPUS": "loop"}),
+    "rccl_seal2_ccd": ("rccl", True, {"OCM_TICK_SEAL_SPEC": "0", "OCM_TICK_CPUS": "ccd"}),
+    # the app pinned next to the GPU too (OCM_PIN=1, round-2 default), or nothing pinned
+    "rccl_spec_ccd_pin": ("rccl", True, {"OCM_TICK_CPUS": "ccd", "OCM_PIN": "1"}),
+    "rccl_spec_loop_pin": ("rccl", True, {"OCM_TICK_CPUS": "loop", "OCM_PIN": "1"}),
+    "rccl_seal2_loop_pin": ("rccl", True, {"OCM_TICK_SEAL_SPEC": "0", "OCM_TICK_CPUS": "loop", "OCM_PIN": "1"}),
+    "rccl_spec_nopin": ("rccl", True, {"OCM_PIN": "0"}),
+    "tcp_pin": ("tcp", False, {"OCM_PIN": "1"}),
 }
 
 
@@ -64,9 +92,9 @@ def main():
     ap.add_argument("--repeat", type=int, default=1)
     a = ap.parse_args()
     out = {}
-    for v in a.variants.split(","):
-        ctrl, tick_self, env = VARIANTS[v]
-        for r in range(a.repeat):
+    for r in range(a.repeat):  # interleaved: every variant once per round
+        for v in a.variants.split(","):
+            ctrl, tick_self, env = VARIANTS[v]
             out[v if a.repeat == 1 else f"{v}#{r}"] = run(ctrl, tick_self, **env)
     print(json.dumps(out, indent=1))
     if a.out:
