@@ -180,6 +180,7 @@ private:
     // (and how many each tick took), re-sent by take_unsent if the tick fails.
     std::deque<TickRecord> inflight_;
     std::deque<uint32_t> inflight_n_;
+    bool timed_out_ = false;  // the watchdog (OCM_TICK_TIMEOUT_MS) ended the transport
 };
 
 }  // namespace ocm

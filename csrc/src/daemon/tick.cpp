@@ -261,6 +261,11 @@ public:
         recv_.assign(bytes * (size_t)n, 0);
         const char *tf = std::getenv("OCM_TICK_FAULT");
         fault_do_alloc_ = tf && std::strcmp(tf, "fail_after_do_alloc") == 0 && bytes == sizeof(TickSlot);
+        // stall_after=N: from tick N on this rank stops taking part, without an error
+        // (a wedged collective): the peers' watchdogs must end the transport.
+        if (tf && std::strncmp(tf, "stall_after=", 12) == 0) stall_after_ = std::atoll(tf + 12);
+        const char *to = std::getenv("OCM_TICK_TIMEOUT_MS");
+        timeout_ms_ = to && *to ? std::max(1L, std::atol(to)) : 5000;
         const char *sl = std::getenv("OCM_TICK_SOCKET_SEAL");
         if (sl && std::strcmp(sl, "1") == 0 && bytes == sizeof(TickSlot)) {
             outbox_.reset(new TickRing());
@@ -303,6 +308,10 @@ public:
             slot->first = consumed_;
             consumed_ += n;
         }
+        if (stall_after_ > 0 && ++started_ >= (uint64_t)stall_after_) {
+            while (!aborted_) usleep(1000);  // wedged until the transport is torn down
+            return -1;
+        }
         char *out = recv_.data();
         std::memcpy(out + (size_t)rank_ * bytes_, send_.data(), bytes_);
         // Ring: at step s send block (rank - s) right, receive block (rank - s - 1) from the left.
@@ -342,13 +351,23 @@ public:
 private:
     int xfer(int fd, char *p, size_t n, bool snd) {
         // Seqpacket records are capped by the socket buffer; move the block in pieces.
+        // A neighbour that stops taking part without closing its socket is caught by
+        // the same OCM_TICK_TIMEOUT_MS as an RCCL tick that never completes.
         size_t done = 0;
+        int idle_ms = 0;
         while (done < n && !aborted_) {
             const size_t piece = std::min<size_t>(n - done, 4096);
             struct pollfd q = {fd, (short)(snd ? POLLOUT : POLLIN), 0};
             int pr = poll(&q, 1, 200);
             if (pr < 0 && errno != EINTR) return -1;
-            if (pr <= 0) continue;
+            if (pr <= 0) {
+                if ((idle_ms += 200) >= timeout_ms_) {
+                    error_ = "no progress within OCM_TICK_TIMEOUT_MS (a peer stopped taking part)";
+                    return -1;
+                }
+                continue;
+            }
+            idle_ms = 0;
             ssize_t k = snd ? send(fd, p + done, piece, MSG_NOSIGNAL) : recv(fd, p + done, piece, 0);
             if (k <= 0) {
                 if (k < 0 && (errno == EAGAIN || errno == EINTR)) continue;
@@ -365,6 +384,9 @@ private:
     uint64_t consumed_ = 0;
     std::atomic<bool> aborted_{false};
     bool fault_do_alloc_ = false, fault_fired_ = false;
+    long long stall_after_ = 0;
+    uint64_t started_ = 0;
+    long timeout_ms_ = 5000;
     std::string error_;
 };
 
@@ -565,6 +587,21 @@ void TickTransport::run() {
     up_ = true;
     signal();
     uint64_t issued = 0, done = 0, target = 0;
+    // Watchdog: a collective that neither completes nor reports an error (a peer
+    // that never joins it, a wedged transport) would hold every record queued
+    // behind it. After OCM_TICK_TIMEOUT_MS (5 s) the transport fails, and the
+    // daemon re-sends over TCP what it had not delivered.
+    const uint64_t timeout_ns = [] {
+        const char *v = std::getenv("OCM_TICK_TIMEOUT_MS");
+        const long ms = v && *v ? std::atol(v) : 5000;
+        return (uint64_t)std::max(1L, ms) * 1000000ull;
+    }();
+    std::vector<uint64_t> issued_at(depth, 0);
+    auto mono_ns = [] {
+        struct timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+    };
     auto fail = [&] {
         if (!stop_)
             OCM_WARN("rank %d: %s tick transport failed (%s); falling back to TCP", rank_, coll->name(),
@@ -607,6 +644,7 @@ void TickTransport::run() {
                 const int rc = coll->start(i);
                 lk.lock();
                 if (rc != 0) break;
+                issued_at[(size_t)i] = mono_ns();
                 issued++;
             }
             if (issued < target && issued - done < depth) {  // start() failed
@@ -623,9 +661,18 @@ void TickTransport::run() {
         for (unsigned spins = 0; !stop_; spins++) {
             t = coll->test(i);
             if (t != 0) break;
+            if ((spins & 1023) == 1023 && mono_ns() - issued_at[(size_t)i] > timeout_ns) {
+                t = -1;
+                timed_out_ = true;
+                coll->abort();
+                break;
+            }
             if (issued - done < depth && (spins & 15) == 15) break;
         }
         if (t < 0) {
+            if (timed_out_ && !stop_)
+                OCM_WARN("rank %d: tick %llu did not complete within OCM_TICK_TIMEOUT_MS", rank_,
+                         (unsigned long long)(done + 1));
             fail();
             break;
         }

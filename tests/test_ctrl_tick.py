@@ -224,3 +224,27 @@ def test_ctrl_auto_falls_back_to_tcp_when_the_transport_never_comes_up(mesh_fact
         assert all(c.stats(r)["ctrl_ticks"] == 0 for r in range(4))
     logs = m.logs()
     assert "not up within OCM_TICK_UP_MS=400 ms" in logs, logs
+
+
+@pytest.mark.parametrize("sealed", ["0", "1"])
+def test_a_wedged_collective_times_out_and_the_mesh_falls_back(mesh_factory, sealed):
+    """A rank stops taking part in the ticks without any error (a wedged
+    collective: OCM_TICK_FAULT=stall_after=N on rank 2). The other ranks' tick
+    watchdog (OCM_TICK_TIMEOUT_MS) ends the transport, everybody leaves it, what
+    the ticks had not delivered goes over TCP, and allocations keep working."""
+    m = mesh_factory(3, extra_args=["--ctrl", "socket"],
+                     env={"OCM_TICK_SOCKET_SEAL": sealed, "OCM_TICK_TIMEOUT_MS": "400", "OCM_LEASE_BYTES": "0"},
+                     rank_env={2: {"OCM_TICK_FAULT": "stall_after=30"}})
+    with api.Client(daemon_rank=1, ns=m.ns) as c:
+        for i in range(30):  # stalls part-way through: later ones need the TCP fallback
+            a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20, flags=api.OCM_ALLOC_STRIPE)
+            a.fill(seed=40 + i)
+            a.put(0, 0, 1 << 20)
+            a.fill(seed=0)
+            a.get(0, 0, 1 << 20)
+            assert a.check(seed=40 + i) == 0
+            a.free()
+        assert all(c.stats(r)["ctrl"] == "tcp (left ticks)" for r in range(3))
+    logs = m.logs()
+    assert "OCM_TICK_TIMEOUT_MS" in logs, logs
+    assert logs.count("leaving the socket tick transport") == 3, logs
