@@ -46,6 +46,8 @@ struct XferTuning {
     int variant = XFER_AUTO;
     int max_blocks = 0;      // 0: per-path default
     bool nontemporal = true; // nt stores on the destination
+    bool write_through = false;  // register kernel: sc1 (write-through) loads and stores instead
+                                 // (autotune candidate over xGMI; what won PCIe puts)
 };
 
 // Completion published by the kernel itself (blocking ops): every workgroup

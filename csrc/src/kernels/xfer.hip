@@ -247,14 +247,14 @@ __device__ __forceinline__ void xfer_publish(const XferDone &d) {
     }
 }
 
-template <bool NT>
+template <int ST>
 __global__ __launch_bounds__(kThreads) void xfer_reg_kernel(XferArgs a, XferDone d) {
     const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
     const uint64_t first = a.rem_off & ~tile_mask;
     const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - first) >> a.tile_shift;
     for (uint64_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
         TileSpan s = tile_span(a, ti, first);
-        span_copy<NT ? ST_NT : ST_PLAIN>(s.dst, s.src, s.n);
+        span_copy<ST>(s.dst, s.src, s.n);
     }
     xfer_publish(d);
 }
@@ -444,6 +444,7 @@ XferTuning xfer_tuning_from_env() {
     if (v && (!std::strcmp(v, "push") || !std::strcmp(v, "5"))) t.variant = XFER_PUSH;
     t.max_blocks = env_int("OCM_XFER_BLOCKS", 0);
     t.nontemporal = env_int("OCM_XFER_NT", 1) != 0;
+    t.write_through = env_int("OCM_XFER_NT", 1) == 2;  // 2: sc1 loads and stores (register kernel)
     return t;
 }
 
@@ -492,10 +493,12 @@ hipError_t xfer_launch(const XferArgs &in, const XferTuning &t, hipStream_t stre
         else
             hipLaunchKernelGGL(xfer_lds_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a, d);
     } else {
-        if (t.nontemporal)
-            hipLaunchKernelGGL(xfer_reg_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a, d);
+        if (t.write_through)
+            hipLaunchKernelGGL(xfer_reg_kernel<ST_WT>, dim3(grid), dim3(kThreads), 0, stream, a, d);
+        else if (t.nontemporal)
+            hipLaunchKernelGGL(xfer_reg_kernel<ST_NT>, dim3(grid), dim3(kThreads), 0, stream, a, d);
         else
-            hipLaunchKernelGGL(xfer_reg_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a, d);
+            hipLaunchKernelGGL(xfer_reg_kernel<ST_PLAIN>, dim3(grid), dim3(kThreads), 0, stream, a, d);
     }
     return hipGetLastError();
 }

@@ -911,6 +911,7 @@ void ocm_x_set_tuning(int variant, int blocks, int nt) {
     s.tuning.variant = variant;
     s.tuning.max_blocks = blocks;
     s.tuning.nontemporal = nt != 0;
+    s.tuning.write_through = nt == 2;
     s.dir_tuning[0] = s.dir_tuning[1] = XferTuning{};
 }
 
@@ -925,6 +926,7 @@ int ocm_x_set_tuning_dir(int dir, int variant, int blocks, int nt) {
     t.variant = variant;
     t.max_blocks = blocks;
     t.nontemporal = nt != 0;
+    t.write_through = nt == 2;  // 2: sc1 loads and stores (register kernel)
     s.dir_tuning[dir] = t;
     return 0;
 }
@@ -1041,6 +1043,7 @@ double ocm_x_time_device_copy(int device, void *dst, const void *src, uint64_t b
     t.variant = variant;
     t.max_blocks = blocks;
     t.nontemporal = nt != 0;
+    t.write_through = nt == 2;
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);

@@ -309,10 +309,12 @@ def set_tuning(variant: int = 0, blocks: int = 0, nontemporal: bool = True) -> N
     load().ocm_x_set_tuning(variant, blocks, 1 if nontemporal else 0)
 
 
-def set_tuning_dir(op_flag: int, variant: int = 0, blocks: int = 0, nontemporal: bool = True) -> None:
+def set_tuning_dir(op_flag: int, variant: int = 0, blocks: int = 0, nontemporal=True) -> None:
     """Per-direction override for one-sided kernel ops (op_flag 0 get, 1 put); variant 0 clears it.
-    ``set_tuning`` clears both overrides."""
-    if load().ocm_x_set_tuning_dir(op_flag, variant, blocks, 1 if nontemporal else 0) != 0:
+    ``nontemporal``: True / 1 nt stores, False / 0 plain, 2 write-through (sc1) loads and stores
+    in the register kernel. ``set_tuning`` clears both overrides."""
+    nt = 2 if nontemporal == 2 else (1 if nontemporal else 0)
+    if load().ocm_x_set_tuning_dir(op_flag, variant, blocks, nt) != 0:
         raise ValueError(f"bad tuning: op_flag={op_flag} variant={variant} blocks={blocks}")
 
 

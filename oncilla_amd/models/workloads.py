@@ -83,10 +83,12 @@ def characterize(alloc: api.Allocation, sizes: Iterable[int], target_s: float = 
 # Configurations an autotune chooses from: (variant 0 auto / 1 register kernel /
 # 2 LDS-DMA kernel / 3 the runtime's copy engines / 4 PCIe streaming kernel /
 # 5 push-based get (kernels on the owners' GPUs write into the local half; puts
-# fall back to auto), grid cap 0 = default, nontemporal destination stores).
+# fall back to auto), grid cap 0 = default, destination stores: 1 nontemporal,
+# 0 plain, 2 write-through sc1 loads and stores, which won PCIe puts).
 TUNING_CANDIDATES = {"auto": (0, 0, 1), "reg_b256": (1, 256, 1), "reg_b1024": (1, 1024, 1),
                      "reg_b2048": (1, 2048, 1), "reg_nt0": (1, 0, 0), "lds_default": (2, 0, 1),
-                     "lds_b512": (2, 512, 1), "push": (5, 0, 1), "push_b1024": (5, 1024, 1), "dma": (3, 0, 1)}
+                     "lds_b512": (2, 512, 1), "reg_wt": (1, 0, 2), "reg_wt_b1024": (1, 1024, 2), "push": (5, 0, 1),
+                     "push_b1024": (5, 1024, 1), "dma": (3, 0, 1)}
 # Measured and reported, never installed: the runtime's copy engines are the
 # comparison baseline for the repo's own kernels, not a data path.
 BASELINE_ONLY = frozenset({"dma"})
@@ -116,7 +118,7 @@ def autotune(alloc: api.Allocation, nbytes: int, reps: int = 3, gather=None, can
         for op, key in ((0, "get"), (1, "put")):
             t, err = None, None
             try:
-                api.set_tuning_dir(op, variant, blocks, bool(nt))
+                api.set_tuning_dir(op, variant, blocks, nt)
                 alloc.time_onesided(op, nbytes, 1)
             except Exception as e:  # noqa: BLE001 - recorded; every rank still reaches every gather
                 err = repr(e)[:160]
@@ -135,7 +137,7 @@ def autotune(alloc: api.Allocation, nbytes: int, reps: int = 3, gather=None, can
         ok = {n: r[key]["s"] for n, r in table.items() if "s" in r[key] and n not in baselines}
         pick = min(ok, key=ok.get) if ok else "auto"
         variant, blocks, nt = cands[pick]
-        api.set_tuning_dir(op, variant, blocks, bool(nt))
+        api.set_tuning_dir(op, variant, blocks, nt)
         best[key] = pick
     ranks = len(gather(None))
     return {"get": best["get"], "put": best["put"], "bytes": nbytes, "ranks": ranks, "baselines": sorted(baselines),

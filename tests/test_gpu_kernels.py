@@ -85,6 +85,27 @@ def test_pcie_kernel_on_pinned_host_memory(put, n_ext, unit):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("put", [True, False])
+def test_register_kernel_write_through_matches_reference(monkeypatch, put):
+    # OCM_XFER_NT=2: the register kernel with sc1 (write-through) loads and stores,
+    # an autotune candidate over xGMI; byte-exact, striped, unaligned.
+    monkeypatch.setenv("OCM_XFER_NT", "2")
+    n_ext, unit = 3, 65536
+    total = n_ext * unit * 5 + 12345
+    rem_off, nbytes = unit // 2 + 3, total - unit - 100
+    ext_len = ((rem_off + nbytes) // unit // n_ext + 2) * unit
+    exts = [_rand(ext_len, 700 + i) for i in range(n_ext)]
+    lin = _rand(nbytes + 64, 11)
+    exts_ref = [e.clone() for e in exts]
+    lin_ref = lin.clone()
+    ops.striped_reference(lin_ref, exts_ref, unit, rem_off, nbytes, put)
+    ops.xfer(lin, exts, unit, rem_off, nbytes, put=put, variant=ops.XFER_REG)
+    torch.cuda.synchronize()
+    assert torch.equal(lin, lin_ref)
+    for a, b in zip(exts, exts_ref):
+        assert torch.equal(a, b)
+
+
 def test_grid_sizes_and_small_grids():
     n = (3 << 20) + 7
     src = _rand(n, 1)
