@@ -117,10 +117,16 @@ int main(int argc, char **argv) {
         std::fprintf(stderr, "bytes must be a multiple of 4 KiB in (0, 1 GiB]\n");
         return 2;
     }
-    const int fd = memfd_create("pcie_probe", 0);
-    if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) return 1;
-    void *host = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    // argv[6] "anonhuge": anonymous memory with MADV_HUGEPAGE (2 MiB host pages when
+    // THP allows) instead of the memfd slab (4 KiB shmem pages): does the GPU's
+    // translation of host pages cost PCIe throughput?
+    const bool anonhuge = argc > 6 && std::string(argv[6]) == "anonhuge";
+    const int fd = anonhuge ? -1 : memfd_create("pcie_probe", 0);
+    if (!anonhuge && (fd < 0 || ftruncate(fd, (off_t)bytes) != 0)) return 1;
+    void *host = anonhuge ? mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0)
+                          : mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     if (host == MAP_FAILED) return 1;
+    if (anonhuge) (void)madvise(host, bytes, MADV_HUGEPAGE);
     std::memset(host, 0x5a, bytes);
     CHECK(hipHostRegister(host, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
     void *hdev = nullptr;
@@ -207,6 +213,6 @@ int main(int argc, char **argv) {
     std::printf("}\n");
     CHECK(hipHostUnregister(host));
     munmap(host, bytes);
-    close(fd);
+    if (fd >= 0) close(fd);
     return 0;
 }
