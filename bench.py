@@ -112,6 +112,10 @@ class Phases:
 
     def run(self, name: str, fn):
         self.current = name
+        if self.rank == 0:
+            # progress on stderr (stdout carries only the final JSON line): a long N=8 setup
+            # (RCCL bootstrap, autotune) is never mistaken for a hang by a silence watchdog
+            print(f"[bench] {time.strftime('%H:%M:%S')} phase {name}", file=sys.stderr, flush=True)
         val, err = None, None
         try:
             if self.inject and int(self.inject[0]) == self.rank and self.inject[1] == name:
