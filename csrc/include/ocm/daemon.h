@@ -31,6 +31,7 @@
 #include "ocm/pmsg.h"
 #include "ocm/siphash.h"
 #include "ocm/sock.h"
+#include "ocm/shmlink.h"
 #include "ocm/tick.h"
 
 namespace ocm {
@@ -80,6 +81,8 @@ private:
         int pidfd = -1;
         std::deque<Msg> backlog;
         bool watching_out = false;
+        std::shared_ptr<ShmLink> link;  // shared-memory fast path (ocm/shmlink.h), if the app offered one
+        std::deque<Msg> link_backlog;   // replies waiting for room in the link's ring
     };
     struct AppConn {
         int fd = -1;
@@ -157,6 +160,12 @@ private:
     // dispatch
     void handle_app_msg(Msg &m);
     void handle_mesh_msg(Msg &m, int from_fd);
+    // Shared-memory links of the apps: take their requests (returns how many),
+    // and the daemon_polling flag around the event loop's sleeps.
+    int poll_links();
+    void links_polling(bool on);
+    bool links_polling_ = true;
+    int pending_link_fd_ = -1;  // a link memfd that arrived with MSG_CONNECT, for app_connect
     // Once a tick transport exists, the allocation protocol's records are
     // remembered by content: when the transport fails, a sender re-sends over TCP
     // every record it cannot prove delivered (TickTransport::take_unsent), and a

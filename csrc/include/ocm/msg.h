@@ -45,6 +45,7 @@ enum MsgType : uint32_t {
     MSG_NODE_LINKS,       // daemon -> rank0 after ADD_NODE: xGMI link type / hops from its GPU (u.links)
     MSG_SLAB_FD,          // app -> owner daemon: a host-tier slab's memfd (u.region.slab_id), reply carries it (SCM_RIGHTS)
     MSG_TICK_STOP,        // any -> all (TCP): the sender left the tick transport; leave it too (records ride TCP)
+    MSG_WAKE,             // app <-> daemon (mailbox socket): look at the shared-memory link (ocm/shmlink.h)
     MSG_MAX
 };
 

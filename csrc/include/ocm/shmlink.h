@@ -1,0 +1,89 @@
+// Shared-memory fast path of an app's mailbox (app <-> its local ocmd).
+//
+// The mailbox (ocm/pmsg.h) costs a system call per record on each side, plus an
+// epoll wake-up in the daemon and a poll in the app: 2.5-3 us for a remote
+// ocm_alloc round trip on MI355X hosts, most of it kernel entry and exit. The
+// reference paid a 500 us mailbox poll here (src/main.c:112-126).
+//
+// A ShmLink is one memfd the app creates at ocm_init, seals against resizing
+// (F_SEAL_SHRINK/GROW/SEAL, so the daemon's mapping can never fault), and passes
+// to its daemon with MSG_CONNECT (SCM_RIGHTS). It holds two single-producer /
+// single-consumer rings of 160-byte records: requests app -> daemon, replies
+// daemon -> app. Records, ordering and semantics are exactly those of the
+// mailbox; only the transport changes. The socket stays for the connection's
+// lifetime (EOF still tells the daemon that the app died) and carries the
+// wake-ups:
+//   * the daemon polls its links while it is awake (its post-activity spin);
+//     before it sleeps it clears `daemon_polling`, fences and looks once more.
+//     An app that posts a request, fences and finds the flag clear sends
+//     MSG_WAKE on the socket (Dekker: one of the two always sees the other);
+//   * an app spins on the reply ring for OCM_RPC_SPIN_US, then sets
+//     `app_waiting`, fences, looks once more and sleeps in poll(2) on the
+//     socket; a daemon that posts a reply and finds the flag set sends MSG_WAKE.
+// The daemon copies every record out of the shared ring before it looks at it
+// (the app may rewrite the ring at any time) and trusts the connection's
+// SO_PEERCRED pid, not the record's, as on the socket path.
+#pragma once
+#include <atomic>
+#include <cstddef>
+#include <cstdint>
+
+#include "ocm/msg.h"
+
+namespace ocm {
+
+constexpr uint32_t kShmLinkSlots = 64;  // power of two
+constexpr uint32_t kShmLinkMagic = 0x4f434d4cu;  // "OCML"
+
+struct ShmLinkLayout {
+    alignas(64) uint32_t magic;
+    uint32_t slots;
+    alignas(64) std::atomic<uint64_t> req_head;  // app: records posted
+    alignas(64) std::atomic<uint64_t> req_tail;  // daemon: records taken
+    alignas(64) std::atomic<uint64_t> rsp_head;  // daemon: records posted
+    alignas(64) std::atomic<uint64_t> rsp_tail;  // app: records taken
+    alignas(64) std::atomic<uint32_t> daemon_polling;  // the daemon looks at the link without a wake-up
+    alignas(64) std::atomic<uint32_t> app_waiting;     // the app sleeps on the socket: wake it
+    alignas(64) Msg req[kShmLinkSlots];
+    alignas(64) Msg rsp[kShmLinkSlots];
+};
+static_assert(std::atomic<uint64_t>::is_always_lock_free, "ring counters must be lock-free across processes");
+
+class ShmLink {
+public:
+    ShmLink() = default;
+    ~ShmLink() { close(); }
+    ShmLink(const ShmLink &) = delete;
+    ShmLink &operator=(const ShmLink &) = delete;
+
+    // App: a fresh sealed memfd with the layout, mapped. Returns 0; fd() passes it.
+    int create();
+    // Daemon: map an app's link. Refuses a descriptor that is not a sealed memfd
+    // of exactly the layout's size. Takes ownership of `fd` either way.
+    int attach(int fd);
+    void close();
+    bool ok() const { return l_ != nullptr; }
+    int fd() const { return fd_; }
+
+    // App side.
+    bool post_request(const Msg &m);  // false: ring full (use the socket)
+    bool take_reply(Msg *m);
+    // Daemon side.
+    bool take_request(Msg *m);        // a copy, taken out of the shared ring first
+    bool post_reply(const Msg &m);    // false: ring full (keep it and retry)
+
+    // The wake-up protocol (see the header comment). Each returns whether the
+    // caller must send MSG_WAKE on the socket.
+    bool request_needs_wake();        // app, after post_request
+    bool reply_needs_wake();          // daemon, after post_reply
+    void set_daemon_polling(bool on);
+    bool requests_pending();          // daemon, after set_daemon_polling(false): look once more
+    void set_app_waiting(bool on);
+    bool replies_pending();           // app, after set_app_waiting(true)
+
+private:
+    ShmLinkLayout *l_ = nullptr;
+    int fd_ = -1;
+};
+
+}  // namespace ocm

@@ -17,6 +17,8 @@ struct OpCounters {
     uint64_t n_batch_launches = 0;  // batch kernels launched outside plans (batches, remote->remote copies)
     uint64_t n_slab_fd = 0;         // host-tier slabs imported through an fd from their owner (SCM_RIGHTS)
     uint64_t n_slab_path = 0;       // ... through the /proc/<pid>/fd path fallback
+    uint64_t n_link_rpc = 0;        // RPCs posted on the shared-memory link (ocm/shmlink.h)
+    uint64_t n_link_wake = 0;       // ... of which had to wake the daemon over the socket
 };
 
 bool trace_enabled();  // OCM_TRACE=0 disables the roctx ranges

@@ -38,6 +38,7 @@ void Daemon::handle_app_msg(Msg &m) {
         return;
     }
     switch (m.type) {
+    case MSG_WAKE: break;  // the app posted on its shared-memory link while we slept: the loop looks there
     case MSG_DISCONNECT: app_disconnect(m.pid, false); break;
     case MSG_REQ_ALLOC: app_req_alloc(m); break;
     case MSG_REQ_FREE: app_req_free(m); break;
@@ -63,6 +64,18 @@ void Daemon::app_connect(const Msg &m, int fd) {
     App a;
     a.pid = pid;
     a.fd = fd;
+    if (pending_link_fd_ >= 0) {
+        // The app offered a shared-memory link with its CONNECT (SCM_RIGHTS).
+        auto link = std::make_shared<ShmLink>();
+        const int lfd = pending_link_fd_;
+        pending_link_fd_ = -1;
+        if (link->attach(lfd) == 0) {
+            link->set_daemon_polling(links_polling_);
+            a.link = std::move(link);
+        } else {
+            OCM_WARN("rank %d: app %d offered an unusable shared-memory link; using its mailbox", rank_, (int)pid);
+        }
+    }
     a.pidfd = pidfd_open_compat(pid);
     if (a.pidfd >= 0) ep_add(a.pidfd, EPOLLIN, tag(T_PIDFD, (uint64_t)pid));
     apps_[pid] = std::move(a);

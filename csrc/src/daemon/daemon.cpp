@@ -408,8 +408,21 @@ int Daemon::loop() {
         int timeout = 1000;
         if (r0_lost_) timeout = 100;
         if (gov_ && !cfg_.state_file.empty() && gov_->version() != saved_version_) timeout = cfg_.state_interval_ms;
+        // Apps' shared-memory links are looked at on every pass: while the loop
+        // is awake (its post-activity spin) their requests need no wake-up.
+        if (poll_links() > 0) last_event_ns = now_ns();
         const bool spinning = spin_ns && now_ns() - last_event_ns < spin_ns;
-        int n = epoll_wait(ep_, evs, 64, (self_q_.empty() && !spinning) ? timeout : 0);
+        int wait_ms = (self_q_.empty() && !spinning) ? timeout : 0;
+        if (wait_ms > 0) {
+            // About to sleep: from here on an app that posts must wake us; look once more.
+            links_polling(false);
+            if (poll_links() > 0) {
+                last_event_ns = now_ns();
+                wait_ms = 0;
+            }
+        }
+        int n = epoll_wait(ep_, evs, 64, wait_ms);
+        links_polling(true);
         if (n > 0 && spin_ns) last_event_ns = now_ns();
         sweep_timeouts();
         check_tick_bootstrap();
@@ -515,9 +528,11 @@ void Daemon::on_app_conn(int fd, uint32_t events) {
     if (!(events & (EPOLLIN | EPOLLHUP | EPOLLERR))) return;
     Msg m;
     for (int i = 0; i < 64; i++) {
-        int rc = mbox_recv(fd, &m, kMsgBytes, 0);
+        int passed = -1;
+        int rc = mbox_recv_fd(fd, &m, kMsgBytes, &passed, 0);
         if (rc == 0) return;
         if (rc < 0) {
+            if (passed >= 0) close(passed);
             close_app_conn(fd);
             return;
         }
@@ -525,9 +540,13 @@ void Daemon::on_app_conn(int fd, uint32_t events) {
         if (it->second.peer_pid > 0) m.pid = it->second.peer_pid;
         if (m.type == MSG_CONNECT) {
             it->second.app_pid = m.pid;
+            pending_link_fd_ = passed;  // a shared-memory link, if the app offered one
             app_connect(m, fd);
+            if (pending_link_fd_ >= 0) close(pending_link_fd_);
+            pending_link_fd_ = -1;
             continue;
         }
+        if (passed >= 0) close(passed);  // descriptors ride only with CONNECT
         if (m.type == MSG_SLAB_FD) {
             // Capability transfer of a host-tier slab to an app of our uid (checked at
             // accept): the memfd itself, so no /proc path (ptrace rules, hidepid) is needed.
@@ -655,10 +674,68 @@ void Daemon::send_tcp(int r, Msg &m) {
     if (c.want_write) ep_mod(fd, EPOLLIN | EPOLLOUT, tag(T_CONN, (uint64_t)fd));
 }
 
+int Daemon::poll_links() {
+    int n = 0;
+    std::vector<pid_t> with_links;
+    for (auto &kv : apps_)
+        if (kv.second.link) with_links.push_back(kv.first);
+    for (pid_t pid : with_links) {
+        auto it = apps_.find(pid);
+        if (it == apps_.end() || !it->second.link) continue;
+        std::shared_ptr<ShmLink> link = it->second.link;  // stays mapped if the app goes away meanwhile
+        App &a = it->second;
+        bool wake = false;
+        while (!a.link_backlog.empty() && link->post_reply(a.link_backlog.front())) {
+            a.link_backlog.pop_front();
+            wake = true;
+        }
+        if (wake && link->reply_needs_wake()) {
+            Msg w;
+            std::memset(&w, 0, sizeof(w));
+            w.type = MSG_WAKE;
+            w.pid = pid;
+            w.rank = rank_;
+            send_app(pid, w);
+        }
+        Msg m;
+        for (int i = 0; i < 64 && link->take_request(&m); i++) {
+            m.pid = pid;  // the connection's SO_PEERCRED pid, never the record's
+            n++;
+            if (m.type == MSG_CONNECT || m.type == MSG_SLAB_FD || m.type == MSG_WAKE) continue;  // socket-only records
+            handle_app_msg(m);
+            if (!apps_.count(pid)) break;  // it disconnected
+        }
+    }
+    return n;
+}
+
+void Daemon::links_polling(bool on) {
+    if (links_polling_ == on) return;
+    links_polling_ = on;
+    for (auto &kv : apps_)
+        if (kv.second.link) kv.second.link->set_daemon_polling(on);
+}
+
 void Daemon::send_app(pid_t pid, const Msg &m) {
     auto it = apps_.find(pid);
     if (it == apps_.end() || it->second.fd < 0) return;
     App &a = it->second;
+    if (a.link && m.type != MSG_WAKE) {
+        // Replies ride the app's shared-memory link, in order; the socket only wakes it.
+        if (a.link_backlog.empty() && a.link->post_reply(m)) {
+            if (a.link->reply_needs_wake()) {
+                Msg w;
+                std::memset(&w, 0, sizeof(w));
+                w.type = MSG_WAKE;
+                w.pid = pid;
+                w.rank = rank_;
+                send_app(pid, w);
+            }
+        } else {
+            a.link_backlog.push_back(m);  // drained by poll_links
+        }
+        return;
+    }
     if (a.backlog.empty()) {
         int rc = mbox_send(a.fd, &m, kMsgBytes, 0);
         if (rc == 1) return;

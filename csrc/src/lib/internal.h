@@ -28,6 +28,7 @@
 #include "ocm/netdata.h"
 #include "ocm/pmsg.h"
 #include "ocm/range_alloc.h"
+#include "ocm/shmlink.h"
 #include "ocm/sock.h"
 #include "ocm/trace.h"
 #include "ocm/xfer.h"
@@ -178,6 +179,7 @@ struct State {
     pid_t pid = 0;
     std::string ns, daemon_mbox;
     Channel chan;
+    ShmLink link;  // shared-memory fast path to the daemon (OCM_SHM_LINK=0: the mailbox alone)
     NodeConfig daemon{};
     int daemon_rank = 0;
     int device = -1;

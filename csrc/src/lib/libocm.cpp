@@ -45,16 +45,20 @@ int ocm_init(void) {
     long deadline = now_ms() + connect_ms;
     if (s.chan.connect(s.daemon_mbox, connect_ms) != 0)
         OCM_FAIL(-1, "no ocmd mailbox @%s (is the daemon running?)", s.daemon_mbox.c_str());
+    // Shared-memory fast path of the mailbox (ocm/shmlink.h), offered with CONNECT.
+    if (env_int("OCM_SHM_LINK", 1) && s.link.create() != 0) OCM_WARN("no shared-memory link (%s); mailbox only", strerror(errno));
     Msg reply;
     for (;;) {
         Msg c = new_msg(MSG_CONNECT);
         if (rpc(c, &reply, std::max(1000, connect_ms)) != 0) {
             s.chan.close();
+            s.link.close();
             return -1;
         }
         if (reply.err != EAGAIN) break;
         if (now_ms() > deadline) {
             s.chan.close();
+            s.link.close();
             OCM_FAIL(-1, "daemon mesh not ready after %d ms", connect_ms);
         }
         usleep(20000);  // mesh still joining
@@ -200,6 +204,7 @@ int ocm_tini(void) {
     s.pool_tried = false;
     if (s.pinned) s.pinned->release_all();
     s.chan.close();
+    s.link.close();
     s.inited = false;
     trace_flush("app");
     return 0;
@@ -732,12 +737,12 @@ const char *ocm_last_error(void) { return last_error(); }
 // ---------------- internal hooks for tests and benchmarks (not part of the ABI) ----------------
 
 // Per-process operation counters (see ocm/trace.h): 17 x uint64.
-void ocm_x_counters(uint64_t out[19]) {
+void ocm_x_counters(uint64_t out[21]) {
     const OpCounters &c = S().ctr;
-    const uint64_t v[19] = {c.n_put,  c.n_get,    c.bytes_put, c.bytes_get,   c.n_alloc,     c.n_free,
+    const uint64_t v[21] = {c.n_put,  c.n_get,    c.bytes_put, c.bytes_get,   c.n_alloc,     c.n_free,
                             c.n_copy, c.bytes_copy, c.ns_put,  c.ns_get,      c.ns_alloc,    c.ns_free,
                             c.n_batch, c.n_batch_ops, c.bytes_batch, c.ns_batch, c.n_batch_launches,
-                            c.n_slab_fd, c.n_slab_path};
+                            c.n_slab_fd, c.n_slab_path, c.n_link_rpc, c.n_link_wake};
     std::memcpy(out, v, sizeof(v));
 }
 

@@ -35,31 +35,77 @@ Msg new_msg(uint32_t type) {
     return m;
 }
 
+// The next record from the daemon: the shared-memory link first (ocm/shmlink.h),
+// then the socket (everything when there is no link; wake-ups, which are
+// skipped, when there is one). Polls for `spin_ns`, then sleeps in poll(2) on
+// the socket until `deadline_ms`. Returns 1, 0 on timeout, -1 on error.
+static int recv_record(Msg *m, long deadline_ms, uint64_t spin_ns) {
+    State &s = S();
+    const bool link = s.link.ok();
+    const uint64_t t0 = now_ns();
+    for (unsigned i = 0;; i++) {
+        if (link && s.link.take_reply(m)) return 1;
+        // With a link the socket carries only wake-ups: look at it now and then.
+        if (!link || (i & 63) == 0) {
+            const int rc = s.chan.recv(m, kMsgBytes, 0);
+            if (rc < 0) return -1;
+            if (rc == 1 && m->type != MSG_WAKE) return 1;
+        }
+        if (now_ns() - t0 >= spin_ns) break;
+    }
+    for (;;) {
+        const long left = deadline_ms - now_ms();
+        if (left <= 0) return 0;
+        if (link) {
+            s.link.set_app_waiting(true);  // from here the daemon wakes us; look once more
+            if (s.link.replies_pending()) {
+                s.link.set_app_waiting(false);
+                if (s.link.take_reply(m)) return 1;
+                continue;
+            }
+        }
+        const int rc = s.chan.recv(m, kMsgBytes, (int)std::min<long>(left, 1000));
+        if (link) {
+            s.link.set_app_waiting(false);
+            if (rc >= 0 && (rc == 0 || m->type == MSG_WAKE)) {
+                if (s.link.take_reply(m)) return 1;
+                continue;
+            }
+        }
+        if (rc < 0) return -1;
+        if (rc == 1 && m->type != MSG_WAKE) return 1;
+    }
+}
+
 // Send a request and wait for the reply carrying the same seq.
 int rpc(Msg &req, Msg *reply, int timeout_ms) {
     State &s = S();
     req.seq = ++s.seq;
-    if (s.chan.send(&req, kMsgBytes, timeout_ms) != 1) OCM_FAIL(-1, "mailbox send to daemon failed");
-    // A reply usually lands within a few microseconds: poll for it (bounded,
-    // OCM_RPC_SPIN_US) before sleeping in poll(2), which adds a wake-up.
-    if (s.rpc_spin_ns) {
-        const uint64_t t0 = now_ns();
-        do {
-            const int rc = s.chan.recv(reply, kMsgBytes, 0);
-            if (rc < 0) return -1;
-            if (rc == 1) {
-                if (reply->seq == req.seq && reply->type != MSG_EXTENT) return 0;
-                OCM_LOG("dropping stale reply %s seq %llu", msg_type_str(reply->type), (unsigned long long)reply->seq);
-            }
-        } while (now_ns() - t0 < s.rpc_spin_ns);
+    int sent = 0;
+    if (req.type == MSG_CONNECT && s.link.ok()) {
+        // Offer the shared-memory link with the CONNECT (SCM_RIGHTS).
+        sent = mbox_send_fd(s.chan.fd(), &req, kMsgBytes, s.link.fd(), timeout_ms);
+    } else if (s.link.ok() && req.type != MSG_CONNECT && req.type != MSG_SLAB_FD && s.link.post_request(req)) {
+        sent = 1;
+        s.ctr.n_link_rpc++;
+        if (s.link.request_needs_wake()) {  // the daemon sleeps: a wake-up on the socket
+            Msg w = new_msg(MSG_WAKE);
+            sent = s.chan.send(&w, kMsgBytes, timeout_ms);
+            s.ctr.n_link_wake++;
+        }
+    } else {
+        sent = s.chan.send(&req, kMsgBytes, timeout_ms);
     }
+    if (sent != 1) OCM_FAIL(-1, "mailbox send to daemon failed");
+    // A reply usually lands within a few microseconds: poll for it (bounded,
+    // OCM_RPC_SPIN_US) before sleeping, which adds a wake-up.
     const long deadline = now_ms() + timeout_ms;
+    uint64_t spin = s.rpc_spin_ns;
     for (;;) {
-        long left = deadline - now_ms();
-        if (left <= 0) OCM_FAIL(-1, "daemon did not answer %s within %d ms", msg_type_str(req.type), timeout_ms);
-        int rc = s.chan.recv(reply, kMsgBytes, (int)std::min<long>(left, 1000));
+        const int rc = recv_record(reply, deadline, spin);
+        spin = 0;
         if (rc < 0) return -1;
-        if (rc == 0) continue;
+        if (rc == 0) OCM_FAIL(-1, "daemon did not answer %s within %d ms", msg_type_str(req.type), timeout_ms);
         if (reply->seq == req.seq && reply->type != MSG_EXTENT) return 0;
         OCM_LOG("dropping stale reply %s seq %llu", msg_type_str(reply->type), (unsigned long long)reply->seq);
     }
@@ -68,11 +114,10 @@ int rpc(Msg &req, Msg *reply, int timeout_ms) {
 int recv_seq(Msg *m, uint64_t seq, uint32_t type, int timeout_ms) {
     const long deadline = now_ms() + timeout_ms;
     for (;;) {
-        long left = deadline - now_ms();
-        if (left <= 0) OCM_FAIL(-1, "timed out waiting for %s", msg_type_str(type));
-        int rc = S().chan.recv(m, kMsgBytes, (int)std::min<long>(left, 1000));
+        const int rc = recv_record(m, deadline, S().rpc_spin_ns);
         if (rc < 0) return -1;
-        if (rc == 1 && m->seq == seq && m->type == type) return 0;
+        if (rc == 0) OCM_FAIL(-1, "timed out waiting for %s", msg_type_str(type));
+        if (m->seq == seq && m->type == type) return 0;
     }
 }
 

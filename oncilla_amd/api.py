@@ -228,7 +228,7 @@ def last_error() -> str:
 
 COUNTER_KEYS = ["n_put", "n_get", "bytes_put", "bytes_get", "n_alloc", "n_free", "n_copy", "bytes_copy", "ns_put",
                 "ns_get", "ns_alloc", "ns_free", "n_batch", "n_batch_ops", "bytes_batch", "ns_batch",
-                "n_batch_launches", "n_slab_fd", "n_slab_path"]
+                "n_batch_launches", "n_slab_fd", "n_slab_path", "n_link_rpc", "n_link_wake"]
 OCM_BATCH_ASYNC = 1
 
 

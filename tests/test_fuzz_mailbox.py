@@ -302,3 +302,89 @@ def test_other_users_get_no_slab_fds(mesh_factory, monkeypatch):
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=30)
         assert r.stdout.split() == ["13", "0"], r.stdout + r.stderr  # EACCES, no fd attached
         a.free()
+
+
+def _hostile_link(kind):
+    """A memfd offered as a shared-memory link that the daemon must refuse (or
+    survive): unsealed, the wrong size, or sealed and valid but with garbage
+    ring counters and records."""
+    import mmap
+
+    size = 4096 * 8  # not the layout's size
+    fd = os.memfd_create("hostile", os.MFD_ALLOW_SEALING)
+    if kind == "unsealed":
+        os.ftruncate(fd, 28672)
+    elif kind == "size":
+        os.ftruncate(fd, size)
+        fcntl_seal(fd)
+    return fd
+
+
+def fcntl_seal(fd):
+    import fcntl
+
+    F_ADD_SEALS, F_SEAL_SEAL, F_SEAL_SHRINK, F_SEAL_GROW = 1033, 1, 2, 4
+    fcntl.fcntl(fd, F_ADD_SEALS, F_SEAL_SEAL | F_SEAL_SHRINK | F_SEAL_GROW)
+
+
+@pytest.mark.parametrize("kind", ["unsealed", "size"])
+def test_daemon_refuses_hostile_shared_memory_links(mesh_factory, kind):
+    """Any local process can offer a link with MSG_CONNECT; the daemon maps only a
+    memfd sealed against resizing at exactly the layout's size (else its next
+    access could SIGBUS), answers on the socket instead, and keeps serving."""
+    m = mesh_factory(1)
+    s = _connect(m.ns)
+    s.setblocking(True)
+    s.settimeout(5)
+    fd = _hostile_link(kind)
+    s.sendmsg([MSG.pack(1, 1, 0, 0, 5, -1, 0, b"\0" * 128)], [(socket.SOL_SOCKET, socket.SCM_RIGHTS, struct.pack("i", fd))])
+    os.close(fd)
+    data = s.recv(160)  # the CONNECT_CONFIRM came over the socket: no link was attached
+    t, _, _, _, seq = MSG.unpack(data)[:5]
+    assert t == 2 and seq == 5
+    s.close()
+    assert "unusable shared-memory link" in m.logs()
+    with api.Client(daemon_rank=0, ns=m.ns) as c:  # still serving, over a proper link
+        c.alloc(api.OCM_LOCAL_HOST, local_bytes=4096).free()
+        assert api.counters()["n_link_rpc"] > 0
+
+
+def test_daemon_survives_garbage_in_a_valid_link(mesh_factory):
+    """A sealed link of the right layout whose app then scribbles over the ring
+    counters and records: the daemon bounds what it reads, copies records out
+    before looking at them, and stays up for everyone else."""
+    import mmap
+
+    m = mesh_factory(1)
+    code = textwrap.dedent(f"""
+        import ctypes, mmap, os, random, sys, time
+        sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})
+        os.environ["OCM_NO_GPU"] = "1"
+        from oncilla_amd import api
+        c = api.Client(daemon_rank=0, ns={m.ns!r})
+        c.init()
+        c.alloc(api.OCM_LOCAL_HOST, local_bytes=4096).free()
+        # find our link's mapping (the memfd named ocm_link) and scribble over it
+        for line in open("/proc/self/maps"):
+            if "memfd:ocm_link" in line:
+                lo, hi = (int(x, 16) for x in line.split()[0].split("-"))
+                break
+        rng = random.Random(3)
+        buf = (ctypes.c_char * (hi - lo)).from_address(lo)
+        for _ in range(2000):
+            off = rng.randrange(0, hi - lo - 8)
+            ctypes.memmove(lo + off, os.urandom(8), 8)
+        time.sleep(0.3)
+        os._exit(0)
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert m.daemons[0].alive()
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)
+        a.fill(seed=3)
+        a.put(0, 0, 1 << 20)
+        a.fill(seed=0)
+        a.get(0, 0, 1 << 20)
+        assert a.check(seed=3) == 0
+        a.free()

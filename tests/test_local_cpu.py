@@ -178,3 +178,29 @@ def test_prometheus_metrics_exporter(mesh_factory, monkeypatch):
         assert f'oncilla_up{{rank="{r}"}} 1' in text
         assert f'oncilla_host_capacity{{rank="{r}",gpu="-1"}}' in text
     assert "# TYPE oncilla_n_alloc gauge" in text
+
+
+def test_shared_memory_link_carries_the_rpcs_and_survives_idle_daemons(mesh_factory, monkeypatch):
+    """The app's shared-memory link (ocm/shmlink.h) carries the RPCs; when the
+    daemon has gone to sleep between requests the app wakes it over the socket,
+    and when the app sleeps the daemon wakes it. Every round trip completes, with
+    and without the link (OCM_SHM_LINK=0: the mailbox alone)."""
+    import time
+
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    for link in ("1", "0"):
+        monkeypatch.setenv("OCM_SHM_LINK", link)
+        m = mesh_factory(2)
+        with api.Client(daemon_rank=0, ns=m.ns) as c:
+            before = api.counters()
+            for i in range(40):
+                a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20)
+                a.free()
+                if i % 4 == 3:
+                    time.sleep(0.002)  # past the daemon's 50 us spin: the next request must wake it
+            after = api.counters()
+            if link == "1":
+                assert after["n_link_rpc"] - before["n_link_rpc"] >= 80
+                assert after["n_link_wake"] - before["n_link_wake"] >= 10
+            else:
+                assert after["n_link_rpc"] == before["n_link_rpc"]

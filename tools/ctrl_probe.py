@@ -22,18 +22,21 @@ from oncilla_amd.parallel import Mesh  # noqa: E402
 def run(ctrl, tick_self, **extra_env):
     env = {"OCM_LEASE_BYTES": "0", **extra_env}
     # OCM_PIN is read by the daemon (from env) and by this process's libocm (os.environ)
-    saved = os.environ.get("OCM_PIN")
+    app_keys = ("OCM_PIN", "OCM_RPC_SPIN_US")  # read by this process's libocm too
+    saved = {k: os.environ.get(k) for k in app_keys}
     mask = os.sched_getaffinity(0)  # a pinned variant must not leave this thread pinned for the next
-    if "OCM_PIN" in extra_env:
-        os.environ["OCM_PIN"] = extra_env["OCM_PIN"]
+    for k in app_keys:
+        if k in extra_env:
+            os.environ[k] = extra_env[k]
     try:
         return _run(ctrl, tick_self, env)
     finally:
         os.sched_setaffinity(0, mask)
-        if saved is None:
-            os.environ.pop("OCM_PIN", None)
-        else:
-            os.environ["OCM_PIN"] = saved
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def _run(ctrl, tick_self, env):
@@ -81,6 +84,8 @@ VARIANTS = {
     "rccl_seal2_loop_pin": ("rccl", True, {"OCM_TICK_SEAL_SPEC": "0", "OCM_TICK_CPUS": "loop", "OCM_PIN": "1"}),
     "rccl_spec_nopin": ("rccl", True, {"OCM_PIN": "0"}),
     "tcp_pin": ("tcp", False, {"OCM_PIN": "1"}),
+    # the app's reply spin and the daemon's post-activity spin at 300 us (default 50)
+    "rccl_spec_ccd_spin300": ("rccl", True, {"OCM_RPC_SPIN_US": "300", "OCM_DAEMON_SPIN_US": "300"}),
 }
 
 
