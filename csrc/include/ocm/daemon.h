@@ -83,6 +83,7 @@ private:
         bool watching_out = false;
         std::shared_ptr<ShmLink> link;  // shared-memory fast path (ocm/shmlink.h), if the app offered one
         std::deque<Msg> link_backlog;   // replies waiting for room in the link's ring
+        bool overflowed = false;        // its replies piled up past kAppBacklogMax: being dropped
     };
     struct AppConn {
         int fd = -1;
@@ -166,6 +167,14 @@ private:
     void links_polling(bool on);
     bool links_polling_ = true;
     int pending_link_fd_ = -1;  // a link memfd that arrived with MSG_CONNECT, for app_connect
+    // An app that never takes its replies (socket or link) must not grow the
+    // daemon without bound: past this many queued replies it is disconnected
+    // and its memory reclaimed, as if it had died.
+    static constexpr size_t kAppBacklogMax = 4096;
+    std::vector<pid_t> overflowed_apps_;
+    std::vector<pid_t> link_pids_;  // poll_links scratch
+    void reap_overflowed_apps();
+    void app_overflowed(App &a);
     // Once a tick transport exists, the allocation protocol's records are
     // remembered by content: when the transport fails, a sender re-sends over TCP
     // every record it cannot prove delivered (TickTransport::take_unsent), and a

@@ -411,6 +411,7 @@ int Daemon::loop() {
         // Apps' shared-memory links are looked at on every pass: while the loop
         // is awake (its post-activity spin) their requests need no wake-up.
         if (poll_links() > 0) last_event_ns = now_ns();
+        if (!overflowed_apps_.empty()) reap_overflowed_apps();
         const bool spinning = spin_ns && now_ns() - last_event_ns < spin_ns;
         int wait_ms = (self_q_.empty() && !spinning) ? timeout : 0;
         if (wait_ms > 0) {
@@ -674,12 +675,32 @@ void Daemon::send_tcp(int r, Msg &m) {
     if (c.want_write) ep_mod(fd, EPOLLIN | EPOLLOUT, tag(T_CONN, (uint64_t)fd));
 }
 
+void Daemon::app_overflowed(App &a) {
+    if (a.overflowed) return;
+    a.overflowed = true;
+    OCM_WARN("rank %d: app %d does not take its replies (%zu queued); disconnecting it", rank_, (int)a.pid,
+             kAppBacklogMax);
+    overflowed_apps_.push_back(a.pid);
+}
+
+void Daemon::reap_overflowed_apps() {
+    // Outside any handler: closing the connection reclaims the app's memory.
+    std::vector<pid_t> pids;
+    pids.swap(overflowed_apps_);
+    for (pid_t pid : pids) {
+        auto it = apps_.find(pid);
+        if (it == apps_.end() || !it->second.overflowed) continue;
+        if (it->second.fd >= 0) close_app_conn(it->second.fd);
+        else app_disconnect(pid, true);
+    }
+}
+
 int Daemon::poll_links() {
     int n = 0;
-    std::vector<pid_t> with_links;
+    link_pids_.clear();
     for (auto &kv : apps_)
-        if (kv.second.link) with_links.push_back(kv.first);
-    for (pid_t pid : with_links) {
+        if (kv.second.link) link_pids_.push_back(kv.first);
+    for (pid_t pid : link_pids_) {
         auto it = apps_.find(pid);
         if (it == apps_.end() || !it->second.link) continue;
         std::shared_ptr<ShmLink> link = it->second.link;  // stays mapped if the app goes away meanwhile
@@ -731,9 +752,15 @@ void Daemon::send_app(pid_t pid, const Msg &m) {
                 w.rank = rank_;
                 send_app(pid, w);
             }
-        } else {
+        } else if (a.link_backlog.size() < kAppBacklogMax) {
             a.link_backlog.push_back(m);  // drained by poll_links
+        } else {
+            app_overflowed(a);
         }
+        return;
+    }
+    if (a.backlog.size() >= kAppBacklogMax) {
+        app_overflowed(a);
         return;
     }
     if (a.backlog.empty()) {

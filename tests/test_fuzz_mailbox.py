@@ -349,37 +349,96 @@ def test_daemon_refuses_hostile_shared_memory_links(mesh_factory, kind):
         assert api.counters()["n_link_rpc"] > 0
 
 
-def test_daemon_survives_garbage_in_a_valid_link(mesh_factory):
-    """A sealed link of the right layout whose app then scribbles over the ring
-    counters and records: the daemon bounds what it reads, copies records out
-    before looking at them, and stays up for everyone else."""
+# ocm/shmlink.h ShmLinkLayout (offsets checked by the native unit tests' static layout)
+LINK_BYTES, LINK_REQ_HEAD, LINK_REQ_TAIL, LINK_RSP_HEAD, LINK_RSP_TAIL = 24576, 64, 128, 192, 256
+LINK_POLLING, LINK_WAITING, LINK_REQ, LINK_RSP, LINK_SLOTS = 320, 384, 448, 10688, 64
+MSG_WAKE = 26
+
+
+def _raw_link(ns, seq=5):
+    """Connect like libocm does, but with a link this process owns: a sealed memfd
+    of the layout, offered with MSG_CONNECT. Returns (socket, mmap)."""
     import mmap
 
+    fd = os.memfd_create("ocm_link", os.MFD_ALLOW_SEALING)
+    os.ftruncate(fd, LINK_BYTES)
+    fcntl_seal(fd)
+    mm = mmap.mmap(fd, LINK_BYTES)
+    struct.pack_into("<II", mm, 0, 0x4F434D4C, LINK_SLOTS)
+    s = _connect(ns)
+    s.setblocking(True)
+    s.settimeout(5)
+    s.sendmsg([MSG.pack(1, 1, 0, 0, seq, -1, 0, b"\0" * 128)],
+              [(socket.SOL_SOCKET, socket.SCM_RIGHTS, struct.pack("i", fd))])
+    os.close(fd)
+    return s, mm
+
+
+def _link_reply(s, mm, timeout=5.0):
+    """The next reply, from the link's reply ring (or the socket)."""
+    import select
+    import time
+
+    end = time.time() + timeout
+    while time.time() < end:
+        head, tail = struct.unpack_from("<Q", mm, LINK_RSP_HEAD)[0], struct.unpack_from("<Q", mm, LINK_RSP_TAIL)[0]
+        if head != tail:
+            off = LINK_RSP + (tail % LINK_SLOTS) * 160
+            rec = bytes(mm[off:off + 160])
+            struct.pack_into("<Q", mm, LINK_RSP_TAIL, tail + 1)
+            return MSG.unpack(rec)
+        if select.select([s], [], [], 0.001)[0]:
+            data = s.recv(160)
+            if len(data) == 160 and MSG.unpack(data)[0] != MSG_WAKE:
+                return MSG.unpack(data)
+    raise TimeoutError("no reply on the link or the socket")
+
+
+def _post(s, mm, rec):
+    head = struct.unpack_from("<Q", mm, LINK_REQ_HEAD)[0]
+    off = LINK_REQ + (head % LINK_SLOTS) * 160
+    mm[off:off + 160] = rec
+    struct.pack_into("<Q", mm, LINK_REQ_HEAD, head + 1)
+    s.send(MSG.pack(MSG_WAKE, 1, 0, 0, 0, -1, 0, b"\0" * 128))
+
+
+def test_link_carries_requests_and_the_daemon_survives_garbage_in_it(mesh_factory):
+    """A valid link driven by hand: the CONNECT_CONFIRM and a PING's reply come back
+    on the reply ring. Then the app scribbles: random records, request heads far
+    ahead of the tail or behind it, a reply tail past the head. The daemon bounds
+    what it reads, copies records out before looking at them, and keeps serving
+    other apps; a fresh link on a new connection still works."""
+    import random
+
     m = mesh_factory(1)
-    code = textwrap.dedent(f"""
-        import ctypes, mmap, os, random, sys, time
-        sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})
-        os.environ["OCM_NO_GPU"] = "1"
-        from oncilla_amd import api
-        c = api.Client(daemon_rank=0, ns={m.ns!r})
-        c.init()
-        c.alloc(api.OCM_LOCAL_HOST, local_bytes=4096).free()
-        # find our link's mapping (the memfd named ocm_link) and scribble over it
-        for line in open("/proc/self/maps"):
-            if "memfd:ocm_link" in line:
-                lo, hi = (int(x, 16) for x in line.split()[0].split("-"))
-                break
-        rng = random.Random(3)
-        buf = (ctypes.c_char * (hi - lo)).from_address(lo)
-        for _ in range(2000):
-            off = rng.randrange(0, hi - lo - 8)
-            ctypes.memmove(lo + off, os.urandom(8), 8)
-        time.sleep(0.3)
-        os._exit(0)
-    """)
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 0, r.stderr
+    s, mm = _raw_link(m.ns)
+    t, _, _, _, seq = _link_reply(s, mm)[:5]
+    assert (t, seq) == (2, 5)
+    _post(s, mm, MSG.pack(18, 1, 0, 0, 77, -1, 0, b"\0" * 128))  # MSG_PING
+    rep = _link_reply(s, mm)
+    assert rep[4] == 77
+    rng = random.Random(7)
+    for i in range(400):
+        k = i % 4
+        if k == 0:  # a random record, properly posted
+            _post(s, mm, bytes(rng.getrandbits(8) for _ in range(160)))
+        elif k == 1:  # a head far ahead of the tail
+            struct.pack_into("<Q", mm, LINK_REQ_HEAD, rng.getrandbits(64))
+            s.send(MSG.pack(MSG_WAKE, 1, 0, 0, 0, -1, 0, b"\0" * 128))
+        elif k == 2:  # a reply tail past the head (the daemon must not overrun the ring)
+            struct.pack_into("<Q", mm, LINK_RSP_TAIL, rng.getrandbits(64))
+            _post(s, mm, MSG.pack(18, 1, 0, 0, 1000 + i, -1, 0, b"\0" * 128))
+        else:  # garbage over the records themselves
+            off = LINK_REQ + rng.randrange(0, LINK_SLOTS * 160 - 8)
+            mm[off:off + 8] = os.urandom(8)
+            s.send(MSG.pack(MSG_WAKE, 1, 0, 0, 0, -1, 0, b"\0" * 128))
+    s.close()
+    mm.close()
     assert m.daemons[0].alive()
+    s2, mm2 = _raw_link(m.ns, seq=9)
+    assert _link_reply(s2, mm2)[4] == 9
+    s2.close()
+    mm2.close()
     with api.Client(daemon_rank=0, ns=m.ns) as c:
         a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)
         a.fill(seed=3)
@@ -388,3 +447,53 @@ def test_daemon_survives_garbage_in_a_valid_link(mesh_factory):
         a.get(0, 0, 1 << 20)
         assert a.check(seed=3) == 0
         a.free()
+
+
+@pytest.mark.parametrize("path", ["socket", "link"])
+def test_an_app_that_never_takes_its_replies_is_disconnected(mesh_factory, path):
+    """Requests whose replies the app never reads (a full socket, or a link whose
+    reply ring it has jammed) pile up in the daemon. Past a bound the daemon drops
+    the app as if it had died, instead of growing without limit."""
+    import time
+
+    m = mesh_factory(1)
+    ping = MSG.pack(18, 1, 0, 0, 1, -1, 0, b"\0" * 128)
+    if path == "socket":
+        s = _connect(m.ns)
+        s.setblocking(True)
+        s.settimeout(5)
+        s.send(MSG.pack(1, 1, 0, 0, 5, -1, 0, b"\0" * 128))
+        try:
+            for _ in range(6000):
+                s.send(ping)
+        except (ConnectionResetError, BrokenPipeError):
+            pass  # dropped already
+    else:
+        s, mm = _raw_link(m.ns)
+        assert _link_reply(s, mm)[4] == 5
+        struct.pack_into("<Q", mm, LINK_RSP_TAIL, 1 << 40)  # the reply ring looks full forever
+        sent = 0
+        end = time.time() + 30
+        try:
+            while sent < 6000 and time.time() < end:
+                head = struct.unpack_from("<Q", mm, LINK_REQ_HEAD)[0]
+                if head - struct.unpack_from("<Q", mm, LINK_REQ_TAIL)[0] < LINK_SLOTS:
+                    _post(s, mm, ping)
+                    sent += 1
+        except (ConnectionResetError, BrokenPipeError):
+            pass  # dropped already
+        assert sent > 4096
+    end = time.time() + 20
+    while time.time() < end and "does not take its replies" not in m.logs():
+        time.sleep(0.05)
+    assert "does not take its replies" in m.logs()
+    s.settimeout(5)
+    try:
+        while s.recv(160):  # queued replies, then EOF
+            pass
+    except ConnectionResetError:
+        pass
+    s.close()
+    assert m.daemons[0].alive()
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        c.alloc(api.OCM_LOCAL_HOST, local_bytes=4096).free()
