@@ -50,6 +50,9 @@ struct TickSlot {
     uint32_t count;    // records used in this slot
     uint32_t busy;     // sender still has queued records (keep ticking)
     uint64_t first;    // device-sealed slots: ring index of rec[0] (the sender's progress)
+    uint64_t tick;     // device-sealed slots: the tick number the seal ran for
+    uint64_t tag;      // device-sealed slots: tick_slot_tag() of this slot, so a receiver that
+                       // reads the gathered slots in place can tell a whole copy from one in flight
     TickRecord rec[kTickMsgs];
 };
 static_assert(sizeof(TickRecord) == 168, "tick record layout");
@@ -87,9 +90,37 @@ inline uint64_t tick_record_tag(const uint64_t *w, uint64_t j) {
     return h;
 }
 
+// Tag of a sealed slot: its header, its tick number, and the XOR of its records'
+// tick_record_tag()s (record r at ring index first + r). Whoever reads the
+// gathered slots while the collective may still be writing them (the tick
+// thread polls them in mapped host memory instead of waiting for a done kernel)
+// takes a slot only when its tick and tag match.
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint64_t tick_slot_tag(uint32_t count, uint32_t busy, uint64_t first, uint64_t tick, uint64_t rec_xor) {
+    uint64_t h = (tick + 0x51ull) * 0x9E3779B97F4A7C15ull;
+    h ^= (((uint64_t)count << 32) | busy) * 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 31;
+    h ^= first * 0x94D049BB133111EBull;
+    h ^= h >> 29;
+    h ^= rec_xor;
+    h *= 0xBF58476D1CE4E5B9ull;
+    return h ^ (h >> 32);
+}
+// Host: `s` (a private copy) is the whole slot sealed for tick `tick`.
+bool tick_slot_whole(const TickSlot &s, uint64_t tick);
+// Host: what tick_seal_kernel stores into a slot's tick/tag fields.
+void tick_slot_seal_tag(TickSlot *s, uint64_t tick);
+
 // Queue the seal of one tick on `stream`: *consumed (device memory, only this
 // stream touches it) -> slot->first, up to kTickMsgs records of `ring` -> slot.
-hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, hipStream_t stream);
+// `tick`: the tick's number (stored with the slot's tag). `wait_us`: when the
+// ring holds nothing unsent, the seal polls it for up to this long before it
+// seals an empty slot, so a record the host posts right after the previous
+// tick completed still rides this one (OCM_TICK_SEAL_WAIT_US).
+hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, uint64_t tick, uint32_t wait_us,
+                            hipStream_t stream);
 // Queue a one-lane kernel that stores `seq` to `flag` (pinned, device-mapped
 // host memory) at system scope: the host sees a tick end ~6 us sooner than
 // through an event query (tools/launch_probe.hip, profiles/launch_flag_r01.json).
@@ -143,6 +174,9 @@ public:
     bool post(int dest, const Msg &m);
     // Records delivered to this rank (drained by the event loop).
     std::vector<Msg> drain();
+    // drain() has records: a spinning event loop looks here on every pass rather
+    // than waiting for epoll to report the eventfd.
+    bool has_input() const { return in_ready_.load(std::memory_order_acquire); }
     // Readable when drain() has records, a wake-up must be announced, or the
     // transport failed.
     int event_fd() const { return efd_; }
@@ -167,7 +201,7 @@ private:
     std::condition_variable cv_;
     std::deque<TickRecord> out_;
     std::vector<Msg> in_;
-    std::atomic<bool> stop_{false}, failed_{false}, announce_{false}, up_{false};
+    std::atomic<bool> stop_{false}, failed_{false}, announce_{false}, up_{false}, in_ready_{false};
     std::atomic<uint64_t> ticks_{0}, wake_upto_{0}, announce_tick_{0};
     TickRing *ring_ = nullptr;  // device-sealed collectives: their outbox (under mu_)
     uint64_t ring_sent_ = 0;    // ring records a completed tick of ours carried

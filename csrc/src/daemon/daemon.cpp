@@ -411,6 +411,10 @@ int Daemon::loop() {
         // Apps' shared-memory links are looked at on every pass: while the loop
         // is awake (its post-activity spin) their requests need no wake-up.
         if (poll_links() > 0) last_event_ns = now_ns();
+        if (tick_ && tick_->has_input()) {  // delivered by the tick thread: no epoll round
+            on_tick();
+            last_event_ns = now_ns();
+        }
         if (!overflowed_apps_.empty()) reap_overflowed_apps();
         const bool spinning = spin_ns && now_ns() - last_event_ns < spin_ns;
         int wait_ms = (self_q_.empty() && !spinning) ? timeout : 0;

@@ -26,6 +26,40 @@ namespace ocm {
 
 namespace {
 
+uint64_t slot_rec_xor(const TickSlot &s, uint32_t n) {
+    uint64_t x = 0;
+    for (uint32_t r = 0; r < n; r++)
+        x ^= tick_record_tag(reinterpret_cast<const uint64_t *>(&s.rec[r]), s.first + (uint64_t)r);
+    return x;
+}
+
+}  // namespace
+
+bool tick_slot_whole(const TickSlot &s, uint64_t tick) {
+    if (s.tick != tick || s.count > (uint32_t)kTickMsgs) return false;
+    return tick_slot_tag(s.count, s.busy, s.first, s.tick, slot_rec_xor(s, s.count)) == s.tag;
+}
+
+void tick_slot_seal_tag(TickSlot *s, uint64_t tick) {
+    s->tick = tick;
+    s->tag = tick_slot_tag(s->count, s->busy, s->first, tick, slot_rec_xor(*s, std::min<uint32_t>(s->count, kTickMsgs)));
+}
+
+namespace {
+
+// Every rank's slot of a gathered tick, read in place while the collective may
+// still be writing it: whole copies of the slots sealed for `tick`?
+bool gathered_whole(const void *recv, int n, uint64_t tick) {
+    const TickSlot *g = static_cast<const TickSlot *>(recv);
+    for (int k = 0; k < n; k++) {
+        if (__atomic_load_n(&g[k].tick, __ATOMIC_ACQUIRE) != tick) return false;
+        TickSlot copy;
+        std::memcpy(&copy, &g[k], sizeof(copy));
+        if (!tick_slot_whole(copy, tick)) return false;
+    }
+    return true;
+}
+
 // RCCL over xGMI: a ring of depth() tick slots, one ncclAllGather per tick on
 // one stream, an event per slot for completion.
 //
@@ -93,6 +127,15 @@ public:
         };
         mapped_ = flag("OCM_TICK_MAPPED", true);
         sealed_ = flag("OCM_TICK_SEAL", true) && bytes == sizeof(TickSlot);
+        // Completion seen in the gathered slots themselves (tick number + tag, read in
+        // mapped host memory) instead of a done kernel after each collective.
+        // Measured (1 daemon, records to itself, profiles/ctrl_probe_r03_tagged.json): alloc p50
+        // 28.3-29.1 us with tagged slots and a 6 us seal wait, against 36-78 us (bimodal) with a done
+        // kernel and no wait; the wait is what removes the slow mode (a record posted just after a
+        // tick completed had missed the already-running seal of the next one and waited a whole tick).
+        done_kernel_ = flag("OCM_TICK_DONE_KERNEL", false) || !sealed_ || !mapped_;
+        const char *wv = std::getenv("OCM_TICK_SEAL_WAIT_US");
+        wait_us_ = wv && *wv ? (uint32_t)std::max(0, std::atoi(wv)) : 6;
         const char *d = std::getenv("OCM_TICK_DEPTH");
         const int depth = std::max(1, std::min(d && *d ? std::atoi(d) : (sealed_ ? 2 : 1), 64));
         if (hipSetDevice(gpu) != hipSuccess || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
@@ -168,9 +211,11 @@ public:
         if (aborted_) return -1;
         Slot &sl = ring_[(size_t)i];
         (void)hipSetDevice(gpu_);
+        const uint64_t seq = started_ + 1;
         if (sealed_) {
             if (!out_dev_ || !consumed_ || !sl.dsend || !sl.drecv || !done_dev_) return why("tick slots missing");
-            const hipError_t e = tick_seal_launch(out_dev_, consumed_, static_cast<TickSlot *>(sl.dsend), stream_);
+            const hipError_t e =
+                tick_seal_launch(out_dev_, consumed_, static_cast<TickSlot *>(sl.dsend), seq, wait_us_, stream_);
             if (e != hipSuccess) return why(std::string("seal launch: ") + hipGetErrorString(e));
         } else if (!mapped_ && hipMemcpyAsync(sl.dsend, sl.hsend, bytes_, hipMemcpyHostToDevice, stream_) != hipSuccess) {
             return -1;
@@ -180,8 +225,10 @@ public:
         if (!mapped_ && hipMemcpyAsync(sl.hrecv, sl.drecv, bytes_ * (size_t)n_, hipMemcpyDeviceToHost, stream_) != hipSuccess)
             return -1;
         sl.seq = ++started_;
-        const hipError_t de = tick_done_launch(done_dev_, sl.seq, stream_);
-        if (de != hipSuccess) return why(std::string("done launch: ") + hipGetErrorString(de));
+        if (done_kernel_) {
+            const hipError_t de = tick_done_launch(done_dev_, sl.seq, stream_);
+            if (de != hipSuccess) return why(std::string("done launch: ") + hipGetErrorString(de));
+        }
         if (ring_.size() == 1) return 0;
         return hipEventRecord(sl.ev, stream_) == hipSuccess ? 0 : -1;
     }
@@ -193,7 +240,9 @@ public:
             return why("aborted");
         }
         // The tick's done kernel stored its sequence number: seen without a runtime call.
-        if (__atomic_load_n(done_, __ATOMIC_ACQUIRE) >= ring_[(size_t)i].seq) return 1;
+        if (done_kernel_ ? __atomic_load_n(done_, __ATOMIC_ACQUIRE) >= ring_[(size_t)i].seq
+                         : gathered_whole(ring_[(size_t)i].hrecv, n_, ring_[(size_t)i].seq))
+            return 1;
         if ((++polls_ & 255) != 0) return 0;
         // Backstop every 256 polls: the runtime's view (errors surface here), and
         // RCCL's async error (a dead peer never joins the collective).
@@ -226,7 +275,8 @@ private:
     };
     int gpu_ = 0, n_ = 1;
     size_t bytes_ = 0;
-    bool mapped_ = true, sealed_ = true;
+    bool mapped_ = true, sealed_ = true, done_kernel_ = true;
+    uint32_t wait_us_ = 0;
     unsigned polls_ = 0;
     ncclComm_t comm_ = nullptr;
     hipStream_t stream_ = nullptr;
@@ -307,6 +357,7 @@ public:
             slot->busy = pending > n ? 1u : 0u;
             slot->first = consumed_;
             consumed_ += n;
+            tick_slot_seal_tag(slot, ++ticks_);
         }
         if (stall_after_ > 0 && ++started_ >= (uint64_t)stall_after_) {
             while (!aborted_) usleep(1000);  // wedged until the transport is torn down
@@ -325,6 +376,12 @@ public:
     }
     int test(int) override {
         if (aborted_) return -1;
+        // Sealed emulation: every gathered slot must check out as the RCCL path's
+        // done-kernel-less completion requires (same tags, computed on the host).
+        if (outbox_ && !gathered_whole(recv_.data(), n_, ticks_)) {
+            error_ = "gathered tick slot failed its tag check";
+            return -1;
+        }
         if (fault_do_alloc_ && !fault_fired_) {
             // OCM_TICK_FAULT=fail_after_do_alloc (tests): the tick that carried one of
             // our DO_ALLOC requests reached every peer, then fails here, so the
@@ -386,6 +443,7 @@ private:
     bool fault_do_alloc_ = false, fault_fired_ = false;
     long long stall_after_ = 0;
     uint64_t started_ = 0;
+    uint64_t ticks_ = 0;  // sealed emulation: ticks sealed so far
     long timeout_ms_ = 5000;
     std::string error_;
 };
@@ -517,6 +575,7 @@ std::vector<Msg> TickTransport::drain() {
     std::lock_guard<std::mutex> lk(mu_);
     std::vector<Msg> out;
     out.swap(in_);
+    in_ready_.store(false, std::memory_order_relaxed);
     return out;
 }
 
@@ -700,6 +759,7 @@ void TickTransport::run() {
                         delivered++;
                     }
             }
+            if (delivered) in_ready_.store(true, std::memory_order_release);
         }
         done++;
         ticks_ = done;

@@ -10,6 +10,7 @@
 // stream reads the slot after this kernel ends.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -23,7 +24,18 @@ __device__ __forceinline__ uint64_t sys_load(const uint64_t *p) {
 }
 
 // Two round trips: `published` first, then the records it covers (OCM_TICK_SEAL_SPEC=0).
-__global__ __launch_bounds__(64) void tick_seal2_kernel(const TickRing *ring, uint64_t *consumed, TickSlot *slot) {
+__device__ __forceinline__ uint64_t wave_xor64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, off, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), off, 64);
+        v ^= ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(64) void tick_seal2_kernel(const TickRing *ring, uint64_t *consumed, TickSlot *slot,
+                                                       uint64_t tick) {
     const int lane = threadIdx.x;
     const uint64_t c = *consumed;  // this stream's own counter: plain load
     const uint64_t pub = sys_load(&ring->published);
@@ -35,10 +47,17 @@ __global__ __launch_bounds__(64) void tick_seal2_kernel(const TickRing *ring, ui
         uint64_t *dst = reinterpret_cast<uint64_t *>(&slot->rec[r]) + k;
         *dst = sys_load(src);
     }
+    __syncthreads();  // the slot's records, written above, are hashed below
+    uint64_t rt = 0;
+    if ((uint32_t)lane < n) rt = tick_record_tag(reinterpret_cast<const uint64_t *>(&slot->rec[lane]), c + (uint64_t)lane);
+    rt = wave_xor64(rt);
     if (lane == 0) {
+        const uint32_t busy = pending > n ? 1u : 0u;
         slot->count = n;
-        slot->busy = pending > n ? 1u : 0u;
+        slot->busy = busy;
         slot->first = c;
+        slot->tick = tick;
+        slot->tag = tick_slot_tag(n, busy, c, tick, rt);
         *consumed = c + n;
     }
 }
@@ -49,38 +68,54 @@ __global__ __launch_bounds__(64) void tick_seal2_kernel(const TickRing *ring, ui
 // host finished it (it cannot be a published one then): every record the tick
 // takes is read again after `published` is known, the two-round-trip path.
 // Measured: the seal was 2.6 us of a ~9 us tick (profiles/rocprof_tick_kernels_r02.json).
-__global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uint64_t *consumed, TickSlot *slot) {
+// With `wait` (s_memrealtime ticks, 100 MHz) the read repeats while the ring
+// holds nothing unsent, up to that long: a record the host posts just after the
+// previous tick completed then rides this tick rather than the next one.
+__global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uint64_t *consumed, TickSlot *slot,
+                                                      uint64_t tick, uint64_t wait) {
     const int lane = threadIdx.x;
     const uint64_t c = *consumed;  // this stream's own counter: plain load
     uint64_t w[kTickRecordWords];
-    uint64_t tag = 0, pub_l = 0;
+    uint64_t tag = 0, pub = 0;
     const uint64_t j = c + (uint64_t)lane;
     const uint64_t *src = reinterpret_cast<const uint64_t *>(&ring->rec[j & (kTickRing - 1)]);
-    if (lane < kTickMsgs) {
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + wait;
+    for (;;) {
+        uint64_t pub_l = 0;
+        if (lane < kTickMsgs) {
 #pragma unroll
-        for (int k = 0; k < kTickRecordWords; k++) w[k] = sys_load(src + k);
-        tag = sys_load(&ring->tag[j & (kTickRing - 1)]);
+            for (int k = 0; k < kTickRecordWords; k++) w[k] = sys_load(src + k);
+            tag = sys_load(&ring->tag[j & (kTickRing - 1)]);
+        }
+        if (lane == 63) pub_l = sys_load(&ring->published);
+        pub = ((uint64_t)__builtin_amdgcn_readlane((int)(pub_l >> 32), 63) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pub_l, 63);
+        // Uniform exit: pub is read-lane broadcast and the clock is scalar.
+        if (pub > c || wait == 0 || (int64_t)(__builtin_amdgcn_s_memrealtime() - t_end) >= 0) break;
     }
-    if (lane == 63) pub_l = sys_load(&ring->published);
-    const uint64_t pub = ((uint64_t)__builtin_amdgcn_readlane((int)(pub_l >> 32), 63) << 32) |
-                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pub_l, 63);
     const uint64_t pending = pub > c ? pub - c : 0;
     const uint32_t n = pending < (uint64_t)kTickMsgs ? (uint32_t)pending : (uint32_t)kTickMsgs;
     const bool mine = (uint32_t)lane < n;
     const bool torn = mine && tick_record_tag(w, j) != tag;
+    uint64_t rt = mine ? tag : 0;
     if (__builtin_amdgcn_ballot_w64(torn) != 0 && mine) {
 #pragma unroll
         for (int k = 0; k < kTickRecordWords; k++) w[k] = sys_load(src + k);  // published: complete now
+        rt = tick_record_tag(w, j);
     }
     if (mine) {
         uint64_t *dst = reinterpret_cast<uint64_t *>(&slot->rec[lane]);
 #pragma unroll
         for (int k = 0; k < kTickRecordWords; k++) dst[k] = w[k];
     }
+    rt = wave_xor64(rt);
     if (lane == 0) {
+        const uint32_t busy = pending > n ? 1u : 0u;
         slot->count = n;
-        slot->busy = pending > n ? 1u : 0u;
+        slot->busy = busy;
         slot->first = c;
+        slot->tick = tick;
+        slot->tag = tick_slot_tag(n, busy, c, tick, rt);
         *consumed = c + n;
     }
 }
@@ -99,16 +134,18 @@ hipError_t tick_done_launch(uint64_t *flag, uint64_t seq, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, hipStream_t stream) {
+hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, uint64_t tick, uint32_t wait_us,
+                            hipStream_t stream) {
     (void)hipGetLastError();  // report this launch, not an earlier call's error
     static const bool spec = [] {
         const char *v = std::getenv("OCM_TICK_SEAL_SPEC");
         return !(v && std::strcmp(v, "0") == 0);
     }();
+    const uint64_t wait = (uint64_t)std::min<uint32_t>(wait_us, 1000) * 100;  // s_memrealtime: 100 MHz
     if (spec)
-        hipLaunchKernelGGL(tick_seal_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot);
+        hipLaunchKernelGGL(tick_seal_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot, tick, wait);
     else
-        hipLaunchKernelGGL(tick_seal2_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot);
+        hipLaunchKernelGGL(tick_seal2_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot, tick);
     return hipGetLastError();
 }
 

@@ -140,15 +140,29 @@ def test_socket_tick_self_loop(mesh_factory):
         assert c.stats(0)["ctrl_ticks"] > 0
 
 
+RCCL_TICK_MODES = {
+    "default": {},  # tagged slots, 6 us seal wait
+    "done_kernel": {"OCM_TICK_DONE_KERNEL": "1", "OCM_TICK_SEAL_WAIT_US": "0"},
+    "done_kernel_wait": {"OCM_TICK_DONE_KERNEL": "1"},
+    "tagged_wait_seal2": {"OCM_TICK_DONE_KERNEL": "0", "OCM_TICK_SEAL_WAIT_US": "6", "OCM_TICK_SEAL_SPEC": "0"},
+    "depth3_tagged_wait": {"OCM_TICK_DEPTH": "3", "OCM_TICK_DONE_KERNEL": "0", "OCM_TICK_SEAL_WAIT_US": "4"},
+}
+
+
 @pytest.mark.gpu
-def test_rccl_tick_single_gpu(mesh_factory, monkeypatch):
+@pytest.mark.parametrize("mode", sorted(RCCL_TICK_MODES))
+def test_rccl_tick_single_gpu(mesh_factory, monkeypatch, mode):
     """ncclCommInitRank + ncclAllGather on the MI355X carry the daemon's own
-    REQ_ALLOC/DO_ALLOC/FREED records (1-rank communicator, OCM_TICK_SELF)."""
+    REQ_ALLOC/DO_ALLOC/FREED records (1-rank communicator, OCM_TICK_SELF), with a
+    done kernel per tick or with completion read from the gathered slots' tags,
+    and with the seal waiting for late records."""
     monkeypatch.delenv("OCM_NO_GPU", raising=False)
-    m = mesh_factory(1, gpus=[0], extra_args=["--ctrl", "rccl"], env={"OCM_TICK_SELF": "1"})
+    m = mesh_factory(1, gpus=[0], extra_args=["--ctrl", "rccl"], env={"OCM_TICK_SELF": "1", **RCCL_TICK_MODES[mode]})
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         _wait_tick_up(c, 1)
         before = c.stats(0)["ctrl_ticks"]
+        for _ in range(20):  # many ticks through every ring slot
+            c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=4096).free()
         for flags in (api.OCM_ALLOC_LOOPBACK, 0):
             a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=1 << 20, remote_bytes=1 << 20, flags=flags)
             a.fill(seed=1)
@@ -158,6 +172,7 @@ def test_rccl_tick_single_gpu(mesh_factory, monkeypatch):
             assert a.check(seed=1) == 0
             a.free()
         assert c.stats(0)["ctrl_ticks"] > before
+        assert c.stats(0)["ctrl"] == "rccl"  # never fell back
     assert "rccl tick transport" in m.logs()
 
 

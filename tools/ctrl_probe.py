@@ -85,6 +85,17 @@ VARIANTS = {
     "rccl_spec_nopin": ("rccl", True, {"OCM_PIN": "0"}),
     "tcp_pin": ("tcp", False, {"OCM_PIN": "1"}),
     # the app's reply spin and the daemon's post-activity spin at 300 us (default 50)
+    "rccl_r03_old": ("rccl", True, {"OCM_TICK_DONE_KERNEL": "1", "OCM_TICK_SEAL_WAIT_US": "0"}),
+    "rccl_tagged": ("rccl", True, {"OCM_TICK_DONE_KERNEL": "0"}),
+    "rccl_wait3": ("rccl", True, {"OCM_TICK_SEAL_WAIT_US": "3"}),
+    "rccl_wait6": ("rccl", True, {"OCM_TICK_SEAL_WAIT_US": "6"}),
+    "rccl_tagged_wait3": ("rccl", True, {"OCM_TICK_DONE_KERNEL": "0", "OCM_TICK_SEAL_WAIT_US": "3"}),
+    "rccl_tagged_wait6": ("rccl", True, {"OCM_TICK_DONE_KERNEL": "0", "OCM_TICK_SEAL_WAIT_US": "6"}),
+    "rccl_tagged_wait10": ("rccl", True, {"OCM_TICK_DONE_KERNEL": "0", "OCM_TICK_SEAL_WAIT_US": "10"}),
+    "rccl_tagged_wait6_d1": ("rccl", True, {"OCM_TICK_DONE_KERNEL": "0", "OCM_TICK_SEAL_WAIT_US": "6",
+                                             "OCM_TICK_DEPTH": "1"}),
+    "rccl_tagged_wait6_d3": ("rccl", True, {"OCM_TICK_DONE_KERNEL": "0", "OCM_TICK_SEAL_WAIT_US": "6",
+                                             "OCM_TICK_DEPTH": "3"}),
     "rccl_spec_ccd_spin300": ("rccl", True, {"OCM_RPC_SPIN_US": "300", "OCM_DAEMON_SPIN_US": "300"}),
 }
 
