@@ -27,6 +27,8 @@ struct AdamArgs {
     uint64_t w_off;                  // byte offset of element 0's master weight (bf16 mode, 16-byte aligned)
     uint32_t decoupled;              // 1: AdamW (p *= decay before the step; wd unused)
     float decay;                     // 1 - lr * weight_decay (AdamW)
+    uint32_t host_state;             // 1: the state is all in the pinned host tier (PCIe-bound launch shape)
+    uint32_t host_span;              // (set by the launcher) bytes of the host extent the kernel may touch
 };
 
 // Many parameters in one launch: blockIdx.y picks the tensor (descriptors ride

@@ -799,6 +799,7 @@ int ocm_x_adam_multi(ocm_alloc_t a, int count, void *const *p, const void *const
     x.c.inv_sqrt_bc2 = hp[5];
     x.c.decoupled = std::isnan(hp[6]) ? 0u : 1u;  // NaN: L2 Adam; else AdamW's weight multiplier
     x.c.decay = hp[6];
+    x.c.host_state = (!a->any_gpu && !a->any_net) ? 1u : 0u;
     x.c.bf16 = bf16 ? 1u : 0u;
     // Every tensor is checked before the first launch: a bad one never leaves
     // some parameters a step ahead of the others.
@@ -860,6 +861,7 @@ static int adam_common(ocm_alloc_t a, void *p, const void *g, uint64_t n, uint64
     x.inv_sqrt_bc2 = hp[5];
     x.decoupled = std::isnan(hp[6]) ? 0u : 1u;
     x.decay = hp[6];
+    x.host_state = (!a->any_gpu && !a->any_net) ? 1u : 0u;
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (wait_alloc(a) != 0) return -1;  // queued async ops on this allocation come first
     DeviceGuard dg(s.device);

@@ -107,7 +107,8 @@ def test_fused_adam_on_striped_and_host_tier_state(mesh_factory, flags):
 
 
 @pytest.mark.gpu
-def test_fused_adam_bf16_params_with_remote_fp32_master(mesh_factory):
+@pytest.mark.parametrize("flags", [0, api.OCM_ALLOC_HOST_TIER])
+def test_fused_adam_bf16_params_with_remote_fp32_master(mesh_factory, flags):
     """Mixed precision: bf16 parameters and gradients on the GPU, fp32 master
     weights and moments in another daemon's HBM. Oracle: torch.optim.Adam on
     fp32 copies fed the same (bf16-valued) gradients; parameters = master
@@ -121,9 +122,11 @@ def test_fused_adam_bf16_params_with_remote_fp32_master(mesh_factory):
             for r, q in zip(master_ref, mine):
                 r.copy_(q.float())
         opt_ref = torch.optim.Adam(master_ref, lr=3e-3, weight_decay=0.01)
-        opt = OffloadedAdam(mine, c, lr=3e-3, weight_decay=0.01)
+        opt = OffloadedAdam(mine, c, lr=3e-3, weight_decay=0.01, flags=flags)
         try:
             assert opt.mode == "fused" and opt.bf16
+            if flags:  # the PCIe variant of the kernel (host-tier state)
+                assert {e["tier"] for e in opt.allocs[0].remote_info()["extents"]} == {1}
             for s in range(4):
                 _grads(mine, s, "cuda:0")
                 for q in mine:
@@ -144,7 +147,8 @@ def test_fused_adam_bf16_params_with_remote_fp32_master(mesh_factory):
 
 
 @pytest.mark.gpu
-def test_fused_adamw_many_tensors_and_missing_grads(mesh_factory):
+@pytest.mark.parametrize("flags", [0, api.OCM_ALLOC_HOST_TIER])
+def test_fused_adamw_many_tensors_and_missing_grads(mesh_factory, flags):
     """More than one launch's worth of parameters (32 descriptors per launch),
     large and tiny tensors mixed, some without a gradient (skipped, like torch),
     and AdamW with lr * weight_decay == 1 (decay multiplier 0: the weights are
@@ -157,7 +161,7 @@ def test_fused_adamw_many_tensors_and_missing_grads(mesh_factory):
             ref = [torch.randn(s, generator=g).to("cuda:0").requires_grad_() for s in shapes]
             mine = [p.detach().clone().requires_grad_() for p in ref]
             opt_ref = torch.optim.AdamW(ref, lr=lr, weight_decay=wd)
-            opt = OffloadedAdamW(mine, c, lr=lr, weight_decay=wd, mode="fused")
+            opt = OffloadedAdamW(mine, c, lr=lr, weight_decay=wd, mode="fused", flags=flags)
             try:
                 for s in range(3):
                     gg = torch.Generator().manual_seed(200 + s)
@@ -213,3 +217,43 @@ def test_flatten_params_keeps_dtypes_honest():
     p = torch.ones(3, requires_grad=True)
     flat, layout = flatten_params([p])
     assert p.dtype == torch.float32 and flat.numel() == 3 and layout[0][1:] == (0, 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [0, api.OCM_ALLOC_HOST_TIER])
+def test_single_tensor_adam_matches_torch(mesh_factory, flags):
+    """Allocation.adam (ocm_x_adam, one launch for one tensor) with the moments in
+    another daemon's HBM or in the pinned host tier (the PCIe variant of the
+    kernel), a length that leaves a 3-element tail, against torch.optim.Adam."""
+    import math
+
+    m = mesh_factory(2, gpus=[0, 0])
+    n = (1 << 20) + 3
+    vec = (n + 3) // 4 * 4
+    m_off, v_off = 0, 4 * vec
+    rbytes = 8 * vec
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=rbytes, remote_bytes=rbytes, flags=flags)
+        try:
+            if flags:
+                assert {e["tier"] for e in a.remote_info()["extents"]} == {1}
+            a.local_tensor(torch.float32).zero_()
+            a.put(0, 0, rbytes)
+            g0 = torch.Generator().manual_seed(21)
+            ref = torch.randn(n, generator=g0).to("cuda:0").requires_grad_()
+            mine = ref.detach().clone()
+            lr, b1, b2, eps, wd = 2e-3, 0.9, 0.999, 1e-8, 0.05
+            opt_ref = torch.optim.Adam([ref], lr=lr, betas=(b1, b2), eps=eps, weight_decay=wd)
+            for t in range(1, 4):
+                g = torch.randn(n, generator=torch.Generator().manual_seed(100 + t)).to("cuda:0")
+                ref.grad = g.clone()
+                opt_ref.step()
+                a.adam(mine, g, m_off, v_off, (b1, b2, eps, wd, lr / (1 - b1 ** t), 1 / math.sqrt(1 - b2 ** t)))
+            torch.cuda.synchronize()
+            torch.testing.assert_close(mine.cpu(), ref.detach().cpu(), rtol=1e-5, atol=1e-6)
+            a.get(0, 0, rbytes)
+            loc = a.local_tensor(torch.float32).cpu()
+            torch.testing.assert_close(loc[:n], opt_ref.state[ref]["exp_avg"].cpu(), rtol=1e-5, atol=1e-7)
+            torch.testing.assert_close(loc[vec:vec + n], opt_ref.state[ref]["exp_avg_sq"].cpu(), rtol=1e-4, atol=1e-6)
+        finally:
+            a.free()
