@@ -452,7 +452,11 @@ hipError_t adam_remote_multi_launch(const AdamMultiArgs &a, hipStream_t stream) 
         if (a.c.bf16) span = std::max(span, t.w_off + bytes);
     }
     const bool host = a.c.host_state && host_kernel && a.c.n_ext == 1 && span < (1ull << 32);
-    if (host && host_grid > 0) gx = (unsigned)std::max<uint64_t>(1, (uint64_t)host_grid / a.count);
+    if (host && host_grid > 0) {
+        // the host grid shared like the HBM one: in proportion to the biggest tensor's part
+        const uint64_t hg = (uint64_t)((double)host_grid * (double)biggest / (double)total + 0.999);
+        gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(hg, want));
+    }
     if (force_grid > 0) gx = (unsigned)force_grid;
     if (host) {
         AdamMultiArgs h = a;
