@@ -32,12 +32,15 @@ int ShmLink::create() {
     l_ = new (p) ShmLinkLayout();
     l_->magic = kShmLinkMagic;
     l_->slots = kShmLinkSlots;
-    l_->req_head.store(0, std::memory_order_relaxed);
-    l_->req_tail.store(0, std::memory_order_relaxed);
-    l_->rsp_head.store(0, std::memory_order_relaxed);
-    l_->rsp_tail.store(0, std::memory_order_relaxed);
+    l_->req_taken.store(0, std::memory_order_relaxed);
+    l_->rsp_taken.store(0, std::memory_order_relaxed);
     l_->daemon_polling.store(0, std::memory_order_relaxed);
     l_->app_waiting.store(0, std::memory_order_relaxed);
+    for (uint32_t i = 0; i < kShmLinkSlots; i++) {
+        l_->req[i].seq.store(0, std::memory_order_relaxed);
+        l_->rsp[i].seq.store(0, std::memory_order_relaxed);
+    }
+    sent_ = got_ = peer_taken_ = 0;
     fd_ = fd;
     return 0;
 }
@@ -58,6 +61,7 @@ int ShmLink::attach(int fd) {
     }
     l_ = static_cast<ShmLinkLayout *>(p);
     fd_ = fd;
+    sent_ = got_ = peer_taken_ = 0;
     if (l_->magic != kShmLinkMagic || l_->slots != kShmLinkSlots) {
         close();
         return -1;
@@ -72,40 +76,37 @@ void ShmLink::close() {
     fd_ = -1;
 }
 
-bool ShmLink::post_request(const Msg &m) {
-    const uint64_t h = l_->req_head.load(std::memory_order_relaxed);
-    if (h - l_->req_tail.load(std::memory_order_acquire) >= kShmLinkSlots) return false;
-    std::memcpy(&l_->req[h & (kShmLinkSlots - 1)], &m, sizeof(Msg));
-    l_->req_head.store(h + 1, std::memory_order_release);
+// Record n (1-based) lives in slot (n - 1) % slots and is whole once that slot's
+// seq reads n. A producer may reuse a slot once the consumer has taken the
+// record that was there; it re-reads the consumer's count only when its cached
+// one says the ring is full. The peer may write anything anywhere in the
+// mapping: all counts are compared with unsigned wrap-around, so a bogus count
+// reads as "full" (the daemon then keeps the reply, bounded by kAppBacklogMax).
+bool ShmLink::post(ShmLinkSlot *ring, std::atomic<uint64_t> &peer_taken, const Msg &m) {
+    if (sent_ - peer_taken_ >= kShmLinkSlots) {
+        peer_taken_ = peer_taken.load(std::memory_order_acquire);
+        if (sent_ - peer_taken_ >= kShmLinkSlots) return false;
+    }
+    ShmLinkSlot &sl = ring[sent_ & (kShmLinkSlots - 1)];
+    std::memcpy(&sl.msg, &m, sizeof(Msg));
+    sl.seq.store(sent_ + 1, std::memory_order_release);
+    sent_++;
     return true;
 }
 
-bool ShmLink::take_reply(Msg *m) {
-    const uint64_t t = l_->rsp_tail.load(std::memory_order_relaxed);
-    if (l_->rsp_head.load(std::memory_order_acquire) == t) return false;
-    std::memcpy(m, &l_->rsp[t & (kShmLinkSlots - 1)], sizeof(Msg));
-    l_->rsp_tail.store(t + 1, std::memory_order_release);
+bool ShmLink::take(ShmLinkSlot *ring, std::atomic<uint64_t> &taken, Msg *m) {
+    ShmLinkSlot &sl = ring[got_ & (kShmLinkSlots - 1)];
+    if (sl.seq.load(std::memory_order_acquire) != got_ + 1) return false;
+    std::memcpy(m, &sl.msg, sizeof(Msg));
+    got_++;
+    taken.store(got_, std::memory_order_release);
     return true;
 }
 
-bool ShmLink::take_request(Msg *m) {
-    // The app owns req_head and may write anything there: bound what we trust.
-    const uint64_t t = l_->req_tail.load(std::memory_order_relaxed);
-    const uint64_t h = l_->req_head.load(std::memory_order_acquire);
-    if (h == t || h - t > kShmLinkSlots) return false;
-    std::memcpy(m, &l_->req[t & (kShmLinkSlots - 1)], sizeof(Msg));
-    l_->req_tail.store(t + 1, std::memory_order_release);
-    return true;
-}
-
-bool ShmLink::post_reply(const Msg &m) {
-    const uint64_t h = l_->rsp_head.load(std::memory_order_relaxed);
-    const uint64_t t = l_->rsp_tail.load(std::memory_order_acquire);
-    if (h - t >= kShmLinkSlots) return false;  // full (or a tail the app corrupted): the socket path
-    std::memcpy(&l_->rsp[h & (kShmLinkSlots - 1)], &m, sizeof(Msg));
-    l_->rsp_head.store(h + 1, std::memory_order_release);
-    return true;
-}
+bool ShmLink::post_request(const Msg &m) { return post(l_->req, l_->req_taken, m); }
+bool ShmLink::take_reply(Msg *m) { return take(l_->rsp, l_->rsp_taken, m); }
+bool ShmLink::take_request(Msg *m) { return take(l_->req, l_->req_taken, m); }
+bool ShmLink::post_reply(const Msg &m) { return post(l_->rsp, l_->rsp_taken, m); }
 
 bool ShmLink::request_needs_wake() {
     std::atomic_thread_fence(std::memory_order_seq_cst);  // the posted head before the flag's read
@@ -123,7 +124,7 @@ void ShmLink::set_daemon_polling(bool on) {
 }
 
 bool ShmLink::requests_pending() {
-    return l_->req_head.load(std::memory_order_acquire) != l_->req_tail.load(std::memory_order_relaxed);
+    return l_->req[got_ & (kShmLinkSlots - 1)].seq.load(std::memory_order_acquire) == got_ + 1;
 }
 
 void ShmLink::set_app_waiting(bool on) {
@@ -132,7 +133,7 @@ void ShmLink::set_app_waiting(bool on) {
 }
 
 bool ShmLink::replies_pending() {
-    return l_->rsp_head.load(std::memory_order_acquire) != l_->rsp_tail.load(std::memory_order_relaxed);
+    return l_->rsp[got_ & (kShmLinkSlots - 1)].seq.load(std::memory_order_acquire) == got_ + 1;
 }
 
 }  // namespace ocm

@@ -625,6 +625,23 @@ int ocm_x_extent_handle(ocm_alloc_t a, int i, uint8_t *out) {
     return 0;
 }
 
+// Layout of the app's shared-memory link (ocm/shmlink.h), for tests that drive a
+// link by hand: {mapped bytes, req_taken, rsp_taken, daemon_polling, app_waiting,
+// req[0], rsp[0], slot bytes, seq offset in a slot, slots, magic}.
+void ocm_x_link_layout(uint64_t out[11]) {
+    out[0] = ((uint64_t)sizeof(ShmLinkLayout) + 4095) & ~4095ull;
+    out[1] = offsetof(ShmLinkLayout, req_taken);
+    out[2] = offsetof(ShmLinkLayout, rsp_taken);
+    out[3] = offsetof(ShmLinkLayout, daemon_polling);
+    out[4] = offsetof(ShmLinkLayout, app_waiting);
+    out[5] = offsetof(ShmLinkLayout, req);
+    out[6] = offsetof(ShmLinkLayout, rsp);
+    out[7] = sizeof(ShmLinkSlot);
+    out[8] = offsetof(ShmLinkSlot, seq);
+    out[9] = kShmLinkSlots;
+    out[10] = kShmLinkMagic;
+}
+
 // xGMI self-diagnosis of this process: {device, peers with access enabled,
 // other GPUs' HBM slabs imported, such imports refused, push-get launches}.
 void ocm_x_xgmi_diag(uint64_t out[5]) {

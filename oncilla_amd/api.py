@@ -197,6 +197,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_extent_handle": (i32, [vp, i32, ctypes.c_char_p]),
             "ocm_x_extent_region": (i32, [vp, i32, ctypes.POINTER(u64)]),
             "ocm_x_xgmi_diag": (None, [ctypes.POINTER(u64)]),
+            "ocm_x_link_layout": (None, [ctypes.POINTER(u64)]),
             "ocm_x_ipc_open": (i32, [i32, ctypes.c_char_p, ctypes.POINTER(vp)]),
             "ocm_x_ipc_close": (i32, [i32, vp]),
             "ocm_x_pattern_dev": (ctypes.c_longlong, [i32, vp, u64, u64, ctypes.c_uint32, i32]),
@@ -331,6 +332,15 @@ def counters() -> dict:
     out = (ctypes.c_uint64 * len(COUNTER_KEYS))()
     load().ocm_x_counters(out)
     return dict(zip(COUNTER_KEYS, [int(v) for v in out]))
+
+
+def link_layout() -> dict:
+    """Byte layout of the app <-> daemon shared-memory link (ocm/shmlink.h), for tests."""
+    out = (ctypes.c_uint64 * 11)()
+    load().ocm_x_link_layout(out)
+    keys = ("bytes", "req_taken", "rsp_taken", "daemon_polling", "app_waiting", "req", "rsp", "slot", "seq", "slots",
+            "magic")
+    return dict(zip(keys, (int(x) for x in out)))
 
 
 def xgmi_diag() -> dict:

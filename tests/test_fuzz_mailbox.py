@@ -349,96 +349,119 @@ def test_daemon_refuses_hostile_shared_memory_links(mesh_factory, kind):
         assert api.counters()["n_link_rpc"] > 0
 
 
-# ocm/shmlink.h ShmLinkLayout (offsets checked by the native unit tests' static layout)
-LINK_BYTES, LINK_REQ_HEAD, LINK_REQ_TAIL, LINK_RSP_HEAD, LINK_RSP_TAIL = 24576, 64, 128, 192, 256
-LINK_POLLING, LINK_WAITING, LINK_REQ, LINK_RSP, LINK_SLOTS = 320, 384, 448, 10688, 64
 MSG_WAKE = 26
 
 
-def _raw_link(ns, seq=5):
-    """Connect like libocm does, but with a link this process owns: a sealed memfd
-    of the layout, offered with MSG_CONNECT. Returns (socket, mmap)."""
-    import mmap
+class RawLink:
+    """An app's side of a shared-memory link (ocm/shmlink.h), driven by hand: a
+    sealed memfd of the layout (read from the library), offered with MSG_CONNECT."""
 
-    fd = os.memfd_create("ocm_link", os.MFD_ALLOW_SEALING)
-    os.ftruncate(fd, LINK_BYTES)
-    fcntl_seal(fd)
-    mm = mmap.mmap(fd, LINK_BYTES)
-    struct.pack_into("<II", mm, 0, 0x4F434D4C, LINK_SLOTS)
-    s = _connect(ns)
-    s.setblocking(True)
-    s.settimeout(5)
-    s.sendmsg([MSG.pack(1, 1, 0, 0, seq, -1, 0, b"\0" * 128)],
-              [(socket.SOL_SOCKET, socket.SCM_RIGHTS, struct.pack("i", fd))])
-    os.close(fd)
-    return s, mm
+    def __init__(self, ns, seq=5):
+        import mmap
+
+        self.L = L = api.link_layout()
+        fd = os.memfd_create("ocm_link", os.MFD_ALLOW_SEALING)
+        os.ftruncate(fd, L["bytes"])
+        fcntl_seal(fd)
+        self.mm = mmap.mmap(fd, L["bytes"])
+        struct.pack_into("<II", self.mm, 0, L["magic"], L["slots"])
+        self.sent = self.got = 0
+        self.s = _connect(ns)
+        self.s.setblocking(True)
+        self.s.settimeout(5)
+        self.s.sendmsg([MSG.pack(1, 1, 0, 0, seq, -1, 0, b"\0" * 128)],
+                       [(socket.SOL_SOCKET, socket.SCM_RIGHTS, struct.pack("i", fd))])
+        os.close(fd)
+
+    def slot(self, ring, n):  # byte offset of the slot record n (1-based) uses
+        return self.L[ring] + ((n - 1) % self.L["slots"]) * self.L["slot"]
+
+    def q(self, off, v=None):
+        if v is None:
+            return struct.unpack_from("<Q", self.mm, off)[0]
+        struct.pack_into("<Q", self.mm, off, v)
+
+    def wake(self):
+        self.s.send(MSG.pack(MSG_WAKE, 1, 0, 0, 0, -1, 0, b"\0" * 128))
+
+    def post(self, rec, seq=None):
+        """Record `rec` as request sent+1 (or with a forged slot sequence number)."""
+        self.sent += 1
+        off = self.slot("req", self.sent)
+        self.mm[off:off + 160] = rec
+        self.q(off + self.L["seq"], self.sent if seq is None else seq)
+        self.wake()
+
+    def room(self):
+        return self.sent - self.q(self.L["req_taken"]) < self.L["slots"]
+
+    def reply(self, timeout=5.0):
+        """The next reply, from the reply ring (or the socket)."""
+        import select
+        import time
+
+        end = time.time() + timeout
+        while time.time() < end:
+            off = self.slot("rsp", self.got + 1)
+            if self.q(off + self.L["seq"]) == self.got + 1:
+                rec = bytes(self.mm[off:off + 160])
+                self.got += 1
+                self.q(self.L["rsp_taken"], self.got)
+                return MSG.unpack(rec)
+            if select.select([self.s], [], [], 0.001)[0]:
+                data = self.s.recv(160)
+                if len(data) == 160 and MSG.unpack(data)[0] != MSG_WAKE:
+                    return MSG.unpack(data)
+        raise TimeoutError("no reply on the link or the socket")
+
+    def close(self):
+        self.s.close()
+        self.mm.close()
 
 
-def _link_reply(s, mm, timeout=5.0):
-    """The next reply, from the link's reply ring (or the socket)."""
-    import select
-    import time
-
-    end = time.time() + timeout
-    while time.time() < end:
-        head, tail = struct.unpack_from("<Q", mm, LINK_RSP_HEAD)[0], struct.unpack_from("<Q", mm, LINK_RSP_TAIL)[0]
-        if head != tail:
-            off = LINK_RSP + (tail % LINK_SLOTS) * 160
-            rec = bytes(mm[off:off + 160])
-            struct.pack_into("<Q", mm, LINK_RSP_TAIL, tail + 1)
-            return MSG.unpack(rec)
-        if select.select([s], [], [], 0.001)[0]:
-            data = s.recv(160)
-            if len(data) == 160 and MSG.unpack(data)[0] != MSG_WAKE:
-                return MSG.unpack(data)
-    raise TimeoutError("no reply on the link or the socket")
-
-
-def _post(s, mm, rec):
-    head = struct.unpack_from("<Q", mm, LINK_REQ_HEAD)[0]
-    off = LINK_REQ + (head % LINK_SLOTS) * 160
-    mm[off:off + 160] = rec
-    struct.pack_into("<Q", mm, LINK_REQ_HEAD, head + 1)
-    s.send(MSG.pack(MSG_WAKE, 1, 0, 0, 0, -1, 0, b"\0" * 128))
+def test_link_layout_matches_the_native_one():
+    L = api.link_layout()
+    assert L["slot"] % 64 == 0 and L["seq"] + 8 <= L["slot"] and L["bytes"] % 4096 == 0
+    assert L["rsp"] == L["req"] + L["slots"] * L["slot"] and L["rsp"] + L["slots"] * L["slot"] <= L["bytes"]
+    assert len({L[k] // 64 for k in ("req_taken", "rsp_taken", "daemon_polling", "app_waiting")}) == 4
 
 
 def test_link_carries_requests_and_the_daemon_survives_garbage_in_it(mesh_factory):
     """A valid link driven by hand: the CONNECT_CONFIRM and a PING's reply come back
-    on the reply ring. Then the app scribbles: random records, request heads far
-    ahead of the tail or behind it, a reply tail past the head. The daemon bounds
-    what it reads, copies records out before looking at them, and keeps serving
-    other apps; a fresh link on a new connection still works."""
+    on the reply ring. Then the app scribbles: random records, forged slot sequence
+    numbers ahead of and behind the daemon's count, a bogus count of replies taken,
+    garbage over the records. The daemon copies records out before looking at
+    them, treats bogus counts as a full ring, and keeps serving other apps; a fresh
+    link on a new connection still works."""
     import random
 
     m = mesh_factory(1)
-    s, mm = _raw_link(m.ns)
-    t, _, _, _, seq = _link_reply(s, mm)[:5]
+    k = RawLink(m.ns)
+    t, _, _, _, seq = k.reply()[:5]
     assert (t, seq) == (2, 5)
-    _post(s, mm, MSG.pack(18, 1, 0, 0, 77, -1, 0, b"\0" * 128))  # MSG_PING
-    rep = _link_reply(s, mm)
-    assert rep[4] == 77
+    k.post(MSG.pack(18, 1, 0, 0, 77, -1, 0, b"\0" * 128))  # MSG_PING
+    assert k.reply()[4] == 77
     rng = random.Random(7)
     for i in range(400):
-        k = i % 4
-        if k == 0:  # a random record, properly posted
-            _post(s, mm, bytes(rng.getrandbits(8) for _ in range(160)))
-        elif k == 1:  # a head far ahead of the tail
-            struct.pack_into("<Q", mm, LINK_REQ_HEAD, rng.getrandbits(64))
-            s.send(MSG.pack(MSG_WAKE, 1, 0, 0, 0, -1, 0, b"\0" * 128))
-        elif k == 2:  # a reply tail past the head (the daemon must not overrun the ring)
-            struct.pack_into("<Q", mm, LINK_RSP_TAIL, rng.getrandbits(64))
-            _post(s, mm, MSG.pack(18, 1, 0, 0, 1000 + i, -1, 0, b"\0" * 128))
+        kind = i % 4
+        if kind == 0:  # a random record, properly posted
+            k.post(bytes(rng.getrandbits(8) for _ in range(160)))
+        elif kind == 1:  # a forged sequence number in the next slot
+            off = k.slot("req", k.sent + 1)
+            k.q(off + k.L["seq"], rng.getrandbits(64))
+            k.wake()
+        elif kind == 2:  # a bogus count of replies taken (the daemon must not overrun the ring)
+            k.q(k.L["rsp_taken"], rng.getrandbits(64))
+            k.post(MSG.pack(18, 1, 0, 0, 1000 + i, -1, 0, b"\0" * 128))
         else:  # garbage over the records themselves
-            off = LINK_REQ + rng.randrange(0, LINK_SLOTS * 160 - 8)
-            mm[off:off + 8] = os.urandom(8)
-            s.send(MSG.pack(MSG_WAKE, 1, 0, 0, 0, -1, 0, b"\0" * 128))
-    s.close()
-    mm.close()
+            off = k.L["req"] + rng.randrange(0, k.L["slots"] * k.L["slot"] - 8)
+            k.mm[off:off + 8] = os.urandom(8)
+            k.wake()
+    k.close()
     assert m.daemons[0].alive()
-    s2, mm2 = _raw_link(m.ns, seq=9)
-    assert _link_reply(s2, mm2)[4] == 9
-    s2.close()
-    mm2.close()
+    k2 = RawLink(m.ns, seq=9)
+    assert k2.reply()[4] == 9
+    k2.close()
     with api.Client(daemon_rank=0, ns=m.ns) as c:
         a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)
         a.fill(seed=3)
@@ -469,16 +492,16 @@ def test_an_app_that_never_takes_its_replies_is_disconnected(mesh_factory, path)
         except (ConnectionResetError, BrokenPipeError):
             pass  # dropped already
     else:
-        s, mm = _raw_link(m.ns)
-        assert _link_reply(s, mm)[4] == 5
-        struct.pack_into("<Q", mm, LINK_RSP_TAIL, 1 << 40)  # the reply ring looks full forever
+        k = RawLink(m.ns)
+        s = k.s
+        assert k.reply()[4] == 5
+        k.q(k.L["rsp_taken"], 1 << 40)  # the reply ring looks full forever
         sent = 0
         end = time.time() + 30
         try:
             while sent < 6000 and time.time() < end:
-                head = struct.unpack_from("<Q", mm, LINK_REQ_HEAD)[0]
-                if head - struct.unpack_from("<Q", mm, LINK_REQ_TAIL)[0] < LINK_SLOTS:
-                    _post(s, mm, ping)
+                if k.room():
+                    k.post(ping)
                     sent += 1
         except (ConnectionResetError, BrokenPipeError):
             pass  # dropped already
