@@ -23,12 +23,11 @@
 // Slots carry their own sequence number (written last, with release), so a
 // consumer polls the slot it expects next instead of a shared head counter,
 // and each side keeps its own counters privately: a round trip moves the two
-// records' cache lines and little else. That matters when the app runs on the
-// other socket from its daemon, where every line moved costs a cross-socket
-// transfer (bench.py alloc p50 2.0 us there against 0.86 us on the daemon's
-// socket with round 3's first layout of shared head/tail counters). The
-// consumer publishes how many records it took, which the producer reads only
-// when its own count says the ring may be full.
+// records' cache lines and little else (bench.py remote alloc p50 0.75-0.81 us
+// with the app on either NUMA node, against 0.85-1.06 us with shared head/tail
+// counters and 2.6 us over the socket alone; profiles/alloc_link_numa_r03.json).
+// The consumer publishes how many records it took, which the producer reads
+// only when its own count says the ring may be full.
 // The daemon copies every record out of the shared ring before it looks at it
 // (the app may rewrite the ring at any time) and trusts the connection's
 // SO_PEERCRED pid, not the record's, as on the socket path.
