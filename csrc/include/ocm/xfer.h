@@ -169,14 +169,17 @@ static_assert(sizeof(ServiceReq) == 128, "service request layout");
 static_assert(__builtin_offsetof(ServiceReq, seq) == 120 && __builtin_offsetof(ServiceReq, sum) == 112,
               "the kernel reads seq/sum as words 15/14");
 
+constexpr int kServiceWgDoneMax = 128;  // WGDONE: gangs of at most this many workgroups
 struct alignas(128) ServiceSlot {
     ServiceReq req;                   // the request record
     unsigned long long done;          // device -> host (own cache line)
     unsigned long long exited;        // device -> host: first seq NOT served when it left
     unsigned long long gpu_ticks;     // device -> host: sum of request-seen -> done ticks of workgroup 0 (100 MHz)
     unsigned long long pad[13];
+    // WGDONE: gang member i stores the seq it finished here (device -> host)
+    unsigned long long wg_done[kServiceWgDoneMax];
 };
-static_assert(sizeof(ServiceSlot) == 256, "service slot layout");
+static_assert(sizeof(ServiceSlot) == 256 + 8 * kServiceWgDoneMax, "service slot layout");
 
 constexpr int kServiceTraceWgs = 64;
 // Device-memory state of the gang (zeroed before every launch).
@@ -215,8 +218,18 @@ void service_store_seq(ServiceReq *req, unsigned long long seq);
 //   WCREQ     the request record(s) in write-combined host memory (uncached on
 //             the CPU side, so GPU polls need no snoop of the CPU's caches; the
 //             host only ever writes them), `done` stays in coherent memory
+//   WGDONE    gang completion without the device-scope counter: every member
+//             stores the seq it finished into its own ServiceSlot::wg_done word
+//             and the host waits for all `active` of them (gangs of at most
+//             kServiceWgDoneMax); the counter's atomic round trip is then off the
+//             last workgroup's path to `done`
 //   TRACE     diagnostics: stamp each workgroup's phases into ServiceBox::trace
-constexpr unsigned kServiceProtoWT = 1u, kServiceProtoGangRec = 2u, kServiceProtoWCReq = 4u, kServiceProtoTrace = 16u;
+constexpr unsigned kServiceProtoWT = 1u, kServiceProtoGangRec = 2u, kServiceProtoWCReq = 4u, kServiceProtoWgDone = 8u,
+                   kServiceProtoTrace = 16u;
+// Whether a gang of `active` workgroups completes through ServiceSlot::wg_done.
+constexpr bool service_wg_done(unsigned proto, unsigned long long active) {
+    return (proto & kServiceProtoWgDone) && active > 1 && active <= (unsigned long long)kServiceWgDoneMax;
+}
 
 // first_seq >= 1: the first request this instance serves. gang_req: the
 // GANGREC record (nullptr: gang requests are relayed by workgroup 0).

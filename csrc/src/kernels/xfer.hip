@@ -728,7 +728,13 @@ __device__ __forceinline__ void service_serve(const unsigned long long *sh, unsi
         block_release_system();
     }
     service_stamp(box, proto, 2);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && service_wg_done(proto, active)) {
+        // WGDONE: this member's own completion word; the host waits for all of them.
+        if (wt)
+            __hip_atomic_store(&slot->wg_done[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            __hip_atomic_store(&slot->wg_done[blockIdx.x], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (threadIdx.x == 0) {
         bool last = active == 1;
         if (!last) {
             const unsigned long long old =

@@ -268,13 +268,22 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
     const unsigned width = direct ? std::min(s.svc_direct, s.svc_blocks)
                                   : (hbm ? s.svc_blocks : std::min(s.svc_gang_host, s.svc_blocks));
     const unsigned long long active = service_gang_size(x, width, solo_tiles);
+    const bool wgdone = service_wg_done(s.svc_proto, active);
     auto gang_word = [&]() {
         unsigned long long target = 0;
-        if (active > 1) {
+        if (active > 1 && !wgdone) {  // WGDONE gangs leave the counter alone
             s.svc_gang_total += active;
             target = s.svc_gang_total;
         }
         return active | (target << 16) | (strict ? kServiceGangStrict : 0ull);
+    };
+    // Completed: `done` (a solo op or the gang's last member), or under WGDONE
+    // every member's own word.
+    auto finished = [&]() {
+        if (!wgdone) return __atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq;
+        for (unsigned long long i = active; i-- > 0;)
+            if (__atomic_load_n(&s.svc->wg_done[i], __ATOMIC_ACQUIRE) != seq) return false;
+        return true;
     };
     unsigned long long gang = gang_word();
     // GANGREC: gang requests go to the record the whole gang polls.
@@ -283,7 +292,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
     service_post(rq, x, gang, seq);
     const uint64_t t_posted = now_ns();
     for (unsigned spins = 1;; spins++) {
-        if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) {
+        if (finished()) {
             s.svc_ops++;
             s.svc_ns_post += t_posted - t0;
             s.svc_ns_wait += now_ns() - t_posted;
@@ -298,7 +307,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
                 (void)hipStreamSynchronize(s.svc_stream);
                 s.svc_running = false;
                 s.svc_relaunches++;
-                if (__atomic_load_n(&s.svc->done, __ATOMIC_ACQUIRE) == seq) return 0;
+                if (finished()) return 0;
                 if (service_start(seq) != 0) return -1;
                 gang = gang_word();              // counted afresh by the new instance
                 service_post(rq, x, gang, seq);  // start cleared the doorbell: re-post

@@ -209,12 +209,15 @@ def test_push_get_through_the_library_same_gpu(mesh_factory):
                 a.fill(seed=0)
                 a.get(0, 0, n)
                 assert a.check(seed=900 + i) == 0, f"blocking push get, round {i}"
+                # The async put reads local[0, h) after this call returns, so the get
+                # lands in the other half (a refill of the same bytes would race the
+                # put: pattern fills run on the library stream, not the lane).
+                h = n // 2
                 a.fill(seed=950 + i)
-                a.put(0, 0, n, async_=True)
-                a.fill(seed=0)
-                a.get(0, 0, n, async_=True)  # queued behind the async put on the allocation's lane
+                a.put(0, 0, h, async_=True)
+                a.get(h, 0, h, async_=True)  # queued behind the async put on the allocation's lane
                 a.wait()
-                assert a.check(seed=950 + i) == 0, f"async push get, round {i}"
+                assert a.check(seed=950 + i, offset=h, nbytes=h, first_word=0) == 0, f"async push get, round {i}"
             assert api.xgmi_diag()["push_launches"] - before >= 6  # one launch per owner GPU and get
         finally:
             api.set_tuning_dir(0, 0, 0, True)

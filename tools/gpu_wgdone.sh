@@ -1,0 +1,19 @@
+# WGDONE A/B: the copy-service GPU tests under OCM_SERVICE_PROTO=15 (WT, GANGREC,
+# WCREQ + WGDONE), then bench.py's sweep up to 16 MiB (the service's host-tier
+# range) with the default protocol (7) and with WGDONE (15), interleaved.
+set -o pipefail
+OUT=gpurun_out/wgdone
+mkdir -p $OUT
+timeout -k 10 400 env OCM_SERVICE_PROTO=15 python3 -u -m pytest tests/test_gpu_service.py tests/test_gpu_runtime.py -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
+for i in 1 2 3; do
+  for p in 7 15; do
+    timeout -k 10 200 env OCM_SERVICE_PROTO=$p python3 -u bench.py --steps 10 --warmup 3 --max-bytes 16777216 --no-optim-extra --no-characterize --json-out $OUT/p${p}_$i.json > $OUT/p${p}_$i.log 2>&1 || exit $?
+  done
+done
+python3 - <<'PY'
+import json, glob
+for f in sorted(glob.glob('gpurun_out/wgdone/p*.json')):
+    d = json.load(open(f)); sw = d['sweep']
+    print(f.split('/')[-1], ' '.join(f"{int(s)>>10}K:{sw[s]['get_us']}/{sw[s]['put_us']}" for s in sw if int(s) >= 16384))
+PY
