@@ -66,7 +66,11 @@ constexpr int kServiceIdleUsDefault = 50;
 // requests polled directly by the first 16 workgroups: small ops -0.1/-0.2 us,
 // host-tier 128 KiB-4 MiB and HBM 256 KiB-1 MiB gangs 1-1.5 us faster than the
 // relay (profiles/svc_direct_gang_ab_r02.json, svc_direct_hybrid_r02.json).
-constexpr unsigned kServiceProtoDefault = kServiceProtoWT | kServiceProtoGangRec | kServiceProtoWCReq;
+// Round 3: gangs complete through per-workgroup done words (WGDONE) instead of a
+// device-scope counter: host-tier 64-128 KiB ops 0.2-0.3 us faster, 256 KiB-4 MiB
+// 0.1 us, small ops unchanged (profiles/svc_wgdone_ab_r03.json).
+constexpr unsigned kServiceProtoDefault =
+    kServiceProtoWT | kServiceProtoGangRec | kServiceProtoWCReq | kServiceProtoWgDone;
 constexpr int kServiceDirectDefault = 16;
 // Direct gangs (at most kServiceDirectDefault workgroups) for ops up to these
 // sizes; wider relayed gangs above, where 16 workgroups copy too slowly
