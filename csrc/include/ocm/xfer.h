@@ -108,6 +108,8 @@ struct XferBatchArgs {
     uint64_t total_tiles;
     uint32_t grid;                        // workgroups (4 waves each)
     uint32_t abs_lin;                     // 1: op.lin_off is an absolute device address (lin unused)
+    uint32_t host_tier;                   // 1: every extent is pinned host memory (PCIe launch shape, sc1 puts)
+    uint32_t pad0;
     const XferBatchOp *ops;               // device copy when n_ops > kXferInlineOps
     const uint32_t *wave_op;              // device: first op of each wave (n_ops > kXferInlineOps)
     XferBatchOp inline_ops[kXferInlineOps];
@@ -115,8 +117,9 @@ struct XferBatchArgs {
 
 // Host-side plan. Fills first_tile, returns total tiles.
 uint64_t xfer_batch_plan(XferBatchOp *ops, uint32_t n, uint32_t tile_shift);
-// Workgroups for `total_tiles` (4 waves each, capped for residency).
-uint32_t xfer_batch_grid(uint64_t total_tiles);
+// Workgroups for `total_tiles` (4 waves each, capped for residency; host-tier
+// batches are capped lower, OCM_BATCH_HOST_GRID: PCIe wants fewer streams).
+uint32_t xfer_batch_grid(uint64_t total_tiles, bool host_tier = false);
 // wave_op[w] for every wave of `grid` workgroups (4 * grid entries).
 void xfer_batch_wave_ops(const XferBatchOp *ops, uint32_t n, uint64_t total_tiles, uint32_t grid, uint32_t *out);
 // tile shift for a remote layout: 4 KiB wave-tiles, or the stripe unit when smaller.

@@ -537,7 +537,8 @@ constexpr uint32_t kBatchTileShift = 12;  // 4 KiB per wave-tile: 64 lanes x 16 
 constexpr int kBatchUnroll = 4;
 
 // One wave copies n bytes (n <= one wave-tile in the common case; any n works).
-template <bool NT>
+// ST: the store kind (ST_NT / ST_PLAIN; ST_WT for puts into the host tier).
+template <int ST>
 __device__ __forceinline__ void wave_copy(char *__restrict__ dst, const char *__restrict__ src, uint64_t n, int lane) {
     uint64_t head = (16u - ((uintptr_t)dst & 15u)) & 15u;
     if (head > n) head = n;
@@ -555,9 +556,9 @@ __device__ __forceinline__ void wave_copy(char *__restrict__ dst, const char *__
 #pragma unroll
             for (int k = 0; k < kBatchUnroll; k++) v[k] = load16(s + i + k * 64);
 #pragma unroll
-            for (int k = 0; k < kBatchUnroll; k++) store16<NT ? ST_NT : ST_PLAIN>(d + i + k * 64, v[k]);
+            for (int k = 0; k < kBatchUnroll; k++) store16<ST>(d + i + k * 64, v[k]);
         }
-        for (; i < nv; i += 64) store16<NT ? ST_NT : ST_PLAIN>(d + i, load16(s + i));
+        for (; i < nv; i += 64) store16<ST>(d + i, load16(s + i));
         const uint64_t tail = n & 15u;
         if ((uint64_t)lane < tail) dst[(nv << 4) + lane] = src[(nv << 4) + lane];
     } else {
@@ -565,7 +566,9 @@ __device__ __forceinline__ void wave_copy(char *__restrict__ dst, const char *__
     }
 }
 
-template <bool NT>
+// HOST: the host-tier shape: puts store write-through (sc1) into the pinned
+// host extents, as the PCIe streaming kernel does (57.0 vs 55.5 GB/s).
+template <bool NT, bool HOST = false>
 __global__ __launch_bounds__(kThreads) void xfer_batch_kernel(XferBatchArgs a) {
     const int lane = threadIdx.x & 63;
     // wave index, made scalar: everything below is wave-uniform
@@ -585,11 +588,20 @@ __global__ __launch_bounds__(kThreads) void xfer_batch_kernel(XferBatchArgs a) {
         char *lin = a.abs_lin ? reinterpret_cast<char *>(static_cast<uintptr_t>(op.lin_off)) : a.lin + op.lin_off;
         TileSpan sp = tile_span_of(a, a.n_ext, a.unit_shift, a.tile_shift, lin, op.rem_off, op.len, op.put,
                                    t - op.first_tile, op.rem_off & ~tile_mask);
-        wave_copy<NT>(sp.dst, sp.src, sp.n, lane);
+        if (HOST && op.put)
+            wave_copy<ST_WT>(sp.dst, sp.src, sp.n, lane);
+        else
+            wave_copy<NT ? ST_NT : ST_PLAIN>(sp.dst, sp.src, sp.n, lane);
     }
 }
 
 }  // namespace
+
+// Host-tier batches store puts write-through (OCM_BATCH_HOST_SC1=0: the generic kernel).
+static bool host_sc1() {
+    static const bool on = env_int("OCM_BATCH_HOST_SC1", 1) != 0;
+    return on;
+}
 
 uint32_t xfer_batch_tile_shift(uint32_t n_ext, uint32_t unit_shift) {
     return (n_ext > 1 && unit_shift < kBatchTileShift) ? unit_shift : kBatchTileShift;
@@ -606,10 +618,14 @@ uint64_t xfer_batch_plan(XferBatchOp *ops, uint32_t n, uint32_t tile_shift) {
     return total;
 }
 
-uint32_t xfer_batch_grid(uint64_t total_tiles) {
+uint32_t xfer_batch_grid(uint64_t total_tiles, bool host_tier) {
     // One wave per tile until the chip holds 8 workgroups (32 waves) per CU.
     const uint64_t want = (total_tiles + kWaves - 1) / kWaves;
-    const uint64_t cap = (uint64_t)num_cus() * 8;
+    // Host tier: 128 workgroups and write-through puts; 4096-block KV swaps 48.0-48.1 /
+    // 48.8-49.9 GiB/s out/in against 46.8-46.9 / 47.5-48.1 with the HBM shape
+    // (profiles/kv_swap_host_r03.json; the PCIe ceiling is ~53).
+    static const int host_grid = env_int("OCM_BATCH_HOST_GRID", 128);
+    const uint64_t cap = host_tier && host_grid > 0 ? (uint64_t)host_grid : (uint64_t)num_cus() * 8;
     return (uint32_t)(want < cap ? (want ? want : 1) : cap);
 }
 
@@ -628,7 +644,9 @@ hipError_t xfer_batch_launch(const XferBatchArgs &a, const XferTuning &t, hipStr
     if (a.total_tiles == 0 || a.n_ops == 0) return hipSuccess;
     if (a.n_ext < 1 || a.n_ext > (uint32_t)kXferMaxExtents || a.grid == 0) return hipErrorInvalidValue;
     if (a.n_ops > (uint32_t)kXferInlineOps && (!a.ops || !a.wave_op)) return hipErrorInvalidValue;
-    if (t.nontemporal)
+    if (a.host_tier && host_sc1())
+        hipLaunchKernelGGL((xfer_batch_kernel<true, true>), dim3(a.grid), dim3(kThreads), 0, stream, a);
+    else if (t.nontemporal)
         hipLaunchKernelGGL(xfer_batch_kernel<true>, dim3(a.grid), dim3(kThreads), 0, stream, a);
     else
         hipLaunchKernelGGL(xfer_batch_kernel<false>, dim3(a.grid), dim3(kThreads), 0, stream, a);
@@ -646,8 +664,9 @@ hipError_t xfer_batch_graph_node(hipGraph_t graph, hipGraphNode_t dep, const Xfe
     void *params[] = {const_cast<XferBatchArgs *>(&a)};
     hipKernelNodeParams kp;
     std::memset(&kp, 0, sizeof(kp));
-    kp.func = t.nontemporal ? reinterpret_cast<void *>(&xfer_batch_kernel<true>)
-                            : reinterpret_cast<void *>(&xfer_batch_kernel<false>);
+    kp.func = (a.host_tier && host_sc1()) ? reinterpret_cast<void *>(&xfer_batch_kernel<true, true>)
+              : t.nontemporal             ? reinterpret_cast<void *>(&xfer_batch_kernel<true>)
+                                          : reinterpret_cast<void *>(&xfer_batch_kernel<false>);
     kp.gridDim = dim3(a.grid);
     kp.blockDim = dim3(kThreads);
     kp.sharedMemBytes = 0;

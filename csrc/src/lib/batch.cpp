@@ -17,7 +17,8 @@ static void plan_batch_args(lib_alloc *a, std::vector<XferBatchOp> &v, bool abs_
     args->tile_shift = xfer_batch_tile_shift(args->n_ext, args->unit_shift);
     args->n_ops = (uint32_t)v.size();
     args->total_tiles = xfer_batch_plan(v.data(), (uint32_t)v.size(), args->tile_shift);
-    args->grid = args->total_tiles ? xfer_batch_grid(args->total_tiles) : 0;
+    args->host_tier = (!a->any_gpu && !a->any_net) ? 1u : 0u;
+    args->grid = args->total_tiles ? xfer_batch_grid(args->total_tiles, args->host_tier != 0) : 0;
     if (v.size() <= (size_t)kXferInlineOps) std::memcpy(args->inline_ops, v.data(), v.size() * sizeof(XferBatchOp));
 }
 

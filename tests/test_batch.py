@@ -118,14 +118,16 @@ def test_batch_kernel_gpu(mesh_factory, unit, n_ops, max_len, async_):
 
 
 @pytest.mark.gpu
-def test_batch_host_tier_gpu(mesh_factory):
-    # single daemon: the remote half is the pinned host tier, still one kernel (mapped host memory)
+@pytest.mark.parametrize("n_ops,max_len,async_", [(300, 5000, False), (40, 70000, True), (3000, 2500, True)])
+def test_batch_host_tier_gpu(mesh_factory, n_ops, max_len, async_):
+    # single daemon: the remote half is the pinned host tier, still one kernel (mapped
+    # host memory): the host-tier launch shape with write-through puts
     m = mesh_factory(1, gpus=[0])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         n = 4 << 20
         a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n)
         assert a.remote_info()["extents"][0]["tier"] == api.OCM_TIER_HOST
-        run_batch_check(a, n, 300, 5000, seed=7)
+        run_batch_check(a, n, n_ops, max_len, seed=7 + n_ops, async_=async_)
         a.free()
 
 

@@ -69,11 +69,15 @@ def case(label, n_daemons, n_gpu_blocks, n_pool_blocks, n_swap, pool_device):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="")
+    ap.add_argument("--host-only", action="store_true", help="the host-tier pool cases only (and a 4096-block swap)")
     args = ap.parse_args()
-    rows = [case("host_tier_pool", 1, 1024, 4096, 256, "cpu"),
-            case("host_tier_pool", 1, 1024, 4096, 1024, "cpu"),
-            case("hbm_pool_striped3", 4, 1024, 4096, 256, "cuda:0"),
-            case("hbm_pool_striped3", 4, 1024, 4096, 1024, "cuda:0")]
+    if args.host_only:
+        rows = [case("host_tier_pool", 1, 4096, 8192, n, "cpu") for n in (256, 1024, 4096)]
+    else:
+        rows = [case("host_tier_pool", 1, 1024, 4096, 256, "cpu"),
+                case("host_tier_pool", 1, 1024, 4096, 1024, "cpu"),
+                case("hbm_pool_striped3", 4, 1024, 4096, 256, "cuda:0"),
+                case("hbm_pool_striped3", 4, 1024, 4096, 1024, "cuda:0")]
     if args.out:
         os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
         with open(args.out, "w") as f:
