@@ -204,3 +204,29 @@ def test_shared_memory_link_carries_the_rpcs_and_survives_idle_daemons(mesh_fact
                 assert after["n_link_wake"] - before["n_link_wake"] >= 10
             else:
                 assert after["n_link_rpc"] == before["n_link_rpc"]
+
+
+def test_threads_of_one_app_share_its_link(mesh_factory, monkeypatch):
+    """Many threads of one app allocate and free at once: the library serializes
+    its RPCs, so the link's single-producer rings stay single-producer, and every
+    reply reaches the thread that asked (ctypes drops the GIL in the calls)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    m = mesh_factory(2)
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        before = api.counters()
+
+        def work(t):
+            for i in range(60):
+                kind = api.OCM_REMOTE_RDMA if (t + i) % 2 else api.OCM_LOCAL_HOST
+                a = c.alloc(kind, local_bytes=4096 * (1 + t), remote_bytes=(1 << 16) * (1 + i % 3))
+                assert a.localbuf()[1] == 4096 * (1 + t)
+                a.free()
+            return t
+
+        with ThreadPoolExecutor(8) as ex:
+            assert sorted(ex.map(work, range(8))) == list(range(8))
+        after = api.counters()
+        assert after["n_link_rpc"] - before["n_link_rpc"] >= 8 * 60 * 2
+        assert c.stats(0)["ctrl"] == "tcp"
