@@ -106,7 +106,9 @@ def autotune(alloc: api.Allocation, nbytes: int, reps: int = 3, gather=None, can
     `api.set_tuning_dir`; "auto" (the library default) is always a candidate,
     so the choice is never slower than the default as measured. Baseline
     candidates (BASELINE_ONLY: the runtime's copy engines) are timed and
-    reported but never installed. Overwrites the first `nbytes` of both halves.
+    reported but never installed. A candidate whose put/get round trip of a word
+    pattern comes back wrong on any rank is out too. Overwrites the first `nbytes`
+    of both halves.
     """
     cands = dict(candidates or TUNING_CANDIDATES)
     cands.setdefault("auto", (0, 0, 1))
@@ -131,6 +133,25 @@ def autotune(alloc: api.Allocation, nbytes: int, reps: int = 3, gather=None, can
             res = gather((t, err))
             errs = [r[1] for r in res if r[1]]
             row[key] = {"error": errs[0]} if errs else {"s": max(r[0] for r in res)}
+        # A fast candidate must also be a correct one: a round trip of a word pattern
+        # through it, checked on every rank, before it can be installed.
+        verr = None
+        try:
+            api.set_tuning_dir(0, variant, blocks, nt)
+            api.set_tuning_dir(1, variant, blocks, nt)
+            seed = 7001 + len(table)
+            alloc.fill(seed, 0, nbytes)
+            alloc.put(0, 0, nbytes)
+            alloc.fill(0, 0, nbytes)
+            alloc.get(0, 0, nbytes)
+            bad = alloc.check(seed, 0, nbytes)
+            if bad:
+                verr = f"round trip verification: {bad} words wrong"
+        except Exception as e:  # noqa: BLE001 - recorded; every rank still reaches the gather
+            verr = repr(e)[:160]
+        verrs = [v for v in gather(verr) if v]
+        if verrs:
+            row = {k: {"error": verrs[0]} for k in ("get", "put")}
         table[name] = row
     best = {}
     for op, key in ((0, "get"), (1, "put")):

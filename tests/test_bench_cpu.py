@@ -63,6 +63,24 @@ def test_bench_extras_helpers_run(native):
     assert bench._local(lambda: 1 / 0)[1].startswith("ZeroDivisionError")
 
 
+class RoundTrip:
+    """The data path of a fake pair for autotune's per-candidate verification: a
+    pattern seed travels local -> remote -> local; `corrupt(cfg)` spoils a put."""
+    corrupt = staticmethod(lambda cfg: False)
+
+    def fill(self, seed, offset=0, nbytes=None):
+        self.local = seed
+
+    def put(self, lo, ro, n):
+        self.remote = -1 if self.corrupt(self.cur[1]) else self.local
+
+    def get(self, lo, ro, n):
+        self.local = self.remote
+
+    def check(self, seed, offset=0, nbytes=None):
+        return 0 if self.local == seed else 17
+
+
 def test_autotune_picks_fastest_by_slowest_rank(native, monkeypatch):
     """workloads.autotune: per-direction pick by the slowest rank, failing candidates
     excluded, and the same number of collectives on every path (no deadlock)."""
@@ -75,7 +93,7 @@ def test_autotune_picks_fastest_by_slowest_rank(native, monkeypatch):
     cands = {"auto": (0, 0, 1), "reg_b256": (1, 256, 1), "lds_default": (2, 0, 1), "broken": (1, 64, 0)}
     mine = {(0, 0, 1): (3.0, 3.0), (1, 256, 1): (2.0, 1.0), (2, 0, 1): (1.5, 2.5)}
 
-    class FakePair:
+    class FakePair(RoundTrip):
         last = None
 
         def time_onesided(self, op, n, iters):
@@ -85,6 +103,7 @@ def test_autotune_picks_fastest_by_slowest_rank(native, monkeypatch):
             return mine[cfg][op]
 
     pair = FakePair()
+    pair.cur = cur
     calls = []
 
     def gather(obj):  # two ranks; the other one is 4x slower with reg_b256
@@ -97,8 +116,8 @@ def test_autotune_picks_fastest_by_slowest_rank(native, monkeypatch):
     assert r["get"] == "lds_default", r
     assert r["put"] == "lds_default", r  # reg_b256 is fastest here but not on the other rank
     assert "error" in r["GiBps"]["broken"]["get"] and "error" in r["GiBps"]["broken"]["put"]
-    # 2 gathers per (candidate, direction) + 1 for the rank count
-    assert len(calls) == 2 * 2 * len(cands) + 1
+    # 2 gathers per (candidate, direction), 1 for its verification, 1 for the rank count
+    assert len(calls) == (2 * 2 + 1) * len(cands) + 1
     assert cur[0] == cands[r["get"]] and cur[1] == cands[r["put"]]
 
 
@@ -153,11 +172,42 @@ def test_autotune_never_installs_the_dma_baseline(native, monkeypatch):
     cands = {"auto": (0, 0, 1), "reg_b256": (1, 256, 1), "dma": (3, 0, 1)}
     secs = {(0, 0, 1): 2e-4, (1, 256, 1): 1.5e-4, (3, 0, 1): 1e-4}
 
-    class FakePair:
+    class FakePair(RoundTrip):
+        cur = None
+
         def time_onesided(self, op, n, iters):
             return secs[cur[op]]
 
-    r = wl.autotune(FakePair(), 1 << 20, candidates=cands)
+    pair = FakePair()
+    pair.cur = cur
+    r = wl.autotune(pair, 1 << 20, candidates=cands)
     assert r["get"] == "reg_b256" and r["put"] == "reg_b256", r
     assert r["baselines"] == ["dma"] and r["GiBps"]["dma"]["get"] > r["GiBps"]["reg_b256"]["get"], r
     assert cur[0] == (1, 256, 1) and cur[1] == (1, 256, 1)
+
+
+def test_autotune_drops_a_fast_candidate_that_corrupts_data(native, monkeypatch):
+    """The fastest candidate whose round trip comes back wrong (on one rank only)
+    is reported as an error and never installed."""
+    from oncilla_amd import api
+    from oncilla_amd.models import workloads as wl
+
+    cur = {}
+    monkeypatch.setattr(api, "set_tuning_dir", lambda op, v, b, nt: cur.__setitem__(op, (v, b, nt)))
+    cands = {"auto": (0, 0, 1), "fast_but_wrong": (5, 0, 1), "reg_b256": (1, 256, 1)}
+    secs = {(0, 0, 1): 2e-4, (1, 256, 1): 1.5e-4, (5, 0, 1): 0.5e-4}
+
+    class FakePair(RoundTrip):
+        def time_onesided(self, op, n, iters):
+            return secs[cur[op]]
+
+    pair = FakePair()
+    pair.cur = cur
+    pair.corrupt = staticmethod(lambda cfg: cfg == (5, 0, 1))
+
+    def gather(obj):  # rank 1 agrees on timings; its verification is the same as ours
+        return [obj, obj]
+
+    r = wl.autotune(pair, 1 << 20, gather=gather, candidates=cands)
+    assert r["get"] == "reg_b256" and r["put"] == "reg_b256", r
+    assert "verification" in r["GiBps"]["fast_but_wrong"]["get"]["error"], r
