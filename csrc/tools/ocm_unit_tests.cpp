@@ -1,6 +1,7 @@
 // Native unit tests (no daemon, no GPU): wire layout, nodefile, range
 // allocator, governor placement policies, stripe geometry, host-tier arena.
 // Prints one line per test and exits non-zero on the first failure.
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -18,6 +19,7 @@
 #include "ocm/msg.h"
 #include "ocm/nodefile.h"
 #include "ocm/range_alloc.h"
+#include "ocm/shmlink.h"
 #include "ocm/siphash.h"
 
 using namespace ocm;
@@ -372,6 +374,75 @@ static void t_siphash() {
     CHECK(offsetof(Msg, u.hello.mac) == 32 + 24);
 }
 
+// The app <-> daemon shared-memory link (ocm/shmlink.h): order across ring
+// wrap-around, full rings, the wake-up flags, and what a hostile app can write
+// (forged slot numbers, a bogus count of replies taken, a wrong magic).
+static void t_shmlink() {
+    ShmLink app, dmn;
+    CHECK(app.create() == 0);
+    CHECK(dmn.attach(dup(app.fd())) == 0);
+    const size_t bytes = (sizeof(ShmLinkLayout) + 4095) & ~size_t(4095);
+    auto *raw = static_cast<ShmLinkLayout *>(mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, app.fd(), 0));
+    CHECK(raw != MAP_FAILED);
+    auto rec = [](uint64_t i) {
+        Msg m;
+        std::memset(&m, 0, sizeof(m));
+        m.type = MSG_PING;
+        m.seq = i;
+        m.u.raw[0] = (uint8_t)(i * 7);
+        return m;
+    };
+    // requests in bursts of 1..64 with wrap-around, taken in order
+    uint64_t posted = 0, taken = 0;
+    std::mt19937 rng(5);
+    for (int round = 0; round < 50; round++) {
+        const int burst = 1 + (int)(rng() % kShmLinkSlots);
+        for (int k = 0; k < burst; k++) CHECK(app.post_request(rec(++posted)));
+        CHECK(dmn.requests_pending());
+        Msg m;
+        while (dmn.take_request(&m)) {
+            ++taken;
+            CHECK(m.seq == taken && m.u.raw[0] == (uint8_t)(taken * 7));
+        }
+        CHECK(taken == posted && !dmn.requests_pending());
+    }
+    // a full request ring refuses the next record until one is taken
+    for (uint32_t k = 0; k < kShmLinkSlots; k++) CHECK(app.post_request(rec(++posted)));
+    CHECK(!app.post_request(rec(posted + 1)));
+    Msg m;
+    CHECK(dmn.take_request(&m) && m.seq == ++taken);
+    CHECK(app.post_request(rec(++posted)));
+    while (dmn.take_request(&m)) CHECK(m.seq == ++taken);
+    CHECK(taken == posted);
+    // replies: the same, and a bogus count of replies taken reads as a full ring
+    for (uint64_t i = 1; i <= 200; i++) {
+        CHECK(dmn.post_reply(rec(i)));
+        CHECK(app.replies_pending() && app.take_reply(&m) && m.seq == i);
+    }
+    raw->rsp_taken.store(1ull << 40);
+    int ok = 0;
+    while (ok < 1000 && dmn.post_reply(rec(1000 + ok))) ok++;
+    CHECK(ok <= (int)kShmLinkSlots);  // never more than one ring's worth past the app
+    // a forged slot number ahead of the daemon's count is not a record
+    const uint64_t next = taken + 1;
+    raw->req[(next - 1) % kShmLinkSlots].seq.store(next + 5);
+    CHECK(!dmn.requests_pending() && !dmn.take_request(&m));
+    // the wake-up flags (Dekker): a sleeping daemon must be woken, an awake one not
+    dmn.set_daemon_polling(false);
+    CHECK(app.request_needs_wake());
+    dmn.set_daemon_polling(true);
+    CHECK(!app.request_needs_wake());
+    app.set_app_waiting(true);
+    CHECK(dmn.reply_needs_wake());
+    app.set_app_waiting(false);
+    CHECK(!dmn.reply_needs_wake());
+    // a sealed memfd of the right size without the magic is refused
+    raw->magic = 0;
+    ShmLink bad;
+    CHECK(bad.attach(dup(app.fd())) != 0);
+    munmap(static_cast<void *>(raw), bytes);
+}
+
 int main(int argc, char **argv) {
     if (argc > 1 && std::strcmp(argv[1], "--nodefile") == 0) {
         // ocm_unit_tests --nodefile F...: parse each with the daemon's parser
@@ -396,7 +467,8 @@ int main(int argc, char **argv) {
                  {"governor_topology", t_governor_topology},
                  {"governor_checkpoint", t_governor_checkpoint},
                  {"stripe_geometry", t_stripe_geometry},
-                 {"arena_host", t_arena_host},   {"siphash", t_siphash}};
+                 {"arena_host", t_arena_host},   {"siphash", t_siphash},
+                 {"shmlink", t_shmlink}};
     for (auto &t : tests) {
         int before = g_fail;
         t.fn();
