@@ -206,6 +206,11 @@ private:
     TickRing *ring_ = nullptr;  // device-sealed collectives: their outbox (under mu_)
     uint64_t ring_sent_ = 0;    // ring records a completed tick of ours carried
     uint64_t ring_pub_ = 0;     // records appended (host shadow of ring_->published)
+    // OCM_TICK_STATS=1: post -> delivery latency of this rank's own records (device-sealed
+    // rings), and completed-tick periods, logged when the transport stops.
+    bool stats_ = false, stats_logged_ = false;
+    uint64_t post_ns_[kTickRing] = {};
+    uint64_t lat_sum_ns_ = 0, lat_n_ = 0, lat_max_ns_ = 0, period_sum_ns_ = 0, period_n_ = 0, last_done_ns_ = 0;
     void flush_ring();
     uint64_t unsent() const;
     int efd_ = -1;

@@ -1,6 +1,8 @@
 // ocmd entry point: `ocmd <nodefile> [options]` (reference: `oncillamem <nodefile>`,
 // src/main.c:187-224). Start one per GPU; rank0 is the master and must be
 // reachable within --join-timeout-ms by the others.
+#include <pthread.h>
+#include <signal.h>
 #include <cstdio>
 #include <string>
 
@@ -8,6 +10,16 @@
 #include "ocm/log.h"
 
 int main(int argc, char **argv) {
+    // Block the shutdown signals before anything can start a thread (the HIP
+    // runtime does, on first use): threads inherit the mask, so SIGTERM/SIGINT
+    // stay pending for the event loop's signalfd and the daemon shuts down in
+    // order (directory checkpoint, tick transport, data server). Blocked only
+    // later, a runtime thread would take the default action and kill the process.
+    sigset_t mask;
+    sigemptyset(&mask);
+    sigaddset(&mask, SIGINT);
+    sigaddset(&mask, SIGTERM);
+    pthread_sigmask(SIG_BLOCK, &mask, nullptr);
     ocm::DaemonConfig cfg;
     std::string err;
     const int rc = ocm::parse_daemon_args(argc, argv, &cfg, &err);

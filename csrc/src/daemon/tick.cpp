@@ -26,6 +26,12 @@ namespace ocm {
 
 namespace {
 
+uint64_t mono_now_ns() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
 uint64_t slot_rec_xor(const TickSlot &s, uint32_t n) {
     uint64_t x = 0;
     for (uint32_t r = 0; r < n; r++)
@@ -502,6 +508,8 @@ std::unique_ptr<Collective> make_socket_collective(const std::string &ns, int ra
 TickTransport::TickTransport(int rank, int nranks, CollectiveFactory factory)
     : rank_(rank), n_(nranks), factory_(std::move(factory)) {
     efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    const char *st = std::getenv("OCM_TICK_STATS");
+    stats_ = st && std::strcmp(st, "1") == 0;
 }
 
 TickTransport::~TickTransport() {
@@ -512,6 +520,12 @@ TickTransport::~TickTransport() {
 void TickTransport::start() { th_ = std::thread([this] { run(); }); }
 
 void TickTransport::stop() {
+    if (stats_ && lat_n_ && !stats_logged_)
+        OCM_INFO("rank %d: tick stats: %llu own records, post -> delivered %.2f us mean (max %.1f); %llu tick "
+                 "periods of %.2f us mean",
+                 rank_, (unsigned long long)lat_n_, lat_sum_ns_ / 1e3 / (double)lat_n_, lat_max_ns_ / 1e3,
+                 (unsigned long long)period_n_, period_n_ ? period_sum_ns_ / 1e3 / (double)period_n_ : 0.0);
+    stats_logged_ = true;
     if (!th_.joinable()) return;
     stop_ = true;
     {
@@ -553,6 +567,7 @@ void TickTransport::flush_ring() {
     while (!out_.empty() && pub - ring_sent_ < kTickRing) {
         TickRecord &r = ring_->rec[pub & (kTickRing - 1)];
         r = out_.front();
+        if (stats_) post_ns_[pub & (kTickRing - 1)] = mono_now_ns();
         ring_->tag[pub & (kTickRing - 1)] = tick_record_tag(reinterpret_cast<const uint64_t *>(&r), pub);
         out_.pop_front();
         pub++;
@@ -744,6 +759,20 @@ void TickTransport::run() {
             if (ring_) {
                 // Our own slot says how far the seals got through the outbox.
                 const TickSlot &mine = got[rank_];
+                if (stats_) {
+                    const uint64_t t = mono_now_ns();
+                    for (uint32_t r = 0; r < std::min<uint32_t>(mine.count, kTickMsgs); r++) {
+                        const uint64_t d = t - post_ns_[(mine.first + r) & (kTickRing - 1)];
+                        lat_sum_ns_ += d;
+                        lat_n_++;
+                        lat_max_ns_ = std::max(lat_max_ns_, d);
+                    }
+                    if (last_done_ns_) {
+                        period_sum_ns_ += t - last_done_ns_;
+                        period_n_++;
+                    }
+                    last_done_ns_ = t;
+                }
                 ring_sent_ = std::max<uint64_t>(ring_sent_, mine.first + std::min<uint32_t>(mine.count, kTickMsgs));
                 flush_ring();
             } else if (!inflight_n_.empty()) {

@@ -230,3 +230,17 @@ def test_threads_of_one_app_share_its_link(mesh_factory, monkeypatch):
         after = api.counters()
         assert after["n_link_rpc"] - before["n_link_rpc"] >= 8 * 60 * 2
         assert c.stats(0)["ctrl"] == "tcp"
+
+
+def test_daemons_shut_down_in_order_on_sigterm(mesh_factory, monkeypatch):
+    """SIGTERM reaches the event loop's signalfd (blocked before the HIP runtime
+    starts any thread), so a daemon leaves through its shutdown path and exits 0
+    instead of being killed by the signal's default action in some runtime thread."""
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    m = mesh_factory(2)
+    with api.Client(daemon_rank=1, ns=m.ns) as c:
+        c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20).free()
+    m.stop()
+    assert [d.proc.returncode for d in m.daemons] == [0, 0]
+    logs = m.logs()
+    assert logs.count("shutting down") == 2 and logs.count("exiting (allocs") == 2

@@ -47,10 +47,12 @@ def _run(ctrl, tick_self, env):
             r = _measure(m, tick_self)
             if tick_self and r["ticks"] == 0:
                 r["daemon_log"] = [l for l in m.logs().splitlines() if " W " in l or " E " in l][-5:]
-            return r
         except Exception:
             print(m.logs()[-4000:], file=sys.stderr)
             raise
+    if env.get("OCM_TICK_STATS") == "1":  # logged by the tick transport when the daemon stopped
+        r["tick_stats"] = [l.split("tick stats: ", 1)[1] for l in m.logs().splitlines() if "tick stats: " in l]
+    return r
 
 
 def _measure(m, tick_self):
@@ -85,6 +87,8 @@ VARIANTS = {
     "rccl_spec_nopin": ("rccl", True, {"OCM_PIN": "0"}),
     "tcp_pin": ("tcp", False, {"OCM_PIN": "1"}),
     # the app's reply spin and the daemon's post-activity spin at 300 us (default 50)
+    "rccl_stats": ("rccl", True, {"OCM_TICK_STATS": "1"}),
+    "rccl_stats_nowait": ("rccl", True, {"OCM_TICK_STATS": "1", "OCM_TICK_SEAL_WAIT_US": "0"}),
     "rccl_r03_old": ("rccl", True, {"OCM_TICK_DONE_KERNEL": "1", "OCM_TICK_SEAL_WAIT_US": "0"}),
     "rccl_tagged": ("rccl", True, {"OCM_TICK_DONE_KERNEL": "0"}),
     "rccl_wait3": ("rccl", True, {"OCM_TICK_SEAL_WAIT_US": "3"}),
