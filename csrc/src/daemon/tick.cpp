@@ -88,7 +88,9 @@ class RcclCollective : public Collective {
 public:
     ~RcclCollective() override {
         if (comm_) {
-            if (aborted_)
+            // A transport that is being stopped (daemon shutdown, a peer gone) aborts:
+            // ncclCommAbort never waits on peers that may already have left.
+            if (aborted_ || abort_req_.load())
                 (void)ncclCommAbort(comm_);
             else
                 (void)ncclCommDestroy(comm_);
