@@ -87,13 +87,14 @@ bool gathered_whole(const void *recv, int n, uint64_t tick) {
 class RcclCollective : public Collective {
 public:
     ~RcclCollective() override {
-        if (comm_) {
+        for (ncclComm_t c : {comm2_, comm_}) {
+            if (!c) continue;
             // A transport that is being stopped (daemon shutdown, a peer gone) aborts:
             // ncclCommAbort never waits on peers that may already have left.
             if (aborted_ || abort_req_.load())
-                (void)ncclCommAbort(comm_);
+                (void)ncclCommAbort(c);
             else
-                (void)ncclCommDestroy(comm_);
+                (void)ncclCommDestroy(c);
         }
         // Queued ticks read and write the slots: free them only once the stream
         // has drained (an abort ends a collective stuck on a dead peer). If it
@@ -104,7 +105,8 @@ public:
             bool drained = false;
             for (int i = 0; i < 20000 && !drained; i++) {
                 const hipError_t q = hipStreamQuery(stream_);
-                drained = q != hipErrorNotReady;
+                const hipError_t q2 = stream2_ ? hipStreamQuery(stream2_) : hipSuccess;
+                drained = q != hipErrorNotReady && q2 != hipErrorNotReady;
                 if (!drained) usleep(100);
             }
             (void)hipGetLastError();
@@ -115,6 +117,7 @@ public:
         }
         for (auto &sl : ring_) {
             if (sl.ev) (void)hipEventDestroy(sl.ev);
+            if (sl.sealed) (void)hipEventDestroy(sl.sealed);
             if (sl.hsend) (void)hipHostFree(sl.hsend);
             if (sl.hrecv) (void)hipHostFree(sl.hrecv);
             if (sealed_ || !mapped_) (void)hipFree(sl.dsend);
@@ -123,6 +126,7 @@ public:
         if (out_) (void)hipHostFree(out_);
         if (done_) (void)hipHostFree(done_);
         if (consumed_) (void)hipFree(consumed_);
+        if (stream2_) (void)hipStreamDestroy(stream2_);
         if (stream_) (void)hipStreamDestroy(stream_);
     }
     int init(int gpu, int rank, int n, const uint8_t *id, size_t bytes, std::string *err) {
@@ -145,8 +149,16 @@ public:
         const char *wv = std::getenv("OCM_TICK_SEAL_WAIT_US");
         wait_us_ = wv && *wv ? (uint32_t)std::max(0, std::atoi(wv)) : 6;
         const char *d = std::getenv("OCM_TICK_DEPTH");
-        const int depth = std::max(1, std::min(d && *d ? std::atoi(d) : (sealed_ ? 2 : 1), 64));
-        if (hipSetDevice(gpu) != hipSuccess || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+        int depth = std::max(1, std::min(d && *d ? std::atoi(d) : (sealed_ ? 2 : 1), 64));
+        // OCM_TICK_STREAMS=2 (sealed ticks): consecutive ticks alternate between two
+        // streams and two communicators (the second split from the first), so the next
+        // tick's seal waits for records while the previous allgather is still running;
+        // the seals stay in order through an event. Depth is then even.
+        const char *sv = std::getenv("OCM_TICK_STREAMS");
+        nstreams_ = (sealed_ && sv && std::atoi(sv) == 2) ? 2 : 1;
+        if (nstreams_ == 2 && depth % 2) depth++;
+        if (hipSetDevice(gpu) != hipSuccess || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
+            (nstreams_ == 2 && hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking) != hipSuccess)) {
             *err = "rccl: no stream on gpu " + std::to_string(gpu);
             return -1;
         }
@@ -165,6 +177,7 @@ public:
         ring_.resize((size_t)depth);
         for (auto &sl : ring_) {
             ok = ok && hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) == hipSuccess;
+            if (nstreams_ == 2) ok = ok && hipEventCreateWithFlags(&sl.sealed, hipEventDisableTiming) == hipSuccess;
             if (sealed_) {
                 ok = ok && hipMalloc(&sl.dsend, bytes) == hipSuccess;
             } else if (mapped_) {
@@ -208,6 +221,25 @@ public:
             *err = std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r);
             return -1;
         }
+        if (nstreams_ == 2) {
+            // every rank splits the same way (color 0, key = rank): the same membership
+            ncclConfig_t cfg2 = NCCL_CONFIG_INITIALIZER;
+            cfg2.blocking = 0;
+            r = ncclCommSplit(comm_, 0, rank, &comm2_, &cfg2);
+            while (r == ncclInProgress) {
+                if (abort_req_.load()) {
+                    aborted_ = true;
+                    *err = "rccl split aborted";
+                    return -1;
+                }
+                usleep(100);
+                if (ncclCommGetAsyncError(comm2_, &r) != ncclSuccess) break;
+            }
+            if (r != ncclSuccess) {
+                *err = std::string("ncclCommSplit: ") + ncclGetErrorString(r);
+                return -1;
+            }
+        }
         return 0;
     }
     void request_abort() { abort_req_ = true; }
@@ -220,25 +252,34 @@ public:
         Slot &sl = ring_[(size_t)i];
         (void)hipSetDevice(gpu_);
         const uint64_t seq = started_ + 1;
+        // two streams: tick i on stream i % 2 (depth is even, so consecutive ticks alternate)
+        hipStream_t st = (nstreams_ == 2 && (i & 1)) ? stream2_ : stream_;
+        ncclComm_t comm = (nstreams_ == 2 && (i & 1)) ? comm2_ : comm_;
         if (sealed_) {
             if (!out_dev_ || !consumed_ || !sl.dsend || !sl.drecv || !done_dev_) return why("tick slots missing");
+            if (nstreams_ == 2 && started_ > 0) {
+                // this seal follows the previous tick's seal (the outbox is consumed in order)
+                const Slot &prev = ring_[(size_t)((i + (int)ring_.size() - 1) % (int)ring_.size())];
+                if (hipStreamWaitEvent(st, prev.sealed, 0) != hipSuccess) return why("seal ordering");
+            }
             const hipError_t e =
-                tick_seal_launch(out_dev_, consumed_, static_cast<TickSlot *>(sl.dsend), seq, wait_us_, stream_);
+                tick_seal_launch(out_dev_, consumed_, static_cast<TickSlot *>(sl.dsend), seq, wait_us_, st);
             if (e != hipSuccess) return why(std::string("seal launch: ") + hipGetErrorString(e));
-        } else if (!mapped_ && hipMemcpyAsync(sl.dsend, sl.hsend, bytes_, hipMemcpyHostToDevice, stream_) != hipSuccess) {
+            if (nstreams_ == 2 && hipEventRecord(sl.sealed, st) != hipSuccess) return why("seal event");
+        } else if (!mapped_ && hipMemcpyAsync(sl.dsend, sl.hsend, bytes_, hipMemcpyHostToDevice, st) != hipSuccess) {
             return -1;
         }
-        const ncclResult_t nr = ncclAllGather(sl.dsend, sl.drecv, bytes_, ncclUint8, comm_, stream_);
+        const ncclResult_t nr = ncclAllGather(sl.dsend, sl.drecv, bytes_, ncclUint8, comm, st);
         if (nr != ncclSuccess) return why(std::string("ncclAllGather: ") + ncclGetErrorString(nr));
-        if (!mapped_ && hipMemcpyAsync(sl.hrecv, sl.drecv, bytes_ * (size_t)n_, hipMemcpyDeviceToHost, stream_) != hipSuccess)
+        if (!mapped_ && hipMemcpyAsync(sl.hrecv, sl.drecv, bytes_ * (size_t)n_, hipMemcpyDeviceToHost, st) != hipSuccess)
             return -1;
         sl.seq = ++started_;
         if (done_kernel_) {
-            const hipError_t de = tick_done_launch(done_dev_, sl.seq, stream_);
+            const hipError_t de = tick_done_launch(done_dev_, sl.seq, st);
             if (de != hipSuccess) return why(std::string("done launch: ") + hipGetErrorString(de));
         }
         if (ring_.size() == 1) return 0;
-        return hipEventRecord(sl.ev, stream_) == hipSuccess ? 0 : -1;
+        return hipEventRecord(sl.ev, st) == hipSuccess ? 0 : -1;
     }
     int test(int i) override {
         // Bounded by abort requests and RCCL async errors: a dead peer never
@@ -260,9 +301,12 @@ public:
         if (q == hipSuccess) return 1;
         if (q != hipErrorNotReady) return why(std::string("tick completion: ") + hipGetErrorString(q));
         {
-            ncclResult_t async = ncclSuccess;
-            if (ncclCommGetAsyncError(comm_, &async) == ncclSuccess && async != ncclSuccess && async != ncclInProgress)
-                return why(std::string("rccl async error: ") + ncclGetErrorString(async));
+            for (ncclComm_t c : {comm_, comm2_}) {
+                ncclResult_t async = ncclSuccess;
+                if (c && ncclCommGetAsyncError(c, &async) == ncclSuccess && async != ncclSuccess &&
+                    async != ncclInProgress)
+                    return why(std::string("rccl async error: ") + ncclGetErrorString(async));
+            }
         }
         return 0;
     }
@@ -279,6 +323,7 @@ private:
     struct Slot {
         void *hsend = nullptr, *hrecv = nullptr, *dsend = nullptr, *drecv = nullptr;
         hipEvent_t ev = nullptr;
+        hipEvent_t sealed = nullptr;  // two streams: after this tick's seal
         uint64_t seq = 0;  // tick number its done kernel stores
     };
     int gpu_ = 0, n_ = 1;
@@ -286,8 +331,9 @@ private:
     bool mapped_ = true, sealed_ = true, done_kernel_ = true;
     uint32_t wait_us_ = 0;
     unsigned polls_ = 0;
-    ncclComm_t comm_ = nullptr;
-    hipStream_t stream_ = nullptr;
+    ncclComm_t comm_ = nullptr, comm2_ = nullptr;
+    hipStream_t stream_ = nullptr, stream2_ = nullptr;
+    int nstreams_ = 1;
     std::vector<Slot> ring_;
     TickRing *out_ = nullptr, *out_dev_ = nullptr;  // sealed: the outbox (host view / device view)
     uint64_t *consumed_ = nullptr;                  // sealed: records sealed so far (HBM, this stream only)

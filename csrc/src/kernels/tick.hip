@@ -74,7 +74,9 @@ __global__ __launch_bounds__(64) void tick_seal2_kernel(const TickRing *ring, ui
 __global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uint64_t *consumed, TickSlot *slot,
                                                       uint64_t tick, uint64_t wait) {
     const int lane = threadIdx.x;
-    const uint64_t c = *consumed;  // this stream's own counter: plain load
+    // Seals run one at a time (one stream, or two alternating streams ordered by an
+    // event), but possibly on different queues: agent-scope (sc1) load and store.
+    const uint64_t c = __hip_atomic_load(consumed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t w[kTickRecordWords];
     uint64_t tag = 0, pub = 0;
     const uint64_t j = c + (uint64_t)lane;
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uin
         slot->first = c;
         slot->tick = tick;
         slot->tag = tick_slot_tag(n, busy, c, tick, rt);
-        *consumed = c + n;
+        __hip_atomic_store(consumed, c + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

@@ -146,6 +146,8 @@ RCCL_TICK_MODES = {
     "done_kernel_wait": {"OCM_TICK_DONE_KERNEL": "1"},
     "tagged_wait_seal2": {"OCM_TICK_DONE_KERNEL": "0", "OCM_TICK_SEAL_WAIT_US": "6", "OCM_TICK_SEAL_SPEC": "0"},
     "depth3_tagged_wait": {"OCM_TICK_DEPTH": "3", "OCM_TICK_DONE_KERNEL": "0", "OCM_TICK_SEAL_WAIT_US": "4"},
+    "two_streams": {"OCM_TICK_STREAMS": "2"},
+    "two_streams_depth3_done_kernel": {"OCM_TICK_STREAMS": "2", "OCM_TICK_DEPTH": "3", "OCM_TICK_DONE_KERNEL": "1"},
 }
 
 

@@ -87,6 +87,10 @@ VARIANTS = {
     "rccl_spec_nopin": ("rccl", True, {"OCM_PIN": "0"}),
     "tcp_pin": ("tcp", False, {"OCM_PIN": "1"}),
     # the app's reply spin and the daemon's post-activity spin at 300 us (default 50)
+    "rccl_2s": ("rccl", True, {"OCM_TICK_STREAMS": "2"}),
+    "rccl_2s_d4": ("rccl", True, {"OCM_TICK_STREAMS": "2", "OCM_TICK_DEPTH": "4"}),
+    "rccl_2s_w3": ("rccl", True, {"OCM_TICK_STREAMS": "2", "OCM_TICK_SEAL_WAIT_US": "3"}),
+    "rccl_2s_w10": ("rccl", True, {"OCM_TICK_STREAMS": "2", "OCM_TICK_SEAL_WAIT_US": "10"}),
     "rccl_stats": ("rccl", True, {"OCM_TICK_STATS": "1"}),
     "rccl_stats_nowait": ("rccl", True, {"OCM_TICK_STATS": "1", "OCM_TICK_SEAL_WAIT_US": "0"}),
     "rccl_r03_old": ("rccl", True, {"OCM_TICK_DONE_KERNEL": "1", "OCM_TICK_SEAL_WAIT_US": "0"}),
