@@ -52,6 +52,8 @@ static int recv_record(Msg *m, long deadline_ms, uint64_t spin_ns) {
             if (rc == 1 && m->type != MSG_WAKE) return 1;
         }
         if (now_ns() - t0 >= spin_ns) break;
+        // The daemon may be the other hardware thread of this core: leave it the pipeline.
+        if (link) __builtin_ia32_pause();
     }
     for (;;) {
         const long left = deadline_ms - now_ms();
