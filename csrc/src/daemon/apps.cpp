@@ -64,6 +64,15 @@ void Daemon::app_connect(const Msg &m, int fd) {
     App a;
     a.pid = pid;
     a.fd = fd;
+    // OCM_SHM_LINK_ACCEPT=0: take no links (apps then keep to the socket).
+    static const bool accept_links = [] {
+        const char *v = std::getenv("OCM_SHM_LINK_ACCEPT");
+        return !(v && std::strcmp(v, "0") == 0);
+    }();
+    if (pending_link_fd_ >= 0 && !accept_links) {
+        close(pending_link_fd_);
+        pending_link_fd_ = -1;
+    }
     if (pending_link_fd_ >= 0) {
         // The app offered a shared-memory link with its CONNECT (SCM_RIGHTS).
         auto link = std::make_shared<ShmLink>();

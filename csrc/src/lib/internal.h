@@ -183,7 +183,8 @@ struct State {
     pid_t pid = 0;
     std::string ns, daemon_mbox;
     Channel chan;
-    ShmLink link;  // shared-memory fast path to the daemon (OCM_SHM_LINK=0: the mailbox alone)
+    ShmLink link;
+    bool last_via_link = false;  // the last record recv_record returned came over the link  // shared-memory fast path to the daemon (OCM_SHM_LINK=0: the mailbox alone)
     NodeConfig daemon{};
     int daemon_rank = 0;
     int device = -1;

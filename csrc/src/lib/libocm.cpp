@@ -46,14 +46,24 @@ int ocm_init(void) {
     if (s.chan.connect(s.daemon_mbox, connect_ms) != 0)
         OCM_FAIL(-1, "no ocmd mailbox @%s (is the daemon running?)", s.daemon_mbox.c_str());
     // Shared-memory fast path of the mailbox (ocm/shmlink.h), offered with CONNECT.
-    if (env_int("OCM_SHM_LINK", 1) && s.link.create() != 0) OCM_WARN("no shared-memory link (%s); mailbox only", strerror(errno));
+    // Every CONNECT offers a fresh link: the daemon attaches each offer anew, with
+    // its ring counts at zero, so a retried CONNECT must not reuse a link whose
+    // counts have moved on.
+    const bool want_link = env_int("OCM_SHM_LINK", 1) != 0;
     Msg reply;
     for (;;) {
+        if (want_link && s.link.create() != 0) OCM_WARN("no shared-memory link (%s); mailbox only", strerror(errno));
         Msg c = new_msg(MSG_CONNECT);
         if (rpc(c, &reply, std::max(1000, connect_ms)) != 0) {
             s.chan.close();
             s.link.close();
             return -1;
+        }
+        if (s.link.ok() && !s.last_via_link) {
+            // The daemon answered on the socket: it did not take the link (it found it
+            // unusable, or does not take links at all). Requests stay on the socket.
+            OCM_INFO("ocmd declined the shared-memory link; using the mailbox socket");
+            s.link.close();
         }
         if (reply.err != EAGAIN) break;
         if (now_ms() > deadline) {

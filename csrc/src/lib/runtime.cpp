@@ -43,8 +43,9 @@ static int recv_record(Msg *m, long deadline_ms, uint64_t spin_ns) {
     State &s = S();
     const bool link = s.link.ok();
     const uint64_t t0 = now_ns();
+    s.last_via_link = false;
     for (unsigned i = 0;; i++) {
-        if (link && s.link.take_reply(m)) return 1;
+        if (link && s.link.take_reply(m)) return s.last_via_link = true, 1;
         // With a link the socket carries only wake-ups: look at it now and then.
         if (!link || (i & 63) == 0) {
             const int rc = s.chan.recv(m, kMsgBytes, 0);
@@ -62,7 +63,7 @@ static int recv_record(Msg *m, long deadline_ms, uint64_t spin_ns) {
             s.link.set_app_waiting(true);  // from here the daemon wakes us; look once more
             if (s.link.replies_pending()) {
                 s.link.set_app_waiting(false);
-                if (s.link.take_reply(m)) return 1;
+                if (s.link.take_reply(m)) return s.last_via_link = true, 1;
                 continue;
             }
         }
@@ -70,7 +71,7 @@ static int recv_record(Msg *m, long deadline_ms, uint64_t spin_ns) {
         if (link) {
             s.link.set_app_waiting(false);
             if (rc >= 0 && (rc == 0 || m->type == MSG_WAKE)) {
-                if (s.link.take_reply(m)) return 1;
+                if (s.link.take_reply(m)) return s.last_via_link = true, 1;
                 continue;
             }
         }

@@ -244,3 +244,64 @@ def test_daemons_shut_down_in_order_on_sigterm(mesh_factory, monkeypatch):
     assert [d.proc.returncode for d in m.daemons] == [0, 0]
     logs = m.logs()
     assert logs.count("shutting down") == 2 and logs.count("exiting (allocs") == 2
+
+
+def test_app_falls_back_to_the_socket_when_the_daemon_declines_its_link(mesh_factory, monkeypatch):
+    """A daemon that takes no links (OCM_SHM_LINK_ACCEPT=0, or one that found the
+    offered memfd unusable) answers CONNECT on the socket; the app sees that and
+    keeps every later request on the socket instead of waiting on a dead ring."""
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    m = mesh_factory(2, env={"OCM_SHM_LINK_ACCEPT": "0"})
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        before = api.counters()["n_link_rpc"]
+        for _ in range(20):
+            c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20).free()
+        assert api.counters()["n_link_rpc"] == before
+
+
+def test_connect_retries_while_the_mesh_joins_keep_the_link_in_step(monkeypatch, tmp_path):
+    """An app that connects before its daemon's mesh is complete is told EAGAIN and
+    CONNECTs again; each attempt offers a fresh link (the daemon attaches every offer
+    with its counts at zero), so the app's requests after the join still ride the link."""
+    import threading
+    import time
+
+    import uuid
+
+    from oncilla_amd.parallel.mesh import Mesh, free_ports
+
+    monkeypatch.setenv("OCM_NO_GPU", "1")
+    ns, ports, key = f"m{uuid.uuid4().hex[:10]}", free_ports(2), "k" * 32
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    m0 = Mesh(2, ns=ns, ports=ports, ranks=[0], key=key, workdir=str(tmp_path / "a"))
+    m1 = Mesh(2, ns=ns, ports=ports, ranks=[1], key=key, workdir=str(tmp_path / "b"))
+    errs = []
+    starter = threading.Thread(target=lambda: m0.start(timeout=60))
+    starter.start()
+    try:
+        time.sleep(0.3)
+        box = {}
+
+        def connect():
+            try:
+                box["c"] = api.Client(daemon_rank=0, ns=ns).__enter__()
+            except Exception as e:  # noqa: BLE001 - reported below
+                errs.append(e)
+
+        t = threading.Thread(target=connect)
+        t.start()
+        time.sleep(1.0)  # the app keeps getting EAGAIN: rank 1 is not up yet
+        m1.start(timeout=60)
+        t.join(30)
+        starter.join(30)
+        assert not errs and "c" in box, errs
+        c = box["c"]
+        before = api.counters()["n_link_rpc"]
+        for _ in range(10):
+            c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20).free()
+        assert api.counters()["n_link_rpc"] - before >= 20
+        c.__exit__(None, None, None)
+    finally:
+        m1.stop()
+        m0.stop()
