@@ -68,3 +68,13 @@ def test_fuzz_apps_share_a_mesh_cpu(native, mesh_factory, monkeypatch):
 @pytest.mark.gpu
 def test_fuzz_apps_share_a_mesh_gpu(native, mesh_factory):
     _procs(mesh_factory, dict(os.environ), 15, 16 << 20)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto", ["7", "1", "9"])
+def test_fuzz_service_protocols_gpu(native, proto):
+    """The copy service's other hand-off protocols stay correct now that the default
+    (15) completes gangs through per-workgroup done words: 7 = the device-scope
+    counter, 1 = write-through without the gang record (relayed gangs), 9 = that
+    with per-workgroup done words."""
+    _run(8, dict(os.environ, OCM_SERVICE_PROTO=proto), 16 << 20, ("--configs", "hbm,host"))
