@@ -425,16 +425,20 @@ def main() -> int:
         def latency(flags):
             def run():
                 st0, _ = _local(lambda: client.stats(rank))
+                link0 = api.counters()["n_link_rpc"]
                 lat_remote = wl.alloc_latency(client, remote_kind, args.alloc_samples, local_bytes=64 << 10,
                                               remote_bytes=1 << 20, flags=flags)
+                link1 = api.counters()["n_link_rpc"]
                 st1, _ = _local(lambda: client.stats(rank))
                 lat_local = wl.alloc_latency(client, api.OCM_LOCAL_HOST, args.alloc_samples, local_bytes=1 << 20)
                 leases = st1["lease_allocs"] if st1 else None
                 if st0 and st1:
                     # How the remote allocations were served: carved from a capacity lease
                     # (no daemon<->daemon record) or through the mesh on the control transport.
+                    # app_link_rpcs: the app's requests that rode the shared-memory link to its daemon
                     lat_remote["via"] = {"lease": st1["lease_allocs"] - st0["lease_allocs"],
-                                         "ctrl": st1["ctrl"], "ctrl_ticks": st1["ctrl_ticks"] - st0["ctrl_ticks"]}
+                                         "ctrl": st1["ctrl"], "ctrl_ticks": st1["ctrl_ticks"] - st0["ctrl_ticks"],
+                                         "app_link_rpcs": link1 - link0}
                 return lat_remote, lat_local, leases
 
             return run
