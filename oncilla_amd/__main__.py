@@ -83,6 +83,16 @@ def _build(args) -> int:
     return 0
 
 
+def _selftest(args) -> int:
+    import json
+
+    from .utils.selftest import format_report, run
+
+    rep = run(gpus=args.gpus, ns=args.ns, nbytes=args.bytes, daemons=args.daemons)
+    print(json.dumps(rep) if args.json else format_report(rep))
+    return 0 if rep["ok"] else 1
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="python -m oncilla_amd", description=__doc__.splitlines()[0])
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -91,7 +101,7 @@ def main(argv=None) -> int:
     m.add_argument("--daemons", type=int, default=0, help="daemons (default: one per GPU)")
     m.add_argument("--policy", default="stripe", choices=["ring", "least_loaded", "stripe", "loopback"])
     m.add_argument("--ns", default=None)
-    m.add_argument("--ctrl", default=None, choices=["tcp", "rccl", "socket"])
+    m.add_argument("--ctrl", default=None, choices=["auto", "tcp", "rccl", "socket"])
     m.add_argument("--state-file", default=None, help="rank0 directory checkpoint")
     m.add_argument("--keep-going", action="store_true", help="keep running when a daemon exits")
     s = sub.add_parser("stats", help="print every daemon's counters")
@@ -103,8 +113,15 @@ def main(argv=None) -> int:
     x.add_argument("--rank", type=int, default=0, help="daemon to attach to")
     b = sub.add_parser("build", help="build the native tree (CMake + Ninja, gfx950)")
     b.add_argument("--sanitize", default=None, choices=["address", "thread"])
+    t = sub.add_parser("selftest", help="verified put/get through every owner daemon, rates, alloc latency, xGMI diagnosis")
+    t.add_argument("--gpus", type=int, default=None, help="GPUs for a temporary mesh (default: all visible)")
+    t.add_argument("--daemons", type=int, default=None, help="daemons of the temporary mesh (default: one per GPU)")
+    t.add_argument("--ns", default=None, help="test this running mesh instead of starting one")
+    t.add_argument("--bytes", type=int, default=64 << 20)
+    t.add_argument("--json", action="store_true", help="one JSON object instead of the summary")
     args = ap.parse_args(argv)
-    return {"mesh": _mesh, "stats": _stats, "metrics": _metrics, "build": _build}[args.cmd](args)
+    return {"mesh": _mesh, "stats": _stats, "metrics": _metrics, "build": _build,
+            "selftest": _selftest}[args.cmd](args)
 
 
 if __name__ == "__main__":

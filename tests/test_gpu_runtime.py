@@ -616,3 +616,14 @@ def test_torch_pool_random_churn(mesh_factory):
         torch.cuda.synchronize()
         assert RemoteMemPool.stats()["blocks"] == 0
 
+
+
+@pytest.mark.gpu
+def test_selftest_on_this_node():
+    """The node self-test on the GPU box: every owner daemon's round trip verified
+    (one GPU: the daemon's pinned host tier), rates reported."""
+    from oncilla_amd.utils.selftest import run
+
+    rep = run(nbytes=16 << 20, samples=50)
+    assert rep["ok"], rep
+    assert all(p["get_GiBps"] > 1 and p["put_GiBps"] > 1 for p in rep["peers"].values()), rep

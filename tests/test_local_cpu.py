@@ -305,3 +305,21 @@ def test_connect_retries_while_the_mesh_joins_keep_the_link_in_step(monkeypatch,
     finally:
         m1.stop()
         m0.stop()
+
+
+def test_selftest_cli_cpu(monkeypatch):
+    """`python -m oncilla_amd selftest`: a temporary mesh, one verified round trip per
+    owner daemon, exit code 0, and the JSON report's fields."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, OCM_NO_GPU="1")
+    r = subprocess.run([sys.executable, "-m", "oncilla_amd", "selftest", "--daemons", "3", "--bytes", str(1 << 20),
+                        "--json"], capture_output=True, text=True, timeout=120, env=env,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stdout + r.stderr
+    rep = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rep["ok"] and rep["daemons"] == 3 and sorted(rep["peers"]) == ["1", "2"]
+    assert all(p["ok"] and p["bad_words"] == 0 for p in rep["peers"].values())
+    assert rep["xgmi"] is False and rep["ctrl"] == "tcp"
