@@ -51,10 +51,13 @@ def run(gpus: Optional[int] = None, ns: Optional[str] = None, nbytes: int = 64 <
                 row: dict = {}
                 a = None
                 try:
-                    a = c.alloc(kind, local_bytes=nbytes, remote_bytes=nbytes, remote_rank=r)
+                    # one daemon: its placement (the pinned host tier, as in bench.py N=1);
+                    # several: a pair on each other daemon in turn
+                    a = c.alloc(kind, local_bytes=nbytes, remote_bytes=nbytes, remote_rank=r if r != 0 else -1)
                     ext = a.remote_info()["extents"]
                     row["tier"] = "+".join(sorted({{1: "host", 2: "hbm"}.get(e["tier"], "?") for e in ext}))
                     row["owner_gpu"] = ext[0].get("owner_gpu")
+                    row["same_gpu"] = row["tier"] == "hbm" and row["owner_gpu"] == c.device
                     seed = 4242 + r
                     a.fill(seed)
                     a.put(0, 0, nbytes)  # first touch of the mapping, untimed
@@ -89,7 +92,8 @@ def format_report(rep: dict) -> str:
              f"  remote ocm_alloc p50 {rep['alloc_p50_us']} us (p99 {rep['alloc_p99_us']})"]
     for r, p in rep["peers"].items():
         if p.get("ok"):
-            lines.append(f"  owner rank {r} ({p['tier']}, gpu {p['owner_gpu']}): put {p['put_GiBps']} GiB/s, "
+            where = f"{p['tier']}, gpu {p['owner_gpu']}{', same GPU as this process' if p.get('same_gpu') else ''}"
+            lines.append(f"  owner rank {r} ({where}): put {p['put_GiBps']} GiB/s, "
                          f"get {p['get_GiBps']} GiB/s, round trip verified")
         else:
             lines.append(f"  owner rank {r}: FAILED {p.get('error') or str(p.get('bad_words')) + ' words wrong'}")
