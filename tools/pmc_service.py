@@ -2,7 +2,9 @@
 
 On a loopback HBM pair (the owner daemon's HBM, IPC-mapped) and a pinned host-tier pair it runs:
 - 200 blocking 1 MiB puts and 200 gets: one resident service_kernel dispatch serves all of them;
-- 8 puts and 8 gets of 256 MiB: xfer kernel launches.
+- 8 puts and 8 gets of 256 MiB: xfer kernel launches (on the host tier: the PCIe streaming kernel);
+- 4 fused remote-Adam steps over 64 Mi fp32 parameters with the moments in the host tier (round 3's
+  PCIe variant of the kernel).
 Per-dispatch FETCH_SIZE / WRITE_SIZE then show how many bytes each kernel moved for the bytes requested,
 including the service's polling overhead.
 
@@ -33,6 +35,18 @@ def main() -> None:
                     a.get(0, 0, n)
                 a.free()
                 print(f"{tier}: 200 x 1 MiB put + get (service), 8 x 256 MiB put + get (launches)", flush=True)
+            import torch
+
+            from oncilla_amd.models import OffloadedAdam
+
+            p = torch.zeros(64 << 20, device="cuda:0").requires_grad_()
+            p.grad = torch.randn(64 << 20, device="cuda:0")
+            opt = OffloadedAdam([p], c, lr=1e-3, flags=api.OCM_ALLOC_HOST_TIER)
+            for _ in range(4):
+                opt.step()
+            opt.synchronize()
+            opt.close()
+            print("adam: 4 fused steps, 64 Mi params, moments in the host tier", flush=True)
 
 
 if __name__ == "__main__":
