@@ -2,7 +2,7 @@
 # kernel stats of the bench, the 4-rank shared-GPU rehearsal of the N>1 path,
 # the GPU suite, smoke. A fault, abort, segfault or time limit ends the script.
 set -o pipefail
-OUT=gpurun_out/r03f
+OUT=${OUT:-gpurun_out/r03f}
 mkdir -p $OUT
 export TMPDIR=/tmp
 fatal() { case $1 in 124|134|137|139) return 0 ;; *) return 1 ;; esac; }
