@@ -211,6 +211,7 @@ private:
     bool stats_ = false, stats_logged_ = false;
     uint64_t post_ns_[kTickRing] = {};
     uint64_t lat_sum_ns_ = 0, lat_n_ = 0, lat_max_ns_ = 0, period_sum_ns_ = 0, period_n_ = 0, last_done_ns_ = 0;
+    uint64_t start_sum_ns_ = 0, start_n_ = 0, start_max_ns_ = 0;  // host time inside Collective::start
     void flush_ring();
     uint64_t unsent() const;
     int efd_ = -1;

@@ -570,9 +570,11 @@ void TickTransport::start() { th_ = std::thread([this] { run(); }); }
 void TickTransport::stop() {
     if (stats_ && lat_n_ && !stats_logged_)
         OCM_INFO("rank %d: tick stats: %llu own records, post -> delivered %.2f us mean (max %.1f); %llu tick "
-                 "periods of %.2f us mean",
+                 "periods of %.2f us mean; start() %.2f us mean (max %.1f) over %llu ticks",
                  rank_, (unsigned long long)lat_n_, lat_sum_ns_ / 1e3 / (double)lat_n_, lat_max_ns_ / 1e3,
-                 (unsigned long long)period_n_, period_n_ ? period_sum_ns_ / 1e3 / (double)period_n_ : 0.0);
+                 (unsigned long long)period_n_, period_n_ ? period_sum_ns_ / 1e3 / (double)period_n_ : 0.0,
+                 start_n_ ? start_sum_ns_ / 1e3 / (double)start_n_ : 0.0, start_max_ns_ / 1e3,
+                 (unsigned long long)start_n_);
     stats_logged_ = true;
     if (!th_.joinable()) return;
     stop_ = true;
@@ -763,10 +765,17 @@ void TickTransport::run() {
                 }
                 if (announce_.load()) signal();  // let the event loop wake the peers first
                 lk.unlock();
+                const uint64_t t0 = mono_ns();
                 const int rc = coll->start(i);
+                const uint64_t t1 = mono_ns();
                 lk.lock();
                 if (rc != 0) break;
-                issued_at[(size_t)i] = mono_ns();
+                if (stats_) {
+                    start_sum_ns_ += t1 - t0;
+                    start_n_++;
+                    start_max_ns_ = std::max(start_max_ns_, t1 - t0);
+                }
+                issued_at[(size_t)i] = t1;
                 issued++;
             }
             if (issued < target && issued - done < depth) {  // start() failed
