@@ -118,9 +118,11 @@ void tick_slot_seal_tag(TickSlot *s, uint64_t tick);
 // `tick`: the tick's number (stored with the slot's tag). `wait_us`: when the
 // ring holds nothing unsent, the seal polls it for up to this long before it
 // seals an empty slot, so a record the host posts right after the previous
-// tick completed still rides this one (OCM_TICK_SEAL_WAIT_US).
+// tick completed still rides this one (OCM_TICK_SEAL_WAIT_US). `tick_ctr`
+// (device memory, graph-captured ticks): the seal numbers the tick itself,
+// *tick_ctr + 1, and stores that back; `tick` is then ignored.
 hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, uint64_t tick, uint32_t wait_us,
-                            hipStream_t stream);
+                            hipStream_t stream, uint64_t *tick_ctr = nullptr);
 // Queue a one-lane kernel that stores `seq` to `flag` (pinned, device-mapped
 // host memory) at system scope: the host sees a tick end ~6 us sooner than
 // through an event query (tools/launch_probe.hip, profiles/launch_flag_r01.json).
@@ -133,6 +135,13 @@ public:
     // rank's slot i into recv_slots(i) (rank-major), test(i) reports it done.
     // Ticks on different slots may be in flight together (stream-ordered).
     virtual int depth() const { return 1; }
+    // Ticks one start() queues: start(i) runs slots i .. i + K - 1 (i a multiple
+    // of K; depth() a multiple of 2K). K > 1: a graph of K captured ticks.
+    virtual int ticks_per_start() const { return 1; }
+    // Every rank rounds its tick target up to a multiple of this (the configured
+    // K, the same on every rank), so a rank whose graphs could not be captured
+    // and queues ticks one at a time still joins exactly the same collectives.
+    virtual int tick_quantum() const { return ticks_per_start(); }
     // Device-sealed collectives expose their outbox ring; the transport then
     // appends records there instead of filling send slots (host-filled: null).
     virtual TickRing *ring() { return nullptr; }

@@ -115,6 +115,9 @@ public:
                 return;
             }
         }
+        for (hipGraphExec_t &g : gexec_)
+            if (g) (void)hipGraphExecDestroy(g);
+        if (tick_ctr_) (void)hipFree(tick_ctr_);
         for (auto &sl : ring_) {
             if (sl.ev) (void)hipEventDestroy(sl.ev);
             if (sl.sealed) (void)hipEventDestroy(sl.sealed);
@@ -157,6 +160,17 @@ public:
         const char *sv = std::getenv("OCM_TICK_STREAMS");
         nstreams_ = (sealed_ && sv && std::atoi(sv) == 2) ? 2 : 1;
         if (nstreams_ == 2 && depth % 2) depth++;
+        // OCM_TICK_GRAPH=K: ticks are queued K at a time as one replay of a captured
+        // hipGraph (seal + allgather per tick, the seal numbering the tick from a
+        // device counter), two graphs over 2K slots. One tick queued through the
+        // runtime and RCCL costs the host 6.6-9.2 us, more than the tick itself
+        // runs on the GPU (profiles/tick_timeline_r03.json).
+        const char *gv = std::getenv("OCM_TICK_GRAPH");
+        graph_k_ = gv && *gv ? std::max(0, std::min(std::atoi(gv), 32)) : kGraphDefault;
+        if (graph_k_ <= 1 || !sealed_ || done_kernel_ || !mapped_ || nstreams_ != 1) graph_k_ = 0;
+        quantum_ = std::max(1, graph_k_);
+        plain_depth_ = depth;
+        if (graph_k_) depth = 2 * graph_k_;
         if (hipSetDevice(gpu) != hipSuccess || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
             (nstreams_ == 2 && hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking) != hipSuccess)) {
             *err = "rccl: no stream on gpu " + std::to_string(gpu);
@@ -240,10 +254,57 @@ public:
                 return -1;
             }
         }
+        if (graph_k_ && capture_graphs() != 0) {
+            OCM_WARN("rccl tick graphs unavailable (%s): ticks are queued one at a time", err_.c_str());
+            err_.clear();
+            graph_k_ = 0;
+        } else if (graph_k_) {
+            OCM_INFO("rank %d: %d ticks per captured graph, two graphs over %d slots", rank, graph_k_, 2 * graph_k_);
+        }
+        return 0;
+    }
+    // Two graphs of graph_k_ ticks each: graph g holds slots g*K .. g*K + K - 1.
+    int capture_graphs() {
+        const int k = graph_k_;
+        if (hipMalloc(reinterpret_cast<void **>(&tick_ctr_), sizeof(uint64_t)) != hipSuccess ||
+            hipMemsetAsync(tick_ctr_, 0, sizeof(uint64_t), stream_) != hipSuccess ||
+            hipStreamSynchronize(stream_) != hipSuccess) {
+            (void)hipGetLastError();
+            return why("tick counter");
+        }
+        for (int g = 0; g < 2; g++) {
+            if (hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+                (void)hipGetLastError();
+                return why("begin capture");
+            }
+            bool ok = true;
+            for (int j = 0; j < k && ok; j++) {
+                Slot &sl = ring_[(size_t)(g * k + j)];
+                ok = tick_seal_launch(out_dev_, consumed_, static_cast<TickSlot *>(sl.dsend), 0, wait_us_, stream_,
+                                      tick_ctr_) == hipSuccess &&
+                     ncclAllGather(sl.dsend, sl.drecv, bytes_, ncclUint8, comm_, stream_) == ncclSuccess;
+            }
+            hipGraph_t graph = nullptr;
+            const hipError_t ec = hipStreamEndCapture(stream_, &graph);
+            if (!ok || ec != hipSuccess || !graph) {
+                if (graph) (void)hipGraphDestroy(graph);
+                (void)hipGetLastError();
+                return why(ok ? "end capture" : "captured tick");
+            }
+            const hipError_t ei = hipGraphInstantiate(&gexec_[g], graph, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(graph);
+            if (ei != hipSuccess) {
+                gexec_[g] = nullptr;
+                (void)hipGetLastError();
+                return why(std::string("instantiate: ") + hipGetErrorString(ei));
+            }
+        }
         return 0;
     }
     void request_abort() { abort_req_ = true; }
-    int depth() const override { return (int)ring_.size(); }
+    int depth() const override { return graph_k_ ? 2 * graph_k_ : plain_depth_; }
+    int ticks_per_start() const override { return graph_k_ ? graph_k_ : 1; }
+    int tick_quantum() const override { return quantum_; }
     TickRing *ring() override { return sealed_ ? out_ : nullptr; }
     void *send_slot(int i) override { return ring_[(size_t)i].hsend; }
     const void *recv_slots(int i) override { return ring_[(size_t)i].hrecv; }
@@ -251,6 +312,13 @@ public:
         if (aborted_) return -1;
         Slot &sl = ring_[(size_t)i];
         (void)hipSetDevice(gpu_);
+        if (graph_k_) {
+            if (i % graph_k_) return why("graph ticks start on a multiple of K");
+            const hipError_t e = hipGraphLaunch(gexec_[(i / graph_k_) & 1], stream_);
+            if (e != hipSuccess) return why(std::string("tick graph launch: ") + hipGetErrorString(e));
+            for (int j = 0; j < graph_k_; j++) ring_[(size_t)(i + j)].seq = ++started_;
+            return 0;
+        }
         const uint64_t seq = started_ + 1;
         // two streams: tick i on stream i % 2 (depth is even, so consecutive ticks alternate)
         hipStream_t st = (nstreams_ == 2 && (i & 1)) ? stream2_ : stream_;
@@ -297,7 +365,8 @@ public:
         // RCCL's async error (a dead peer never joins the collective).
         // One tick in flight: the stream is exactly that tick, and a stream query
         // measured cheaper than an event query (profiles/ctrl_probe_r02c.json).
-        const hipError_t q = ring_.size() == 1 ? hipStreamQuery(stream_) : hipEventQuery(ring_[(size_t)i].ev);
+        // (graph ticks record no events: a drained stream has finished them all)
+        const hipError_t q = (ring_.size() == 1 || graph_k_) ? hipStreamQuery(stream_) : hipEventQuery(ring_[(size_t)i].ev);
         if (q == hipSuccess) return 1;
         if (q != hipErrorNotReady) return why(std::string("tick completion: ") + hipGetErrorString(q));
         {
@@ -339,6 +408,11 @@ private:
     uint64_t *consumed_ = nullptr;                  // sealed: records sealed so far (HBM, this stream only)
     uint64_t *done_ = nullptr, *done_dev_ = nullptr;  // last tick whose done kernel ran (pinned host)
     uint64_t started_ = 0;
+    static constexpr int kGraphDefault = 0;
+    int graph_k_ = 0, plain_depth_ = 1;    // OCM_TICK_GRAPH: ticks per graph replay (0: none)
+    int quantum_ = 1;                      // the configured K, kept if capturing fails
+    hipGraphExec_t gexec_[2] = {nullptr, nullptr};
+    uint64_t *tick_ctr_ = nullptr;            // graph ticks: the last tick number a seal took (HBM)
     std::atomic<bool> abort_req_{false};
     bool aborted_ = false;
 };
@@ -362,7 +436,6 @@ public:
         n_ = n;
         bytes_ = bytes;
         send_.assign(bytes, 0);
-        recv_.assign(bytes * (size_t)n, 0);
         const char *tf = std::getenv("OCM_TICK_FAULT");
         fault_do_alloc_ = tf && std::strcmp(tf, "fail_after_do_alloc") == 0 && bytes == sizeof(TickSlot);
         // stall_after=N: from tick N on this rank stops taking part, without an error
@@ -374,7 +447,17 @@ public:
         if (sl && std::strcmp(sl, "1") == 0 && bytes == sizeof(TickSlot)) {
             outbox_.reset(new TickRing());
             std::memset(outbox_.get(), 0, sizeof(TickRing));
+            // OCM_TICK_SOCKET_BATCH=K: start() runs K ticks, like a replay of the RCCL
+            // collective's captured graph of K ticks (OCM_TICK_GRAPH), over 2K slots.
+            const char *bv = std::getenv("OCM_TICK_SOCKET_BATCH");
+            batch_ = bv && *bv ? std::max(1, std::min(std::atoi(bv), 32)) : 1;
+            quantum_ = batch_;
+            // OCM_TICK_FAULT=no_batch (tests): this rank queues its ticks one at a
+            // time, as an RCCL rank whose graph capture failed does
+            if (tf && std::strcmp(tf, "no_batch") == 0) batch_ = 1;
         }
+        recv_.assign(quantum_ > 1 ? 2 * (size_t)quantum_ : 1, std::vector<char>(bytes * (size_t)n, 0));
+        slot_tick_.assign(recv_.size(), 0);
         if (n == 1) return 0;
         listen_ = mbox_listen("ocm_" + ns + "_coll" + std::to_string(rank), 4);
         if (listen_ < 0) {
@@ -397,10 +480,19 @@ public:
         }
         return 0;
     }
+    int depth() const override { return (int)recv_.size(); }
+    int ticks_per_start() const override { return batch_; }
+    int tick_quantum() const override { return quantum_; }
     void *send_slot(int) override { return send_.data(); }
-    const void *recv_slots(int) override { return recv_.data(); }
+    const void *recv_slots(int i) override { return recv_[(size_t)i % recv_.size()].data(); }
     TickRing *ring() override { return outbox_.get(); }
-    int start(int) override {
+    int start(int i) override {
+        if (i % batch_) return -1;
+        for (int j = 0; j < batch_; j++)
+            if (tick((size_t)(i + j) % recv_.size()) != 0) return -1;
+        return 0;
+    }
+    int tick(size_t slot_i) {
         if (outbox_) {  // what tick_seal_kernel does, when the tick runs
             TickSlot *slot = reinterpret_cast<TickSlot *>(send_.data());
             const uint64_t pub = __atomic_load_n(&outbox_->published, __ATOMIC_ACQUIRE);
@@ -412,12 +504,13 @@ public:
             slot->first = consumed_;
             consumed_ += n;
             tick_slot_seal_tag(slot, ++ticks_);
+            slot_tick_[slot_i] = ticks_;
         }
         if (stall_after_ > 0 && ++started_ >= (uint64_t)stall_after_) {
             while (!aborted_) usleep(1000);  // wedged until the transport is torn down
             return -1;
         }
-        char *out = recv_.data();
+        char *out = recv_[slot_i].data();
         std::memcpy(out + (size_t)rank_ * bytes_, send_.data(), bytes_);
         // Ring: at step s send block (rank - s) right, receive block (rank - s - 1) from the left.
         for (int s = 0; s < n_ - 1; s++) {
@@ -428,11 +521,12 @@ public:
         }
         return 0;
     }
-    int test(int) override {
+    int test(int i) override {
         if (aborted_) return -1;
         // Sealed emulation: every gathered slot must check out as the RCCL path's
         // done-kernel-less completion requires (same tags, computed on the host).
-        if (outbox_ && !gathered_whole(recv_.data(), n_, ticks_)) {
+        const size_t si = (size_t)i % recv_.size();
+        if (outbox_ && !gathered_whole(recv_[si].data(), n_, slot_tick_[si])) {
             error_ = "gathered tick slot failed its tag check";
             return -1;
         }
@@ -490,7 +584,10 @@ private:
     }
     int rank_ = 0, n_ = 1, left_ = -1, right_ = -1, listen_ = -1;
     size_t bytes_ = 0;
-    std::vector<char> send_, recv_;
+    std::vector<char> send_;
+    std::vector<std::vector<char>> recv_;  // one gathered buffer per slot
+    std::vector<uint64_t> slot_tick_;      // sealed emulation: the tick each slot carried
+    int batch_ = 1, quantum_ = 1;          // OCM_TICK_SOCKET_BATCH
     std::unique_ptr<TickRing> outbox_;  // OCM_TICK_SOCKET_SEAL
     uint64_t consumed_ = 0;
     std::atomic<bool> aborted_{false};
@@ -518,6 +615,9 @@ int rccl_unique_id(uint8_t out[128], std::string *err) {
 
 std::unique_ptr<Collective> make_rccl_collective(int gpu, int rank, int nranks, const uint8_t *id, size_t slot_bytes,
                                                  std::string *err, const std::atomic<bool> *cancel) {
+    // Captured ticks (OCM_TICK_GRAPH) use plain buffers: no registration of
+    // user buffers with the peers while capturing.
+    setenv("NCCL_GRAPH_REGISTER", "0", 0);
     auto c = std::make_unique<RcclCollective>();
     std::atomic<bool> done{false};
     std::thread watch;
@@ -703,6 +803,10 @@ void TickTransport::run() {
     }
     Collective *coll = coll_.get();
     const uint64_t depth = (uint64_t)std::max(1, coll->depth());
+    // Ticks are queued `per` at a time (a captured graph of `per` ticks); every
+    // rank rounds its target up to the same multiple of `quantum`.
+    const uint64_t per = (uint64_t)std::max(1, coll->ticks_per_start());
+    const uint64_t quantum = (uint64_t)std::max(1, coll->tick_quantum());
     {
         std::lock_guard<std::mutex> lk(mu_);
         ring_ = coll->ring();
@@ -748,8 +852,9 @@ void TickTransport::run() {
                 }
             }
             target = std::max(target, wake_upto_.load());
+            target = (target + quantum - 1) / quantum * quantum;
             // Queue ticks up to the target, at most `depth` in flight.
-            while (issued < target && issued - done < depth) {
+            while (issued < target && issued - done + per <= depth) {
                 const int i = (int)(issued % depth);
                 if (!ring_) {  // host-filled: the slot's records are fixed now
                     TickSlot *slot = static_cast<TickSlot *>(coll->send_slot(i));
@@ -775,10 +880,10 @@ void TickTransport::run() {
                     start_n_++;
                     start_max_ns_ = std::max(start_max_ns_, t1 - t0);
                 }
-                issued_at[(size_t)i] = t1;
-                issued++;
+                for (uint64_t j = 0; j < per; j++) issued_at[(size_t)((issued + j) % depth)] = t1;
+                issued += per;
             }
-            if (issued < target && issued - done < depth) {  // start() failed
+            if (issued < target && issued - done + per <= depth) {  // start() failed
                 lk.unlock();
                 fail();
                 break;
@@ -798,7 +903,7 @@ void TickTransport::run() {
                 coll->abort();
                 break;
             }
-            if (issued - done < depth && (spins & 15) == 15) break;
+            if (issued - done + per <= depth && (spins & 15) == 15) break;
         }
         if (t < 0) {
             if (timed_out_ && !stop_)

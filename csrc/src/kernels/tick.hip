@@ -35,7 +35,7 @@ __device__ __forceinline__ uint64_t wave_xor64(uint64_t v) {
 }
 
 __global__ __launch_bounds__(64) void tick_seal2_kernel(const TickRing *ring, uint64_t *consumed, TickSlot *slot,
-                                                       uint64_t tick) {
+                                                       uint64_t tick, uint64_t *ctr) {
     const int lane = threadIdx.x;
     const uint64_t c = *consumed;  // this stream's own counter: plain load
     const uint64_t pub = sys_load(&ring->published);
@@ -52,6 +52,7 @@ __global__ __launch_bounds__(64) void tick_seal2_kernel(const TickRing *ring, ui
     if ((uint32_t)lane < n) rt = tick_record_tag(reinterpret_cast<const uint64_t *>(&slot->rec[lane]), c + (uint64_t)lane);
     rt = wave_xor64(rt);
     if (lane == 0) {
+        if (ctr) tick = *ctr + 1;  // graph-captured ticks number themselves
         const uint32_t busy = pending > n ? 1u : 0u;
         slot->count = n;
         slot->busy = busy;
@@ -59,6 +60,7 @@ __global__ __launch_bounds__(64) void tick_seal2_kernel(const TickRing *ring, ui
         slot->tick = tick;
         slot->tag = tick_slot_tag(n, busy, c, tick, rt);
         *consumed = c + n;
+        if (ctr) *ctr = tick;
     }
 }
 
@@ -71,8 +73,12 @@ __global__ __launch_bounds__(64) void tick_seal2_kernel(const TickRing *ring, ui
 // With `wait` (s_memrealtime ticks, 100 MHz) the read repeats while the ring
 // holds nothing unsent, up to that long: a record the host posts just after the
 // previous tick completed then rides this tick rather than the next one.
+//
+// `ctr` (graph-captured ticks, whose arguments are fixed at capture): the tick
+// number is the device counter + 1, stored back by the seal (seals run in
+// stream order, one at a time).
 __global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uint64_t *consumed, TickSlot *slot,
-                                                      uint64_t tick, uint64_t wait) {
+                                                      uint64_t tick, uint64_t wait, uint64_t *ctr) {
     const int lane = threadIdx.x;
     // Seals run one at a time (one stream, or two alternating streams ordered by an
     // event), but possibly on different queues: agent-scope (sc1) load and store.
@@ -112,6 +118,7 @@ __global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uin
     }
     rt = wave_xor64(rt);
     if (lane == 0) {
+        if (ctr) tick = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
         const uint32_t busy = pending > n ? 1u : 0u;
         slot->count = n;
         slot->busy = busy;
@@ -119,6 +126,7 @@ __global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uin
         slot->tick = tick;
         slot->tag = tick_slot_tag(n, busy, c, tick, rt);
         __hip_atomic_store(consumed, c + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ctr) __hip_atomic_store(ctr, tick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -137,7 +145,7 @@ hipError_t tick_done_launch(uint64_t *flag, uint64_t seq, hipStream_t stream) {
 }
 
 hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, uint64_t tick, uint32_t wait_us,
-                            hipStream_t stream) {
+                            hipStream_t stream, uint64_t *tick_ctr) {
     (void)hipGetLastError();  // report this launch, not an earlier call's error
     static const bool spec = [] {
         const char *v = std::getenv("OCM_TICK_SEAL_SPEC");
@@ -145,9 +153,9 @@ hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *
     }();
     const uint64_t wait = (uint64_t)std::min<uint32_t>(wait_us, 1000) * 100;  // s_memrealtime: 100 MHz
     if (spec)
-        hipLaunchKernelGGL(tick_seal_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot, tick, wait);
+        hipLaunchKernelGGL(tick_seal_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot, tick, wait, tick_ctr);
     else
-        hipLaunchKernelGGL(tick_seal2_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot, tick);
+        hipLaunchKernelGGL(tick_seal2_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot, tick, tick_ctr);
     return hipGetLastError();
 }
 

@@ -16,6 +16,15 @@ def _cpu_app(monkeypatch):
     monkeypatch.setenv("OCM_NO_GPU", "1")
 
 
+def _seal_env(sealed):
+    """"0": host-filled slots, "1": the socket stand-in for the RCCL seal kernel,
+    "batch4": that, with ticks queued 4 at a time as the RCCL collective queues
+    replays of a captured graph (OCM_TICK_GRAPH)."""
+    if sealed == "batch4":
+        return {"OCM_TICK_SOCKET_SEAL": "1", "OCM_TICK_SOCKET_BATCH": "4"}
+    return {"OCM_TICK_SOCKET_SEAL": sealed}
+
+
 def _wait_tick_up(c, n):
     import time
 
@@ -30,11 +39,11 @@ def _wait_tick_up(c, n):
     raise AssertionError("tick transport never came up")
 
 
-@pytest.mark.parametrize("sealed", ["0", "1"])
+@pytest.mark.parametrize("sealed", ["0", "1", "batch4"])
 def test_socket_tick_mesh_suite(mesh_factory, native, tool, sealed):
     # sealed=1: the socket collective emulates the RCCL seal kernel (outbox ring
     # sealed when the tick runs), so the device-sealed protocol runs multi-rank here
-    m = mesh_factory(4, extra_args=["--ctrl", "socket"], env={"OCM_TICK_SOCKET_SEAL": sealed})
+    m = mesh_factory(4, extra_args=["--ctrl", "socket"], env=_seal_env(sealed))
     with api.Client(daemon_rank=0, ns=m.ns) as c:
         _wait_tick_up(c, 4)
         t0 = [c.stats(r)["ctrl_ticks"] for r in range(4)]
@@ -54,9 +63,9 @@ def test_socket_tick_mesh_suite(mesh_factory, native, tool, sealed):
             assert rc == 0, out + m.logs()
 
 
-@pytest.mark.parametrize("sealed", ["0", "1"])
+@pytest.mark.parametrize("sealed", ["0", "1", "batch4"])
 def test_socket_tick_concurrent_churn(mesh_factory, sealed):
-    m = mesh_factory(4, extra_args=["--ctrl", "socket"], env={"OCM_TICK_SOCKET_SEAL": sealed})
+    m = mesh_factory(4, extra_args=["--ctrl", "socket"], env=_seal_env(sealed))
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     code = textwrap.dedent(f"""
         import sys; sys.path.insert(0, {repo!r})
@@ -76,9 +85,9 @@ def test_socket_tick_concurrent_churn(mesh_factory, sealed):
         assert all(c.stats(r)["ctrl_ticks"] > 0 for r in range(4))
 
 
-@pytest.mark.parametrize("sealed", ["0", "1"])
+@pytest.mark.parametrize("sealed", ["0", "1", "batch4"])
 def test_tick_peer_death_falls_back_to_tcp(mesh_factory, sealed):
-    m = mesh_factory(3, extra_args=["--ctrl", "socket"], env={"OCM_TICK_SOCKET_SEAL": sealed})
+    m = mesh_factory(3, extra_args=["--ctrl", "socket"], env=_seal_env(sealed))
     with api.Client(daemon_rank=0, ns=m.ns) as c:
         _wait_tick_up(c, 3)
         m.kill(2)
@@ -148,6 +157,9 @@ RCCL_TICK_MODES = {
     "depth3_tagged_wait": {"OCM_TICK_DEPTH": "3", "OCM_TICK_DONE_KERNEL": "0", "OCM_TICK_SEAL_WAIT_US": "4"},
     "two_streams": {"OCM_TICK_STREAMS": "2"},
     "two_streams_depth3_done_kernel": {"OCM_TICK_STREAMS": "2", "OCM_TICK_DEPTH": "3", "OCM_TICK_DONE_KERNEL": "1"},
+    "graph8": {"OCM_TICK_GRAPH": "8"},  # ticks queued as replays of a captured graph of 8
+    "graph2_nowait": {"OCM_TICK_GRAPH": "2", "OCM_TICK_SEAL_WAIT_US": "0"},
+    "no_graph": {"OCM_TICK_GRAPH": "0"},
 }
 
 
@@ -175,7 +187,10 @@ def test_rccl_tick_single_gpu(mesh_factory, monkeypatch, mode):
             a.free()
         assert c.stats(0)["ctrl_ticks"] > before
         assert c.stats(0)["ctrl"] == "rccl"  # never fell back
-    assert "rccl tick transport" in m.logs()
+    logs = m.logs()
+    assert "rccl tick transport" in logs
+    if RCCL_TICK_MODES[mode].get("OCM_TICK_GRAPH", "0") != "0":
+        assert "ticks per captured graph" in logs and "rccl tick graphs unavailable" not in logs, logs
 
 
 def _ctrl(c, n):
@@ -194,13 +209,13 @@ def test_ctrl_auto_without_gpus_stays_on_tcp(mesh_factory):
     assert "daemon<->daemon records: tcp (--ctrl auto)" in m.logs()
 
 
-@pytest.mark.parametrize("sealed", ["0", "1"])
+@pytest.mark.parametrize("sealed", ["0", "1", "batch4"])
 def test_ctrl_auto_eight_ranks_join_over_the_ticks(mesh_factory, sealed):
     """--ctrl auto with the CPU stand-in for RCCL (OCM_CTRL_AUTO_SOCKET): rank0
     starts the transport as each link comes up, every peer's join (ADD_NODE,
     NODE_LINKS) is the transport's first traffic, and the 8-rank mesh then
     carries striped allocations on it."""
-    m = mesh_factory(8, env={"OCM_CTRL_AUTO_SOCKET": "1", "OCM_TICK_SOCKET_SEAL": sealed})
+    m = mesh_factory(8, env={"OCM_CTRL_AUTO_SOCKET": "1", **_seal_env(sealed)})
     with api.Client(daemon_rank=3, ns=m.ns) as c:
         assert _ctrl(c, 8) == ["socket"] * 8
         t0 = [c.stats(r)["ctrl_ticks"] for r in range(8)]
@@ -243,14 +258,14 @@ def test_ctrl_auto_falls_back_to_tcp_when_the_transport_never_comes_up(mesh_fact
     assert "not up within OCM_TICK_UP_MS=400 ms" in logs, logs
 
 
-@pytest.mark.parametrize("sealed", ["0", "1"])
+@pytest.mark.parametrize("sealed", ["0", "1", "batch4"])
 def test_a_wedged_collective_times_out_and_the_mesh_falls_back(mesh_factory, sealed):
     """A rank stops taking part in the ticks without any error (a wedged
     collective: OCM_TICK_FAULT=stall_after=N on rank 2). The other ranks' tick
     watchdog (OCM_TICK_TIMEOUT_MS) ends the transport, everybody leaves it, what
     the ticks had not delivered goes over TCP, and allocations keep working."""
     m = mesh_factory(3, extra_args=["--ctrl", "socket"],
-                     env={"OCM_TICK_SOCKET_SEAL": sealed, "OCM_TICK_TIMEOUT_MS": "400", "OCM_LEASE_BYTES": "0"},
+                     env={**_seal_env(sealed), "OCM_TICK_TIMEOUT_MS": "400", "OCM_LEASE_BYTES": "0"},
                      rank_env={2: {"OCM_TICK_FAULT": "stall_after=30"}})
     with api.Client(daemon_rank=1, ns=m.ns) as c:
         for i in range(30):  # stalls part-way through: later ones need the TCP fallback
@@ -265,3 +280,27 @@ def test_a_wedged_collective_times_out_and_the_mesh_falls_back(mesh_factory, sea
     logs = m.logs()
     assert "OCM_TICK_TIMEOUT_MS" in logs, logs
     assert logs.count("leaving the socket tick transport") == 3, logs
+
+
+def test_a_rank_without_tick_batches_stays_in_step(mesh_factory):
+    """Ticks queued 4 at a time (the socket stand-in for replays of a captured
+    graph, OCM_TICK_GRAPH) on every rank but one, which queues them one at a time
+    as an RCCL rank whose capture failed does (OCM_TICK_FAULT=no_batch). All
+    ranks round their tick targets to the same quantum, so they keep joining the
+    same collectives: striped allocations work and nobody leaves the transport."""
+    m = mesh_factory(3, extra_args=["--ctrl", "socket"],
+                     env={**_seal_env("batch4"), "OCM_TICK_TIMEOUT_MS": "2000", "OCM_LEASE_BYTES": "0"},
+                     rank_env={1: {"OCM_TICK_FAULT": "no_batch"}})
+    with api.Client(daemon_rank=2, ns=m.ns) as c:
+        _wait_tick_up(c, 3)
+        for i in range(20):
+            a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20, flags=api.OCM_ALLOC_STRIPE)
+            a.fill(seed=20 + i)
+            a.put(0, 0, 1 << 20)
+            a.fill(seed=0)
+            a.get(0, 0, 1 << 20)
+            assert a.check(seed=20 + i) == 0
+            a.free()
+        assert _ctrl(c, 3) == ["socket"] * 3
+    logs = m.logs()
+    assert "falling back to TCP" not in logs and "leaving the" not in logs, logs

@@ -104,6 +104,13 @@ VARIANTS = {
                                              "OCM_TICK_DEPTH": "1"}),
     "rccl_tagged_wait6_d3": ("rccl", True, {"OCM_TICK_DONE_KERNEL": "0", "OCM_TICK_SEAL_WAIT_US": "6",
                                              "OCM_TICK_DEPTH": "3"}),
+    # round 3: ticks queued as replays of a captured graph of K ticks (OCM_TICK_GRAPH)
+    "rccl_graph4": ("rccl", True, {"OCM_TICK_GRAPH": "4", "OCM_TICK_STATS": "1"}),
+    "rccl_graph8": ("rccl", True, {"OCM_TICK_GRAPH": "8", "OCM_TICK_STATS": "1"}),
+    "rccl_graph16": ("rccl", True, {"OCM_TICK_GRAPH": "16", "OCM_TICK_STATS": "1"}),
+    "rccl_graph8_nowait": ("rccl", True, {"OCM_TICK_GRAPH": "8", "OCM_TICK_SEAL_WAIT_US": "0", "OCM_TICK_STATS": "1"}),
+    "rccl_graph8_w3": ("rccl", True, {"OCM_TICK_GRAPH": "8", "OCM_TICK_SEAL_WAIT_US": "3", "OCM_TICK_STATS": "1"}),
+    "rccl_nograph": ("rccl", True, {"OCM_TICK_GRAPH": "0", "OCM_TICK_STATS": "1"}),
     "rccl_spec_ccd_spin300": ("rccl", True, {"OCM_RPC_SPIN_US": "300", "OCM_DAEMON_SPIN_US": "300"}),
 }
 
