@@ -4,6 +4,7 @@
 #include <pthread.h>
 #include <signal.h>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "ocm/daemon.h"
@@ -20,6 +21,11 @@ int main(int argc, char **argv) {
     sigaddset(&mask, SIGINT);
     sigaddset(&mask, SIGTERM);
     pthread_sigmask(SIG_BLOCK, &mask, nullptr);
+    // RCCL reads its environment when the tick thread creates the communicator;
+    // set here, before any thread exists (setenv is not thread-safe). Captured
+    // ticks (OCM_TICK_GRAPH) use plain buffers: no user-buffer registration with
+    // the peers while capturing.
+    setenv("NCCL_GRAPH_REGISTER", "0", 0);
     ocm::DaemonConfig cfg;
     std::string err;
     const int rc = ocm::parse_daemon_args(argc, argv, &cfg, &err);

@@ -615,9 +615,6 @@ int rccl_unique_id(uint8_t out[128], std::string *err) {
 
 std::unique_ptr<Collective> make_rccl_collective(int gpu, int rank, int nranks, const uint8_t *id, size_t slot_bytes,
                                                  std::string *err, const std::atomic<bool> *cancel) {
-    // Captured ticks (OCM_TICK_GRAPH) use plain buffers: no registration of
-    // user buffers with the peers while capturing.
-    setenv("NCCL_GRAPH_REGISTER", "0", 0);
     auto c = std::make_unique<RcclCollective>();
     std::atomic<bool> done{false};
     std::thread watch;
