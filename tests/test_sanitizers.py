@@ -45,13 +45,15 @@ def tsan_bin():
     return os.path.join(build(sanitize="thread"), "bin")
 
 
-@pytest.mark.parametrize("sealed", ["0", "1"])
+@pytest.mark.parametrize("sealed", ["0", "1", "batch4"])
 def test_threads_under_tsan(tsan_bin, sealed):
     # Threads in the daemon: the tick transport thread (socket collective; sealed=1
     # adds the outbox ring the RCCL seal kernel reads, emulated on the CPU) and
     # the network-tier data server (rank 2 is alone on "node B", so its app's
     # remote halves live on node A and are streamed through rank 0/1 servers).
-    env = {"OCM_NO_GPU": "1", "TSAN_OPTIONS": "halt_on_error=0", "OCM_TICK_SOCKET_SEAL": sealed}
+    # batch4: ticks queued 4 at a time, the stand-in for replays of captured tick graphs
+    seal = {"OCM_TICK_SOCKET_SEAL": "1", "OCM_TICK_SOCKET_BATCH": "4"} if sealed == "batch4" else {"OCM_TICK_SOCKET_SEAL": sealed}
+    env = {"OCM_NO_GPU": "1", "TSAN_OPTIONS": "halt_on_error=0", **seal}
     hosts = {0: {"OCM_HOST_ALIAS": "A"}, 1: {"OCM_HOST_ALIAS": "A"}, 2: {"OCM_HOST_ALIAS": "B"}}
     m = Mesh(3, bin_dir=tsan_bin, env=env, extra_args=["--ctrl", "socket"], rank_env=hosts).start(timeout=120)
     try:
