@@ -359,6 +359,14 @@ def main() -> int:
         # N-rank mesh, placement and IPC paths run without N devices.
         local_rank = 0
     max_bytes = args.max_bytes or ((1 << 30) if use_gpu else (16 << 20))
+    if use_gpu:
+        # This benchmark opts in to the library's app pinning (OCM_PIN=1: the thread
+        # that calls ocm_init, and what it starts later, on the GPU's L3 complex,
+        # off the daemon's core). Measured on one box: 4 KiB get/put 5.04 / 4.17 us
+        # pinned, 5.11-5.15 / 4.19-4.26 unpinned, 6.07-6.45 / 5.21-5.89 with the
+        # process confined to the GPU's NUMA node (profiles/numa_small_r03.json).
+        # The library itself leaves applications unpinned unless they ask.
+        os.environ.setdefault("OCM_PIN", "1")
 
     from oncilla_amd import api
     from oncilla_amd.models import workloads as wl
@@ -605,6 +613,7 @@ def main() -> int:
                 "extents_per_pair": len(stats[0]["extents"]),
                 "sizes": f"{args.min_bytes}..{max_bytes} x2",
                 "device": "gpu" if use_gpu else "cpu",
+                "app_pin": os.environ.get("OCM_PIN", "") if use_gpu else "",
             },
             "alloc_p50_us": round(max(s["lat"]["alloc_p50_us"] for s in stats), 2),
             "alloc_p99_us": round(max(s["lat"]["alloc_p99_us"] for s in stats), 2),
