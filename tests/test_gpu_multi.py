@@ -146,12 +146,15 @@ def test_fused_adam_with_state_in_peer_hbm(mesh_factory):
             opt.close()
 
 
-def test_rccl_control_plane_between_gpus(mesh_factory):
+@pytest.mark.parametrize("graph", ["0", "8"])
+def test_rccl_control_plane_between_gpus(mesh_factory, graph):
     """--ctrl rccl: the daemons' control records ride ncclAllGather ticks over
     xGMI (one rank per GPU). Leases off, so every allocation takes the full
-    REQ_ALLOC -> DO_ALLOC -> reply path through the ticks."""
+    REQ_ALLOC -> DO_ALLOC -> reply path through the ticks. graph=8: the ticks
+    are queued as replays of captured graphs of 8 (OCM_TICK_GRAPH)."""
     k = min(NDEV, 4)
-    m = mesh_factory(k, gpus=list(range(k)), extra_args=["--ctrl", "rccl"], env={"OCM_LEASE_BYTES": "0"})
+    m = mesh_factory(k, gpus=list(range(k)), extra_args=["--ctrl", "rccl"],
+                     env={"OCM_LEASE_BYTES": "0", "OCM_TICK_GRAPH": graph})
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         for i in range(20):
             a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=1 << 20, remote_bytes=1 << 20, remote_rank=1 + i % (k - 1))
@@ -159,6 +162,8 @@ def test_rccl_control_plane_between_gpus(mesh_factory):
             a.free()
         assert c.stats(0)["ctrl_ticks"] > 0, m.logs()
         assert "falling back to TCP" not in m.logs()
+    if graph != "0":
+        assert m.logs().count("ticks per captured graph") == k, m.logs()
 
 
 def test_host_tier_of_another_gpus_daemon(mesh_factory):
