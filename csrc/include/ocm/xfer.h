@@ -227,8 +227,14 @@ void service_store_seq(ServiceReq *req, unsigned long long seq);
 //             kServiceWgDoneMax); the counter's atomic round trip is then off the
 //             last workgroup's path to `done`
 //   TRACE     diagnostics: stamp each workgroup's phases into ServiceBox::trace
+//   STRICTWT  STRICT requests (an extent in another GPU's HBM) keep the system
+//             acquire before the copy (this GPU's L2 may hold stale lines of
+//             peer memory from an earlier request: sc1 loads are L2-served) but
+//             copy write-through (sc1 stores drop their lines from L2 and write
+//             through) and drain, instead of a plain copy and a system release
+//             (an L2 writeback) before `done`
 constexpr unsigned kServiceProtoWT = 1u, kServiceProtoGangRec = 2u, kServiceProtoWCReq = 4u, kServiceProtoWgDone = 8u,
-                   kServiceProtoTrace = 16u;
+                   kServiceProtoTrace = 16u, kServiceProtoStrictWT = 32u;
 // Whether a gang of `active` workgroups completes through ServiceSlot::wg_done.
 constexpr bool service_wg_done(unsigned proto, unsigned long long active) {
     return (proto & kServiceProtoWgDone) && active > 1 && active <= (unsigned long long)kServiceWgDoneMax;

@@ -735,9 +735,14 @@ __device__ __forceinline__ void service_serve(const unsigned long long *sh, unsi
     // under the WT protocol: sc1 accesses keep this GPU's caches coherent with host
     // memory and its own HBM, but a resident instance may hold L2 lines of peer
     // memory from an earlier request, and nothing else invalidates them.
-    const bool wt = (proto & kServiceProtoWT) && !(gang & kServiceGangStrict);
+    const bool strict = (gang & kServiceGangStrict) != 0;
+    const bool wt = (proto & kServiceProtoWT) && (!strict || (proto & kServiceProtoStrictWT));
     service_stamp(box, proto, 1);
     if (wt) {
+        if (strict) {  // STRICTWT: drop stale L2 lines of peer memory before the sc1 (L2-served) loads
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         service_copy<ST_WT>(sh, blockIdx.x, active);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its sc1 stores
         __syncthreads();

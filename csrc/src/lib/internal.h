@@ -219,6 +219,7 @@ struct State {
     unsigned svc_solo_tiles = kServiceSoloTilesDefault;  // requests of <= this many tiles stay on workgroup 0
     unsigned svc_solo_tiles_host_get = 1;  // ... for gets from the host tier (OCM_SERVICE_SOLO_TILES_HOST_GET)
     unsigned svc_proto = kServiceProtoDefault;           // hand-off protocol bits (OCM_SERVICE_PROTO)
+    bool svc_force_strict = false;                       // OCM_SERVICE_STRICT: every request STRICT
     unsigned svc_direct = kServiceDirectDefault;          // GANGREC direct pollers (OCM_SERVICE_DIRECT)
     uint64_t svc_direct_max_host = kServiceDirectMaxHost;  // OCM_SERVICE_DIRECT_MAX_HOST
     uint64_t svc_direct_max_hbm = kServiceDirectMaxHbm;    // OCM_SERVICE_DIRECT_MAX_HBM

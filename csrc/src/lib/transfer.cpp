@@ -405,7 +405,7 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         // HBM owners keep small requests on workgroup 0 (profiles/svc_v4_r02.json).
         const unsigned solo = (!put && !a->any_gpu) ? std::min(s.svc_solo_tiles, s.svc_solo_tiles_host_get)
                                                     : s.svc_solo_tiles;
-        if (service_xfer(x, solo, a->any_gpu, a->any_peer) == 0) return 0;
+        if (service_xfer(x, solo, a->any_gpu, a->any_peer || s.svc_force_strict) == 0) return 0;
         OCM_WARN("copy service failed (%s); falling back to launches", last_error());
         s.svc_max = 0;
     }

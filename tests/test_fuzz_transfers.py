@@ -71,10 +71,14 @@ def test_fuzz_apps_share_a_mesh_gpu(native, mesh_factory):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("proto", ["7", "1", "9"])
+@pytest.mark.parametrize("proto", ["7", "1", "9", "15+strict", "47+strict"])
 def test_fuzz_service_protocols_gpu(native, proto):
     """The copy service's other hand-off protocols stay correct now that the default
     (15) completes gangs through per-workgroup done words: 7 = the device-scope
     counter, 1 = write-through without the gang record (relayed gangs), 9 = that
-    with per-workgroup done words."""
-    _run(8, dict(os.environ, OCM_SERVICE_PROTO=proto), 16 << 20, ("--configs", "hbm,host"))
+    with per-workgroup done words. "+strict": every request takes the peer-HBM
+    (STRICT) hand-off (OCM_SERVICE_STRICT=1), fenced (15) or write-through behind
+    its acquire (47 = 15 | STRICTWT)."""
+    p, _, strict = proto.partition("+")
+    env = dict(os.environ, OCM_SERVICE_PROTO=p, **({"OCM_SERVICE_STRICT": "1"} if strict else {}))
+    _run(8, env, 16 << 20, ("--configs", "hbm,host"))

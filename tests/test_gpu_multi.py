@@ -67,10 +67,14 @@ def test_stripe_over_every_peer_gpu(mesh_factory):
         a.free()
 
 
+@pytest.mark.parametrize("proto", ["15", "47"])
 @pytest.mark.parametrize("size", [4096, 65536, 1 << 20, 4 << 20])
-def test_copy_service_small_ops_on_peer_hbm(mesh_factory, size):
+def test_copy_service_small_ops_on_peer_hbm(mesh_factory, monkeypatch, size, proto):
     """Blocking small ops ride the resident copy service; on peer HBM its
-    stores cross xGMI. Many back-to-back ops, each verified."""
+    stores cross xGMI. Many back-to-back ops, each verified. proto 47 adds
+    STRICTWT: the peer-HBM hand-off copies write-through behind its acquire
+    instead of releasing with an L2 writeback (profiles/svc_strict_cost_r03.json)."""
+    monkeypatch.setenv("OCM_SERVICE_PROTO", proto)
     m = mesh_factory(2, gpus=[0, 1])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=8 << 20, remote_bytes=8 << 20, remote_rank=1)
