@@ -1,10 +1,15 @@
 // Native unit tests (no daemon, no GPU): wire layout, nodefile, range
-// allocator, governor placement policies, stripe geometry, host-tier arena.
+// allocator, governor placement policies, stripe geometry, host-tier arena,
+// tick slot tags and the tick transport's state machine over a 1-rank socket
+// collective (plain and batched).
 // Prints one line per test and exits non-zero on the first failure.
 #include <sys/mman.h>
 #include <unistd.h>
 
 #include <cerrno>
+#include <chrono>
+#include <cstdlib>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -21,6 +26,7 @@
 #include "ocm/range_alloc.h"
 #include "ocm/shmlink.h"
 #include "ocm/siphash.h"
+#include "ocm/tick.h"
 
 using namespace ocm;
 
@@ -443,6 +449,95 @@ static void t_shmlink() {
     munmap(static_cast<void *>(raw), bytes);
 }
 
+// Sealed tick slots: whole only for their own tick, with every record and
+// header field as sealed (tick_slot_whole is what completion detection and the
+// socket stand-in trust).
+static void t_tick_tags() {
+    TickSlot s;
+    std::memset(&s, 0, sizeof(s));
+    s.count = 3;
+    s.busy = 1;
+    s.first = 40;
+    for (int r = 0; r < 3; r++) {
+        s.rec[r].dest = r;
+        s.rec[r].msg.type = MSG_DO_ALLOC;
+        s.rec[r].msg.seq = 100 + (uint64_t)r;
+    }
+    tick_slot_seal_tag(&s, 7);
+    CHECK(tick_slot_whole(s, 7));
+    CHECK(!tick_slot_whole(s, 8));  // a slot left from another tick
+    TickSlot t = s;
+    t.rec[1].msg.seq ^= 1;  // a record torn or changed after sealing
+    CHECK(!tick_slot_whole(t, 7));
+    t = s;
+    t.first = 41;  // the sender's progress changed
+    CHECK(!tick_slot_whole(t, 7));
+    t = s;
+    t.count = kTickMsgs + 1;
+    CHECK(!tick_slot_whole(t, 7));
+    TickSlot e;  // an empty sealed slot is whole too
+    std::memset(&e, 0, sizeof(e));
+    tick_slot_seal_tag(&e, 1);
+    CHECK(tick_slot_whole(e, 1));
+    // record tags depend on the ring index
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(&s.rec[0]);
+    CHECK(tick_record_tag(w, 5) != tick_record_tag(w, 6));
+}
+
+// The transport over a 1-rank socket collective with the sealed outbox (the CPU
+// stand-in for the RCCL seal kernel): records to ourselves come back in order,
+// and with OCM_TICK_SOCKET_BATCH the transport queues ticks K at a time and
+// stops on a multiple of K.
+static void tick_roundtrip(int batch) {
+    setenv("OCM_TICK_SOCKET_SEAL", "1", 1);
+    if (batch > 1)
+        setenv("OCM_TICK_SOCKET_BATCH", std::to_string(batch).c_str(), 1);
+    else
+        unsetenv("OCM_TICK_SOCKET_BATCH");
+    const std::string ns = "ut" + std::to_string(getpid()) + "_" + std::to_string(batch);
+    TickTransport tt(0, 1, [ns](std::string *err, const std::atomic<bool> *cancel) {
+        return make_socket_collective(ns, 0, 1, sizeof(TickSlot), err, cancel);
+    });
+    tt.start();
+    const auto t0 = std::chrono::steady_clock::now();
+    auto elapsed_ms = [&] {
+        return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+    };
+    while (!tt.up() && !tt.failed() && elapsed_ms() < 5000) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    CHECK(tt.up());
+    constexpr int kN = 300;  // more than the outbox ring holds at once (kTickRing records)
+    for (int i = 0; i < kN; i++) {
+        Msg m;
+        std::memset(&m, 0, sizeof(m));
+        m.type = MSG_STATS;
+        m.seq = (uint64_t)i;
+        CHECK(tt.post(0, m));
+    }
+    std::vector<uint64_t> got;
+    while ((int)got.size() < kN && !tt.failed() && elapsed_ms() < 10000) {
+        for (const Msg &m : tt.drain()) got.push_back(m.seq);
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    CHECK((int)got.size() == kN);
+    for (int i = 0; i < kN; i++) CHECK(got[(size_t)i] == (uint64_t)i);
+    // idle again after the burst: every queued tick has completed
+    uint64_t last = tt.ticks();
+    for (int k = 0; k < 200; k++) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        const uint64_t now = tt.ticks();
+        if (now == last) break;
+        last = now;
+    }
+    CHECK(last > 0 && last % (uint64_t)batch == 0);
+    tt.stop();
+    CHECK(!tt.failed());
+    unsetenv("OCM_TICK_SOCKET_SEAL");
+    unsetenv("OCM_TICK_SOCKET_BATCH");
+}
+
+static void t_tick_transport() { tick_roundtrip(1); }
+static void t_tick_transport_batched() { tick_roundtrip(4); }
+
 int main(int argc, char **argv) {
     if (argc > 1 && std::strcmp(argv[1], "--nodefile") == 0) {
         // ocm_unit_tests --nodefile F...: parse each with the daemon's parser
@@ -468,7 +563,9 @@ int main(int argc, char **argv) {
                  {"governor_checkpoint", t_governor_checkpoint},
                  {"stripe_geometry", t_stripe_geometry},
                  {"arena_host", t_arena_host},   {"siphash", t_siphash},
-                 {"shmlink", t_shmlink}};
+                 {"shmlink", t_shmlink},         {"tick_tags", t_tick_tags},
+                 {"tick_transport", t_tick_transport},
+                 {"tick_transport_batched", t_tick_transport_batched}};
     for (auto &t : tests) {
         int before = g_fail;
         t.fn();
