@@ -45,6 +45,14 @@ def tsan_bin():
     return os.path.join(build(sanitize="thread"), "bin")
 
 
+def test_unit_tests_under_tsan(tsan_bin):
+    # the native unit tests run the tick transport's thread against a 1-rank
+    # socket collective, plain and batched
+    r = subprocess.run([f"{tsan_bin}/ocm_unit_tests"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, OCM_NO_GPU="1", TSAN_OPTIONS="halt_on_error=0"))
+    assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("sealed", ["0", "1", "batch4"])
 def test_threads_under_tsan(tsan_bin, sealed):
     # Threads in the daemon: the tick transport thread (socket collective; sealed=1
