@@ -515,7 +515,7 @@ def main() -> int:
         def sync():
             if use_gpu:
                 # the copy service is a persistent kernel: park it, or a device-wide
-                # synchronize waits for its 2 ms idle exit (inside the timed region)
+                # synchronize waits for its idle exit (OCM_SERVICE_IDLE_US, 50 us)
                 api.quiesce()
                 torch.cuda.synchronize(local_rank)
 

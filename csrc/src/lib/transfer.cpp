@@ -153,7 +153,8 @@ int service_start(unsigned long long first_seq) {
         // A stream of its own priority: HIP shares its few hardware queues
         // (GPU_MAX_HW_QUEUES) among a process's streams, and a launch on a stream
         // that shares the service's queue waits behind the persistent kernel until
-        // its idle exit (2 ms per large op in bench.py with torch's streams around).
+        // its idle exit (2 ms per large op in bench.py with torch's streams around, when
+        // the idle exit was 2 ms).
         // Queues are pooled per priority, so the service's is not shared with the
         // normal-priority streams of the library and the application.
         int lo = 0, hi = 0;

@@ -107,10 +107,12 @@ def test_service_direct_and_relayed_gangs_interleave(mesh_factory):
         host.free()
 
 
-def test_quiesce_lets_a_device_sync_return_at_once(mesh_factory):
+def test_quiesce_lets_a_device_sync_return_at_once(mesh_factory, monkeypatch):
     # The service is a persistent kernel: torch.cuda.synchronize() waits for it.
     # api.quiesce() parks it, so the sync returns without waiting for the idle
-    # exit; the next op relaunches the service and still moves the right bytes.
+    # exit (set to 2 ms here, the round-2 default, so skipping it shows); the
+    # next op relaunches the service and still moves the right bytes.
+    monkeypatch.setenv("OCM_SERVICE_IDLE_US", "2000")
     m = mesh_factory(1, gpus=[0])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         n = 64 << 10
