@@ -317,6 +317,8 @@ def ctrl_extra(dist, world: int, rank: int, local_rank: int, use_gpu: bool, samp
                     lat = wl.alloc_latency(c, kind, samples, local_bytes=4096, remote_bytes=1 << 20)
                     lat["ticks"] = c.stats(rank)["ctrl_ticks"]
                     lat["up"] = up
+                    # this rank's records from post to delivery in a gathered tick (one hop)
+                    lat["tick"] = api.tick_stats() if ctrl != "tcp" else None
                     return lat
 
             r, err = _local(run)
@@ -331,6 +333,11 @@ def ctrl_extra(dist, world: int, rank: int, local_rank: int, use_gpu: bool, samp
                      "free_p50_us": round(max(x["r"]["free_p50_us"] for x in res), 2),
                      "ticks_rank0": res[0]["r"]["ticks"], "samples_per_rank": samples,
                      "transport_up_all_ranks": all(x["r"]["up"] for x in res)}
+        ticks = [x["r"].get("tick") for x in res]
+        if any(ticks):
+            out[ctrl]["hop_mean_us_per_rank"] = [t["hop_mean_us"] if t else None for t in ticks]
+            out[ctrl]["tick_period_mean_us_rank0"] = ticks[0]["tick_period_mean_us"] if ticks[0] else None
+            out[ctrl]["start_mean_us_rank0"] = ticks[0]["start_mean_us"] if ticks[0] else None
     return out
 
 

@@ -196,6 +196,7 @@ private:
     void app_req_alloc(Msg &m);
     void app_req_free(Msg &m);
     void app_stats(Msg &m);
+    void app_tick_stats(Msg &m);
     void r0_add_node(const NodeConfig &cfg, uint64_t boot_id);
     void join_rank0();                   // ADD_NODE + OWNED report (boot and rejoin)
     void try_rejoin_rank0();             // survivors: reconnect to a restarted rank0

@@ -46,6 +46,7 @@ enum MsgType : uint32_t {
     MSG_SLAB_FD,          // app -> owner daemon: a host-tier slab's memfd (u.region.slab_id), reply carries it (SCM_RIGHTS)
     MSG_TICK_STOP,        // any -> all (TCP): the sender left the tick transport; leave it too (records ride TCP)
     MSG_WAKE,             // app <-> daemon (mailbox socket): look at the shared-memory link (ocm/shmlink.h)
+    MSG_TICK_STATS,       // app -> its daemon: the tick transport's statistics (u.raw = TickStatsWire)
     MSG_MAX
 };
 
@@ -116,6 +117,19 @@ struct NodeConfig {
     uint32_t lease_allocs; // allocations served from them (no mesh round trip)
 };
 
+// Statistics of a daemon's tick control transport (MSG_TICK_STATS reply, in u.raw):
+// this rank's own records from post to delivery in a gathered tick, the gaps
+// between completed ticks, and the host time the tick thread spends queueing them.
+struct TickStatsWire {
+    uint64_t ticks;           // ticks completed
+    uint64_t own_records;     // own records seen delivered (device-sealed outboxes)
+    uint64_t lat_sum_ns, lat_max_ns;
+    uint64_t periods, period_sum_ns;
+    uint64_t starts, start_sum_ns, start_max_ns;  // Collective::start calls and their host time
+    uint32_t transport;       // ocm_daemon_stats.ctrl_transport
+    uint32_t ticks_per_start; // > 1: ticks queued as captured graphs (OCM_TICK_GRAPH)
+};
+
 // Topology of one daemon's GPU (hipExtGetLinkTypeAndHopCount to every other
 // GPU ordinal on its node), fed to rank0's placement (nearest peer first).
 constexpr int kMaxLinkGpus = 32;
@@ -130,6 +144,7 @@ struct NodeLinks {
 };
 
 static_assert(sizeof(NodeLinks) <= 128, "NodeLinks fits the message union");
+static_assert(sizeof(TickStatsWire) <= 128, "TickStatsWire fits the message union");
 
 // MSG_HELLO body: the first record on a mesh link. mac = SipHash-2-4 under the
 // key derived from namespace + OCM_MESH_KEY over (src, dst, ts_ms, nonce); the

@@ -198,6 +198,9 @@ public:
     // Records still queued when the transport failed (re-send them over TCP).
     std::vector<TickRecord> take_unsent();
     uint64_t ticks() const { return ticks_.load(); }
+    // Latency and host-cost statistics so far (always collected; OCM_TICK_STATS=1
+    // also logs them when the transport stops).
+    void stats(TickStatsWire *out);
     const char *collective_name() const { return coll_ ? coll_->name() : "none"; }
 
 private:
@@ -215,12 +218,13 @@ private:
     TickRing *ring_ = nullptr;  // device-sealed collectives: their outbox (under mu_)
     uint64_t ring_sent_ = 0;    // ring records a completed tick of ours carried
     uint64_t ring_pub_ = 0;     // records appended (host shadow of ring_->published)
-    // OCM_TICK_STATS=1: post -> delivery latency of this rank's own records (device-sealed
-    // rings), and completed-tick periods, logged when the transport stops.
+    // Post -> delivery latency of this rank's own records (device-sealed rings),
+    // completed-tick periods and start() host time; OCM_TICK_STATS=1 logs them at stop.
     bool stats_ = false, stats_logged_ = false;
     uint64_t post_ns_[kTickRing] = {};
     uint64_t lat_sum_ns_ = 0, lat_n_ = 0, lat_max_ns_ = 0, period_sum_ns_ = 0, period_n_ = 0, last_done_ns_ = 0;
     uint64_t start_sum_ns_ = 0, start_n_ = 0, start_max_ns_ = 0;  // host time inside Collective::start
+    uint32_t per_start_ = 1;
     void flush_ring();
     uint64_t unsent() const;
     int efd_ = -1;

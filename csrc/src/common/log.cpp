@@ -77,6 +77,7 @@ const char *msg_type_str(uint32_t t) {
     case MSG_SLAB_FD: return "MSG_SLAB_FD";
     case MSG_TICK_STOP: return "MSG_TICK_STOP";
     case MSG_WAKE: return "MSG_WAKE";
+    case MSG_TICK_STATS: return "MSG_TICK_STATS";
     default: return "INVALID MSG TYPE";
     }
 }

@@ -43,6 +43,7 @@ void Daemon::handle_app_msg(Msg &m) {
     case MSG_REQ_ALLOC: app_req_alloc(m); break;
     case MSG_REQ_FREE: app_req_free(m); break;
     case MSG_STATS: app_stats(m); break;
+    case MSG_TICK_STATS: app_tick_stats(m); break;
     case MSG_PING: {
         Msg r = m;
         r.status = MSG_RESPONSE;
@@ -237,5 +238,22 @@ void Daemon::app_stats(Msg &m) {
     send_app(m.pid, r);
 }
 
+
+// The tick control transport's statistics (this daemon only; zeros without one).
+void Daemon::app_tick_stats(Msg &m) {
+    Msg r;
+    std::memset(&r, 0, sizeof(r));
+    r.type = MSG_RELEASE_APP;
+    r.status = MSG_RESPONSE;
+    r.pid = m.pid;
+    r.rank = rank_;
+    r.seq = m.seq;
+    TickStatsWire st;
+    std::memset(&st, 0, sizeof(st));
+    if (tick_) tick_->stats(&st);
+    st.transport = my_config().ctrl;
+    std::memcpy(r.u.raw, &st, sizeof(st));
+    send_app(m.pid, r);
+}
 
 }  // namespace ocm

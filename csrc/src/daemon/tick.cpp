@@ -664,23 +664,43 @@ TickTransport::~TickTransport() {
 
 void TickTransport::start() { th_ = std::thread([this] { run(); }); }
 
+void TickTransport::stats(TickStatsWire *out) {
+    std::lock_guard<std::mutex> lk(mu_);
+    std::memset(out, 0, sizeof(*out));
+    out->ticks = ticks_.load();
+    out->own_records = lat_n_;
+    out->lat_sum_ns = lat_sum_ns_;
+    out->lat_max_ns = lat_max_ns_;
+    out->periods = period_n_;
+    out->period_sum_ns = period_sum_ns_;
+    out->starts = start_n_;
+    out->start_sum_ns = start_sum_ns_;
+    out->start_max_ns = start_max_ns_;
+    out->ticks_per_start = per_start_;
+}
+
 void TickTransport::stop() {
-    if (stats_ && lat_n_ && !stats_logged_)
+    if (th_.joinable()) {
+        stop_ = true;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (coll_) coll_->abort();
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    // logged once the tick thread has ended (it updates these under mu_)
+    TickStatsWire st;
+    stats(&st);
+    if (stats_ && st.own_records && !stats_logged_)
         OCM_INFO("rank %d: tick stats: %llu own records, post -> delivered %.2f us mean (max %.1f); %llu tick "
                  "periods of %.2f us mean; start() %.2f us mean (max %.1f) over %llu ticks",
-                 rank_, (unsigned long long)lat_n_, lat_sum_ns_ / 1e3 / (double)lat_n_, lat_max_ns_ / 1e3,
-                 (unsigned long long)period_n_, period_n_ ? period_sum_ns_ / 1e3 / (double)period_n_ : 0.0,
-                 start_n_ ? start_sum_ns_ / 1e3 / (double)start_n_ : 0.0, start_max_ns_ / 1e3,
-                 (unsigned long long)start_n_);
+                 rank_, (unsigned long long)st.own_records, st.lat_sum_ns / 1e3 / (double)st.own_records,
+                 st.lat_max_ns / 1e3, (unsigned long long)st.periods,
+                 st.periods ? st.period_sum_ns / 1e3 / (double)st.periods : 0.0,
+                 st.starts ? st.start_sum_ns / 1e3 / (double)st.starts : 0.0, st.start_max_ns / 1e3,
+                 (unsigned long long)st.starts);
     stats_logged_ = true;
-    if (!th_.joinable()) return;
-    stop_ = true;
-    {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (coll_) coll_->abort();
-    }
-    cv_.notify_all();
-    th_.join();
 }
 
 void TickTransport::abort() {
@@ -714,7 +734,7 @@ void TickTransport::flush_ring() {
     while (!out_.empty() && pub - ring_sent_ < kTickRing) {
         TickRecord &r = ring_->rec[pub & (kTickRing - 1)];
         r = out_.front();
-        if (stats_) post_ns_[pub & (kTickRing - 1)] = mono_now_ns();
+        post_ns_[pub & (kTickRing - 1)] = mono_now_ns();
         ring_->tag[pub & (kTickRing - 1)] = tick_record_tag(reinterpret_cast<const uint64_t *>(&r), pub);
         out_.pop_front();
         pub++;
@@ -806,6 +826,10 @@ void TickTransport::run() {
     const uint64_t quantum = (uint64_t)std::max(1, coll->tick_quantum());
     {
         std::lock_guard<std::mutex> lk(mu_);
+        per_start_ = (uint32_t)per;
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu_);
         ring_ = coll->ring();
         flush_ring();
     }
@@ -872,11 +896,9 @@ void TickTransport::run() {
                 const uint64_t t1 = mono_ns();
                 lk.lock();
                 if (rc != 0) break;
-                if (stats_) {
-                    start_sum_ns_ += t1 - t0;
-                    start_n_++;
-                    start_max_ns_ = std::max(start_max_ns_, t1 - t0);
-                }
+                start_sum_ns_ += t1 - t0;
+                start_n_++;
+                start_max_ns_ = std::max(start_max_ns_, t1 - t0);
                 for (uint64_t j = 0; j < per; j++) issued_at[(size_t)((issued + j) % depth)] = t1;
                 issued += per;
             }
@@ -918,7 +940,7 @@ void TickTransport::run() {
             if (ring_) {
                 // Our own slot says how far the seals got through the outbox.
                 const TickSlot &mine = got[rank_];
-                if (stats_) {
+                {
                     const uint64_t t = mono_now_ns();
                     for (uint32_t r = 0; r < std::min<uint32_t>(mine.count, kTickMsgs); r++) {
                         const uint64_t d = t - post_ns_[(mine.first + r) & (kTickRing - 1)];

@@ -912,6 +912,25 @@ void ocm_x_quiesce(void) {
     service_park();
 }
 
+// The local daemon's tick control transport statistics (TickStatsWire as 10
+// words: ticks, own records, latency sum / max ns, periods, period sum ns,
+// start() calls, their sum / max ns, transport | ticks_per_start << 32).
+int ocm_x_tick_stats(uint64_t out[10]) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (!s.inited || !out) return -1;
+    Msg m = new_msg(MSG_TICK_STATS);
+    Msg r;
+    if (rpc(m, &r, s.rpc_timeout_ms) != 0) return -1;
+    TickStatsWire st;
+    std::memcpy(&st, r.u.raw, sizeof(st));
+    const uint64_t v[10] = {st.ticks, st.own_records, st.lat_sum_ns, st.lat_max_ns, st.periods, st.period_sum_ns,
+                            st.starts, st.start_sum_ns, st.start_max_ns,
+                            (uint64_t)st.transport | ((uint64_t)st.ticks_per_start << 32)};
+    std::memcpy(out, v, sizeof(v));
+    return 0;
+}
+
 // Copy-service diagnostics: {ops, ns posting requests, ns waiting for done,
 // GPU ticks (100 MHz) from doorbell seen to done published, relaunches after an
 // idle exit}. The doorbell record stays in host memory (a BAR-mapped HBM record

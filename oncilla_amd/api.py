@@ -183,6 +183,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
             "ocm_x_service_stats": (None, [ctypes.POINTER(u64)]),
+            "ocm_x_tick_stats": (ctypes.c_int, [ctypes.POINTER(u64)]),
             "ocm_x_quiesce": (None, []),
             "ocm_x_service_trace": (i32, [ctypes.POINTER(u64), i32]),
             "ocm_x_adam": (i32, [vp, vp, vp, u64, u64, u64, ctypes.POINTER(ctypes.c_float), vp]),
@@ -372,6 +373,22 @@ def service_stats() -> dict:
     n = int(out[0])
     return {"ops": n, "post_us": out[1] / n / 1e3 if n else None, "wait_us": out[2] / n / 1e3 if n else None,
             "gpu_us": out[3] / 100.0 / n if n else None, "relaunches": int(out[4])}
+
+
+def tick_stats() -> dict | None:
+    """The local daemon's tick control transport (RCCL or socket collective):
+    ticks completed, this rank's own records from post to delivery (mean / max
+    microseconds), the mean gap between completed ticks, and the host time per
+    Collective::start. None when the call fails; zeros on a TCP-only daemon."""
+    out = (ctypes.c_uint64 * 10)()
+    if load().ocm_x_tick_stats(out) != 0:
+        return None
+    n, p, k = int(out[1]), int(out[4]), int(out[6])
+    return {"ticks": int(out[0]), "own_records": n,
+            "hop_mean_us": round(out[2] / n / 1e3, 2) if n else None, "hop_max_us": round(out[3] / 1e3, 1),
+            "tick_period_mean_us": round(out[5] / p / 1e3, 2) if p else None,
+            "start_mean_us": round(out[7] / k / 1e3, 2) if k else None, "start_max_us": round(out[8] / 1e3, 1),
+            "transport": int(out[9] & 0xFFFFFFFF), "ticks_per_start": int(out[9] >> 32)}
 
 
 def service_totals() -> dict:

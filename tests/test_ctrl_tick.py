@@ -187,6 +187,8 @@ def test_rccl_tick_single_gpu(mesh_factory, monkeypatch, mode):
             a.free()
         assert c.stats(0)["ctrl_ticks"] > before
         assert c.stats(0)["ctrl"] == "rccl"  # never fell back
+        st = api.tick_stats()  # the daemon's own records, post -> delivery through the allgather
+        assert st["transport"] == 2 and st["own_records"] > 0 and st["hop_mean_us"] > 0, st
     logs = m.logs()
     assert "rccl tick transport" in logs
     if RCCL_TICK_MODES[mode].get("OCM_TICK_GRAPH", "0") != "0":
@@ -304,3 +306,27 @@ def test_a_rank_without_tick_batches_stays_in_step(mesh_factory):
         assert _ctrl(c, 3) == ["socket"] * 3
     logs = m.logs()
     assert "falling back to TCP" not in logs and "leaving the" not in logs, logs
+
+
+@pytest.mark.parametrize("sealed", ["1", "batch4"])
+def test_tick_stats_query(mesh_factory, sealed):
+    """api.tick_stats(): the local daemon's tick transport statistics over the
+    mailbox (MSG_TICK_STATS): ticks, own records from post to delivery, the host
+    time per Collective::start, and how many ticks one start queues."""
+    m = mesh_factory(3, extra_args=["--ctrl", "socket"], env={**_seal_env(sealed), "OCM_LEASE_BYTES": "0"})
+    with api.Client(daemon_rank=1, ns=m.ns) as c:
+        _wait_tick_up(c, 3)
+        for _ in range(10):
+            c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20, remote_rank=2).free()
+        st = api.tick_stats()
+        assert st is not None and st["ticks"] > 0 and st["own_records"] > 0, st
+        assert st["hop_mean_us"] > 0 and st["start_mean_us"] > 0, st
+        assert st["transport"] == 1, st  # socket ticks
+        assert st["ticks_per_start"] == (4 if sealed == "batch4" else 1), st
+
+
+def test_tick_stats_on_tcp(mesh_factory):
+    m = mesh_factory(2)
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        st = api.tick_stats()
+        assert st is not None and st["ticks"] == 0 and st["transport"] == 0, st
