@@ -35,9 +35,20 @@ METRICS = {
 }
 
 
+# the attached daemon's control-transport statistics (api.tick_stats)
+TICK_METRICS = {
+    "own_records": "this daemon's records delivered through tick collectives",
+    "hop_mean_us": "mean post -> delivery time of those records (one hop)",
+    "hop_max_us": "longest such hop",
+    "tick_period_mean_us": "mean gap between completed ticks",
+    "start_mean_us": "mean host time to queue a tick (seal launch + collective enqueue)",
+}
+
+
 class Exporter:
-    def __init__(self, client: api.Client):
+    def __init__(self, client: api.Client, rank: int = 0):
         self.client = client
+        self.rank = rank  # the daemon this exporter is attached to
         self._lock = threading.Lock()  # one mailbox: scrapes one at a time
 
     def render(self) -> str:
@@ -56,6 +67,15 @@ class Exporter:
             for r, st in rows:
                 if st is not None:
                     out.append(f'oncilla_{key}{{rank="{r}",gpu="{st["gpu"]}"}} {st[key]}')
+        # the attached daemon's tick transport (api.tick_stats: local daemon only)
+        with self._lock:
+            ts = api.tick_stats()
+        if ts is not None:
+            me = self.rank
+            for key, text in TICK_METRICS.items():
+                if ts.get(key) is not None:
+                    out += [f"# HELP oncilla_tick_{key} {text}", f"# TYPE oncilla_tick_{key} gauge",
+                            f'oncilla_tick_{key}{{rank="{me}"}} {ts[key]}']
         return "\n".join(out) + "\n"
 
 
@@ -67,7 +87,7 @@ def serve(ns: str, port: int, rank: int = 0, ready: Optional[threading.Event] = 
 
     os.environ.setdefault("OCM_NO_GPU", "1")  # inspecting needs no GPU
     with api.Client(daemon_rank=rank, ns=ns) as c:
-        exp = Exporter(c)
+        exp = Exporter(c, rank)
 
         class Handler(BaseHTTPRequestHandler):
             def do_GET(self):  # noqa: N802 - http.server API

@@ -178,6 +178,7 @@ def test_prometheus_metrics_exporter(mesh_factory, monkeypatch):
         assert f'oncilla_up{{rank="{r}"}} 1' in text
         assert f'oncilla_host_capacity{{rank="{r}",gpu="-1"}}' in text
     assert "# TYPE oncilla_n_alloc gauge" in text
+    assert 'oncilla_tick_own_records{rank="1"} 0' in text  # TCP mesh: no tick transport
 
 
 def test_shared_memory_link_carries_the_rpcs_and_survives_idle_daemons(mesh_factory, monkeypatch):
