@@ -122,7 +122,7 @@ struct NodeConfig {
 // between completed ticks, and the host time the tick thread spends queueing them.
 struct TickStatsWire {
     uint64_t ticks;           // ticks completed
-    uint64_t own_records;     // own records seen delivered (device-sealed outboxes)
+    uint64_t own_records;     // own records seen delivered
     uint64_t lat_sum_ns, lat_max_ns;
     uint64_t periods, period_sum_ns;
     uint64_t starts, start_sum_ns, start_max_ns;  // Collective::start calls and their host time

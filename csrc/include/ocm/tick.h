@@ -212,13 +212,14 @@ private:
     std::mutex mu_;
     std::condition_variable cv_;
     std::deque<TickRecord> out_;
+    std::deque<uint64_t> out_ns_;       // when each queued record was posted (statistics)
     std::vector<Msg> in_;
     std::atomic<bool> stop_{false}, failed_{false}, announce_{false}, up_{false}, in_ready_{false};
     std::atomic<uint64_t> ticks_{0}, wake_upto_{0}, announce_tick_{0};
     TickRing *ring_ = nullptr;  // device-sealed collectives: their outbox (under mu_)
     uint64_t ring_sent_ = 0;    // ring records a completed tick of ours carried
     uint64_t ring_pub_ = 0;     // records appended (host shadow of ring_->published)
-    // Post -> delivery latency of this rank's own records (device-sealed rings),
+    // Post -> delivery latency of this rank's own records,
     // completed-tick periods and start() host time; OCM_TICK_STATS=1 logs them at stop.
     bool stats_ = false, stats_logged_ = false;
     uint64_t post_ns_[kTickRing] = {};
@@ -232,6 +233,7 @@ private:
     // Host-filled collectives: records of issued ticks not yet completed here
     // (and how many each tick took), re-sent by take_unsent if the tick fails.
     std::deque<TickRecord> inflight_;
+    std::deque<uint64_t> inflight_ns_;  // their post times
     std::deque<uint32_t> inflight_n_;
     bool timed_out_ = false;  // the watchdog (OCM_TICK_TIMEOUT_MS) ended the transport
 };

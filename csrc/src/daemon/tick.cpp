@@ -720,6 +720,7 @@ bool TickTransport::post(int dest, const Msg &m) {
         r.dest = dest;
         r.msg = m;
         out_.push_back(r);
+        out_ns_.push_back(mono_now_ns());
         flush_ring();
     }
     cv_.notify_all();
@@ -734,9 +735,10 @@ void TickTransport::flush_ring() {
     while (!out_.empty() && pub - ring_sent_ < kTickRing) {
         TickRecord &r = ring_->rec[pub & (kTickRing - 1)];
         r = out_.front();
-        post_ns_[pub & (kTickRing - 1)] = mono_now_ns();
+        post_ns_[pub & (kTickRing - 1)] = out_ns_.front();  // when it was posted (it may have waited for room)
         ring_->tag[pub & (kTickRing - 1)] = tick_record_tag(reinterpret_cast<const uint64_t *>(&r), pub);
         out_.pop_front();
+        out_ns_.pop_front();
         pub++;
     }
     if (pub == ring_pub_) return;
@@ -786,8 +788,10 @@ std::vector<TickRecord> TickTransport::take_unsent() {
     v.insert(v.end(), inflight_.begin(), inflight_.end());
     v.insert(v.end(), out_.begin(), out_.end());
     inflight_.clear();
+    inflight_ns_.clear();
     inflight_n_.clear();
     out_.clear();
+    out_ns_.clear();
     ring_sent_ = ring_pub_;
     return v;
 }
@@ -884,7 +888,9 @@ void TickTransport::run() {
                     while (!out_.empty() && slot->count < (uint32_t)kTickMsgs) {
                         slot->rec[slot->count++] = out_.front();
                         inflight_.push_back(out_.front());  // until the tick completes here
+                        inflight_ns_.push_back(out_ns_.front());
                         out_.pop_front();
+                        out_ns_.pop_front();
                     }
                     inflight_n_.push_back(slot->count);
                     slot->busy = out_.empty() ? 0 : 1;
@@ -957,7 +963,15 @@ void TickTransport::run() {
                 ring_sent_ = std::max<uint64_t>(ring_sent_, mine.first + std::min<uint32_t>(mine.count, kTickMsgs));
                 flush_ring();
             } else if (!inflight_n_.empty()) {
-                for (uint32_t r = 0; r < inflight_n_.front() && !inflight_.empty(); r++) inflight_.pop_front();
+                const uint64_t t = mono_now_ns();
+                for (uint32_t r = 0; r < inflight_n_.front() && !inflight_.empty(); r++) {
+                    inflight_.pop_front();
+                    const uint64_t d = t - inflight_ns_.front();  // host-filled: post -> this tick completed here
+                    inflight_ns_.pop_front();
+                    lat_sum_ns_ += d;
+                    lat_n_++;
+                    lat_max_ns_ = std::max(lat_max_ns_, d);
+                }
                 inflight_n_.pop_front();
             }
             for (int k = 0; k < n_; k++) {

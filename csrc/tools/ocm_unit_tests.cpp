@@ -488,13 +488,13 @@ static void t_tick_tags() {
 // stand-in for the RCCL seal kernel): records to ourselves come back in order,
 // and with OCM_TICK_SOCKET_BATCH the transport queues ticks K at a time and
 // stops on a multiple of K.
-static void tick_roundtrip(int batch) {
-    setenv("OCM_TICK_SOCKET_SEAL", "1", 1);
+static void tick_roundtrip(int batch, bool sealed = true) {
+    setenv("OCM_TICK_SOCKET_SEAL", sealed ? "1" : "0", 1);
     if (batch > 1)
         setenv("OCM_TICK_SOCKET_BATCH", std::to_string(batch).c_str(), 1);
     else
         unsetenv("OCM_TICK_SOCKET_BATCH");
-    const std::string ns = "ut" + std::to_string(getpid()) + "_" + std::to_string(batch);
+    const std::string ns = "ut" + std::to_string(getpid()) + "_" + std::to_string(batch) + (sealed ? "s" : "h");
     TickTransport tt(0, 1, [ns](std::string *err, const std::atomic<bool> *cancel) {
         return make_socket_collective(ns, 0, 1, sizeof(TickSlot), err, cancel);
     });
@@ -529,6 +529,10 @@ static void tick_roundtrip(int batch) {
         last = now;
     }
     CHECK(last > 0 && last % (uint64_t)batch == 0);
+    TickStatsWire st;
+    tt.stats(&st);
+    CHECK(st.own_records == (uint64_t)kN && st.lat_sum_ns > 0 && st.starts > 0);
+    CHECK(st.ticks_per_start == (uint32_t)batch);
     tt.stop();
     CHECK(!tt.failed());
     unsetenv("OCM_TICK_SOCKET_SEAL");
@@ -537,6 +541,7 @@ static void tick_roundtrip(int batch) {
 
 static void t_tick_transport() { tick_roundtrip(1); }
 static void t_tick_transport_batched() { tick_roundtrip(4); }
+static void t_tick_transport_host_filled() { tick_roundtrip(1, false); }
 
 int main(int argc, char **argv) {
     if (argc > 1 && std::strcmp(argv[1], "--nodefile") == 0) {
@@ -565,7 +570,8 @@ int main(int argc, char **argv) {
                  {"arena_host", t_arena_host},   {"siphash", t_siphash},
                  {"shmlink", t_shmlink},         {"tick_tags", t_tick_tags},
                  {"tick_transport", t_tick_transport},
-                 {"tick_transport_batched", t_tick_transport_batched}};
+                 {"tick_transport_batched", t_tick_transport_batched},
+                 {"tick_transport_host_filled", t_tick_transport_host_filled}};
     for (auto &t : tests) {
         int before = g_fail;
         t.fn();

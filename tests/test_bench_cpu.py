@@ -50,10 +50,10 @@ def test_bench_multi_rank(native, n):
     assert "alloc_p50_us" in cp["tcp"] and "alloc_p50_us" in cp["socket"], cp
     assert cp["tcp"]["alloc_p50_us"] > 0 and cp["tcp"]["ticks_rank0"] == 0, cp
     assert cp["socket"]["alloc_p50_us"] > 0 and cp["socket"]["ticks_rank0"] > 0, cp
-    # per-rank hop latency of the tick transport (api.tick_stats on every rank; measured
-    # for device-sealed outboxes, as RCCL ticks use: None with the socket ring's host-filled slots)
+    # per-rank hop latency of the tick transport (api.tick_stats on every rank; a rank
+    # that posted nothing through the ticks has none)
     hops = cp["socket"]["hop_mean_us_per_rank"]
-    assert len(hops) == n and all(h is None or h > 0 for h in hops), cp
+    assert len(hops) == n and all(h is None or h > 0 for h in hops) and any(hops), cp
     assert cp["socket"]["start_mean_us_rank0"] > 0, cp
 
 
