@@ -13,8 +13,11 @@
 // launch-and-wait costs ~12-16 us on MI355X, a queued collective ~3.5 us,
 // profiles/rccl_tick_floor_r02.json). Whether tick k is issued is decided from
 // the gathered contents of ticks that every rank has already completed, so all
-// ranks issue the same sequence. Measured, a queued record then waits behind
-// empty ticks, so the RCCL default depth is 1 (OCM_TICK_DEPTH).
+// ranks issue the same sequence. With device-sealed slots (the default) a record
+// rides the next tick to execute, not the next one queued, so the RCCL default
+// depth is 2 (OCM_TICK_DEPTH; host-filled slots: 1, where a queued record would
+// wait behind empty ticks). OCM_TICK_GRAPH=K queues ticks K at a time as replays
+// of captured graphs.
 //
 // The collective is pluggable: RcclCollective (ncclAllGather on the daemon's
 // MI355X) in production, SocketCollective (ring allgather over abstract unix
