@@ -27,13 +27,21 @@ def test_bench_single(native):
     assert res["alloc_p50_us"] > 0 and res["config"]["remote_tier"] == "host"
 
 
-@pytest.mark.parametrize("n", [2, 8])
-def test_bench_multi_rank(native, n):
+# "ticks": the main mesh's records ride tick collectives as they would over RCCL on a
+# GPU node (--ctrl auto with the socket stand-in), device-sealed and queued 4 at a time
+TICK_ENV = {"OCM_CTRL_AUTO_SOCKET": "1", "OCM_TICK_SOCKET_SEAL": "1", "OCM_TICK_SOCKET_BATCH": "4"}
+
+
+@pytest.mark.parametrize("n,mode", [(2, "tcp"), (8, "tcp"), (8, "ticks")])
+def test_bench_multi_rank(native, n, mode):
     # the driver's multi-GPU launch shape (torch.distributed.run, one daemon per rank), on gloo + CPU daemons
+    env = dict(os.environ, **(TICK_ENV if mode == "ticks" else {}))
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
-                        "--master-addr", "127.0.0.1", "--master-port", str(29533 + n), os.path.join(REPO, "bench.py"),
+                        "--master-addr", "127.0.0.1", "--master-port", str(29533 + n + (mode == "ticks")),
+                        os.path.join(REPO, "bench.py"),
                         "--gpus", str(n), "--device", "cpu", "--steps", "2", "--warmup", "1", "--max-bytes",
-                        str(4 << 20), "--alloc-samples", "20"], capture_output=True, text=True, timeout=300, cwd="/tmp")
+                        str(4 << 20), "--alloc-samples", "20"], capture_output=True, text=True, timeout=300, cwd="/tmp",
+                       env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-1500:]
     res = _last_json(r.stdout)
     assert res["n_gpus"] == n and res["value"] > 0 and res["config"]["parallelism"] == f"stripe{n}"
@@ -45,6 +53,8 @@ def test_bench_multi_rank(native, n):
     # CPU ranks move no byte over xGMI, so the flag must say so
     assert res["xgmi"] is False and len(res["ranks"]) == n, res.get("ranks")
     assert all(d["ctrl"] in ("tcp", "socket", "rccl") and d["peer_access"] == 0 for d in res["ranks"]), res["ranks"]
+    if mode == "ticks":
+        assert all(d["ctrl"] == "socket" for d in res["ranks"]), res["ranks"]
     # control-plane extra: the same allocation path on TCP links and on socket-collective ticks
     cp = res["control_plane"]
     assert "alloc_p50_us" in cp["tcp"] and "alloc_p50_us" in cp["socket"], cp
