@@ -253,7 +253,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
         const unsigned sh = x.put ? s.svc_host_tile_shift_put : s.svc_host_tile_shift_get;
         if (sh >= 12 && sh < x.tile_shift) x.tile_shift = sh;
     }
-    const unsigned long long seq = ++s.svc_seq;
+    unsigned long long seq = ++s.svc_seq;
     if (s.svc_running && __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE) != 0) {
         // The instance left on its idle timeout (OCM_SERVICE_IDLE_US): reap it and
         // start the next one right away instead of posting to nobody.
@@ -309,6 +309,13 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
                 s.svc_running = false;
                 s.svc_relaunches++;
                 if (finished()) return 0;
+                // Re-post under a fresh seq. Direct gang members of the instance that
+                // left may have served part of this request and stored its seq in their
+                // WGDONE words; under the old seq those stale words would count as the
+                // new instance's members finishing, and the op would return while some
+                // of them were still copying (a later write to the local half then raced
+                // the copy: tests/test_gpu_service.py::test_service_direct_and_relayed_gangs_interleave).
+                seq = ++s.svc_seq;
                 if (service_start(seq) != 0) return -1;
                 gang = gang_word();              // counted afresh by the new instance
                 service_post(rq, x, gang, seq);  // start cleared the doorbell: re-post

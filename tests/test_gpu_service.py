@@ -82,11 +82,16 @@ def test_service_restarts_after_idle_exit(mesh_factory):
         a.free()
 
 
-def test_service_direct_and_relayed_gangs_interleave(mesh_factory):
+@pytest.mark.parametrize("idle_us", ["50", "1"])
+def test_service_direct_and_relayed_gangs_interleave(mesh_factory, monkeypatch, idle_us):
     # Gangs of up to 16 workgroups poll their own host record; wider ones (HBM
     # ops above 1 MiB, host-tier ops above 4 MiB) are relayed by workgroup 0.
     # Interleave solo ops, direct gangs (16 KiB host-get tiles included) and
-    # relayed gangs on both tiers, with idle exits in between.
+    # relayed gangs on both tiers, with idle exits in between. idle_us=1: the
+    # service leaves after almost every op, so requests keep landing on an
+    # instance that is leaving (whose direct members may serve part of one: the
+    # re-post must not count their completion words).
+    monkeypatch.setenv("OCM_SERVICE_IDLE_US", idle_us)
     m = mesh_factory(1, gpus=[0])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         n = 8 << 20
