@@ -494,7 +494,7 @@ def main() -> int:
                 pair = ph.run("pair_alloc", alloc)
                 tuned = None
                 if world > 1 and not args.no_autotune:
-                    tuned = ph.run("autotune", lambda: wl.autotune(pair, min(256 << 20, max_bytes), reps=3,
+                    tuned = ph.run("autotune", lambda: wl.autotune(pair, min(256 << 20, max_bytes), reps=5,
                                                                    gather=lambda obj: gather_obj(dist, obj, world)))
                 ph.run("verify", lambda: verify(pair))
                 return pair, tuned
@@ -548,6 +548,10 @@ def main() -> int:
             st, _ = _local(lambda: client.stats(rank))
             d["ctrl"] = st["ctrl"] if st else None
             d["remote_gpus"] = sorted({e["owner_gpu"] for e in info["extents"] if e["tier"] == api.OCM_TIER_GPU})
+            if use_gpu:
+                # copy-service health: ops that timed out (and fell back to launches),
+                # gang ops sized below their width because fewer workgroups were resident
+                d["service"] = api.service_health()
             return d
 
         diag, _ = _local(rank_diag)
@@ -562,14 +566,35 @@ def main() -> int:
             ch = ph.run("characterize", lambda: wl.characterize(pair, sizes, breakdown_max=(4 << 20) if use_gpu else 0))
             chs = gather_obj(dist, ch, world)
             for s in sizes:
+                # headline per size: the p50 of ops timed one by one (slowest rank); p99
+                # and mean alongside, so an outlier moves p99 rather than the row
                 g = max(c[s]["get_s"] for c in chs)
                 p = max(c[s]["put_s"] for c in chs)
                 sweep[str(s)] = {"get_GiBps": round(world * s / g / GiB, 3), "put_GiBps": round(world * s / p / GiB, 3),
-                                 "get_us": round(g * 1e6, 2), "put_us": round(p * 1e6, 2)}
+                                 "get_us": round(g * 1e6, 2), "put_us": round(p * 1e6, 2),
+                                 "get_p99_us": round(max(c[s]["get_p99_s"] for c in chs) * 1e6, 2),
+                                 "put_p99_us": round(max(c[s]["put_p99_s"] for c in chs) * 1e6, 2),
+                                 "get_mean_us": round(max(c[s]["get_mean_s"] for c in chs) * 1e6, 2),
+                                 "put_mean_us": round(max(c[s]["put_mean_s"] for c in chs) * 1e6, 2),
+                                 "ops": min(min(c[s]["get_n"], c[s]["put_n"]) for c in chs),
+                                 "relaunches": sum(c[s]["get_relaunches"] + c[s]["put_relaunches"] for c in chs)}
                 if chs[0][s].get("service"):
                     # rank 0's copy-service breakdown per op (us): host post, GPU doorbell-seen
                     # -> done, and the crossings (doorbell read + completion write over PCIe)
                     sweep[str(s)]["service_rank0"] = chs[0][s]["service"]
+        # ---- small ops after host idle gaps: every rank at once ----
+        idle_gap = {}
+        if not args.no_characterize:
+            ig = ph.run("idle_gap", lambda: wl.idle_gap_latency(pair, 4096))
+            igs = gather_obj(dist, ig, world)
+            for gap in ig:
+                row = {k: (max(x[gap][k] for x in igs) if k.endswith("_us") else sum(x[gap][k] for x in igs))
+                       for k in ig[gap]}
+                idle_gap[gap] = row
+            base = idle_gap.get("0")
+            if base and "1000" in idle_gap:
+                idle_gap["ratio_1ms_vs_back_to_back"] = {
+                    k: round(idle_gap["1000"][f"{k}_p50_us"] / base[f"{k}_p50_us"], 2) for k in ("get", "put")}
         # ---- extras, after the timed region (never affect the metric) ----
         # Every rank reaches every collective below even when its local part
         # fails, so a failure is recorded instead of deadlocking the job.
@@ -631,8 +656,15 @@ def main() -> int:
             "alloc_via_per_rank": [s["lat"].get("via") for s in stats],
             "xgmi": xgmi,
             "ranks": diags,
+            # no copy-service op timed out on any rank (no 10 s stall, no fallback to launches)
+            "service_clean": all(not d.get("service") or (d["service"]["aborts"] == 0 and
+                                                          d["service"]["incomplete_exits"] == 0) for d in diags),
             "sweep": sweep,
         }
+        if idle_gap:
+            # 4 KiB blocking get/put after 0 / 100 / 1000 / 10000 us of host idle: p50 / p99
+            # (us, slowest rank) and copy-service relaunches (all ranks)
+            result["idle_gap_4k"] = idle_gap
         if tuned:
             result["autotune"] = tuned
         if fallback:

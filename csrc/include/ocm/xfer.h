@@ -149,6 +149,17 @@ hipError_t xfer_batch_graph_node(hipGraph_t graph, hipGraphNode_t dep, const Xfe
 // Bounded: workgroup 0 leaves on kServiceStop or after `idle_ticks` of
 // s_memrealtime (100 MHz) without work; on leaving it stores STOP as the relayed
 // seq (the gang leaves on it) and `exited` = the first seq it did not serve.
+// Roster (round 4): nothing guarantees that all `blocks` workgroups of the
+// launch are resident at once (other processes' kernels hold CUs; a queue can be
+// preempted). Completion must never wait for a workgroup that has not started:
+// a gang member's id is its check-in order (workgroup 0 is member 0, every other
+// workgroup takes a ticket from ServiceBox::checkin when it starts), workgroup 0
+// publishes the number of checked-in members as ServiceSlot::roster, and the host
+// sizes every gang to at most that roster, so each member a request names is
+// already running. A member that checks in later only gets requests posted after
+// it was counted. Workgroup 0 also takes its idle exit only once the last gang
+// request is complete (every member it named has finished), so a member that was
+// slow to see a request is never told to leave before serving it.
 // Measured history: profiles/svc_trace_r02.json (a relay that re-hashed and
 // fenced first cost the gang ~2 us), profiles/svc_v3_direct_r02.json (every
 // workgroup polling the host record cost every op 3-4 us), profiles/
@@ -178,7 +189,10 @@ struct alignas(128) ServiceSlot {
     unsigned long long done;          // device -> host (own cache line)
     unsigned long long exited;        // device -> host: first seq NOT served when it left
     unsigned long long gpu_ticks;     // device -> host: sum of request-seen -> done ticks of workgroup 0 (100 MHz)
-    unsigned long long pad[13];
+    // device -> host: gang members resident so far (workgroup 0 included); the
+    // host zeroes it before a launch and sizes every gang to at most this many.
+    unsigned long long roster;
+    unsigned long long pad[12];
     // WGDONE: gang member i stores the seq it finished here (device -> host)
     unsigned long long wg_done[kServiceWgDoneMax];
 };
@@ -190,6 +204,8 @@ struct alignas(128) ServiceBox {
     unsigned long long rec[16];       // relayed request record (ServiceReq words), STOP as seq to leave
     unsigned long long cnt;           // gang completions, over all requests (only grows)
     unsigned long long pad1[15];
+    unsigned long long checkin;       // workgroups other than 0 that have started (member id = ticket + 1)
+    unsigned long long pad2[15];
     // OCM_SERVICE_PROTO bit 16 (TRACE): per workgroup, GPU clock (100 MHz) of its
     // last request: seen, copy start, copy drained, counted in / done published.
     unsigned long long trace[kServiceTraceWgs][4];
@@ -197,6 +213,7 @@ struct alignas(128) ServiceBox {
 
 // Workgroups that copy a (normalized) request: 1 when it has at most
 // `solo_tiles` tiles or the gang has one workgroup, else min(tiles, blocks).
+// `blocks` is the host's wanted width, already capped at the roster.
 uint32_t service_gang_size(const XferArgs &a, unsigned blocks, unsigned solo_tiles);
 // Post one request (words, sum, then seq with release) and flush the CPU's
 // write-combining buffers. gang = active | target << 16.

@@ -718,46 +718,46 @@ __device__ __forceinline__ void service_copy(const unsigned long long *sh, uint6
     }
 }
 
-__device__ __forceinline__ void service_stamp(ServiceBox *box, unsigned proto, int k) {
-    if ((proto & kServiceProtoTrace) && threadIdx.x == 0 && blockIdx.x < (unsigned)kServiceTraceWgs)
-        __hip_atomic_store(&box->trace[blockIdx.x][k], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+__device__ __forceinline__ void service_stamp(ServiceBox *box, unsigned proto, unsigned id, int k) {
+    if ((proto & kServiceProtoTrace) && threadIdx.x == 0 && id < (unsigned)kServiceTraceWgs)
+        __hip_atomic_store(&box->trace[id][k], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Copy this workgroup's share of the request in `sh` and make it visible
-// system-wide; the workgroup that completes the request publishes `done`.
+// Copy member `id`'s share of the request in `sh` and make it visible
+// system-wide; the member that completes the request publishes `done`.
 __device__ __forceinline__ void service_serve(const unsigned long long *sh, unsigned long long s, ServiceSlot *slot,
-                                              ServiceBox *box, unsigned proto) {
+                                              ServiceBox *box, unsigned proto, unsigned id) {
     const unsigned long long gang = sh[1];
     const unsigned long long active = gang & 0xFFFFull, target = (gang >> 16) & kServiceGangTargetMask;
-    if (blockIdx.x >= active) return;  // block-uniform: workgroups past `active` sit this one out
+    if (id >= active) return;  // block-uniform: members past `active` sit this one out
     // STRICT requests (extents in another GPU's HBM) take the fenced hand-off even
     // under the WT protocol: sc1 accesses keep this GPU's caches coherent with host
     // memory and its own HBM, but a resident instance may hold L2 lines of peer
     // memory from an earlier request, and nothing else invalidates them.
     const bool strict = (gang & kServiceGangStrict) != 0;
     const bool wt = (proto & kServiceProtoWT) && (!strict || (proto & kServiceProtoStrictWT));
-    service_stamp(box, proto, 1);
+    service_stamp(box, proto, id, 1);
     if (wt) {
         if (strict) {  // STRICTWT: drop stale L2 lines of peer memory before the sc1 (L2-served) loads
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        service_copy<ST_WT>(sh, blockIdx.x, active);
+        service_copy<ST_WT>(sh, id, active);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its sc1 stores
         __syncthreads();
     } else {
         if (proto & kServiceProtoWT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the poll skipped it
-        service_copy<ST_PLAIN>(sh, blockIdx.x, active);
+        service_copy<ST_PLAIN>(sh, id, active);
         block_release_system();
     }
-    service_stamp(box, proto, 2);
+    service_stamp(box, proto, id, 2);
     if (threadIdx.x == 0 && service_wg_done(proto, active)) {
         // WGDONE: this member's own completion word; the host waits for all of them.
         if (wt)
-            __hip_atomic_store(&slot->wg_done[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&slot->wg_done[id], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         else
-            __hip_atomic_store(&slot->wg_done[blockIdx.x], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&slot->wg_done[id], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     } else if (threadIdx.x == 0) {
         bool last = active == 1;
         if (!last) {
@@ -773,7 +773,24 @@ __device__ __forceinline__ void service_serve(const unsigned long long *sh, unsi
                 __hip_atomic_store(&slot->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    service_stamp(box, proto, 3);
+    service_stamp(box, proto, id, 3);
+}
+
+// Whether every member named by the last request workgroup 0 served (seq
+// `last`, gang word `gang`) has finished it. Wave 0 of workgroup 0, all lanes.
+__device__ __forceinline__ bool service_last_complete(ServiceSlot *slot, ServiceBox *box, unsigned proto,
+                                                      unsigned long long last, unsigned long long gang) {
+    const unsigned long long active = gang & 0xFFFFull, target = (gang >> 16) & kServiceGangTargetMask;
+    if (active <= 1) return true;  // workgroup 0 served it alone
+    const unsigned lane = threadIdx.x & 63u;
+    bool ok = true;
+    if (service_wg_done(proto, active)) {
+        for (unsigned long long i = lane; i < active; i += 64)
+            ok &= __hip_atomic_load(&slot->wg_done[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == last;
+    } else {
+        ok = __hip_atomic_load(&box->cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+    }
+    return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
 // Workgroup 0 polls the host request record across PCIe; for a gang request it
@@ -783,25 +800,37 @@ __device__ __forceinline__ void service_serve(const unsigned long long *sh, unsi
 // directly cost every op 3-4 us (profiles/svc_v3_direct_r02.json), and a relay
 // that re-hashed and fenced first cost the gang ~2 us (profiles/svc_trace_r02.json).
 // GANGREC (grq != nullptr): gang requests sit in their own host record, which
-// workgroups 0..direct_wgs-1 poll themselves; workgroup 0 reads both records in
+// members 0..direct_wgs-1 poll themselves; workgroup 0 reads both records in
 // one load (lanes 0..15 the small-op record, 16..31 the gang record) and
 // relays only gangs wider than direct_wgs to the others. 16 direct pollers
 // cost small ops nothing measurable; 32 cost them ~1 us
 // (profiles/svc_direct_gang_ab_r02.json).
+// Members are numbered in check-in order and workgroup 0 publishes how many
+// have checked in (the roster, see ocm/xfer.h): lane 32 of its poll reads the
+// check-in counter until the whole grid is in.
 __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq, const ServiceReq *grq,
                                                            ServiceSlot *slot, ServiceBox *box,
                                                            unsigned long long first_seq,
                                                            unsigned long long idle_ticks, unsigned proto,
                                                            unsigned direct_wgs) {
     __shared__ __attribute__((aligned(16))) unsigned long long sh[16];
+    __shared__ unsigned sh_id;
     const int tid = threadIdx.x;
     const bool lead = blockIdx.x == 0;
-    const bool direct = grq != nullptr && blockIdx.x < direct_wgs;  // polls the host gang record itself
+    if (tid == 0)
+        sh_id = lead ? 0u
+                     : 1u + (unsigned)__hip_atomic_fetch_add(&box->checkin, 1ull, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned id = __builtin_amdgcn_readfirstlane(sh_id);  // this workgroup's member id
+    const bool direct = grq != nullptr && id < direct_wgs;  // polls the host gang record itself
     const unsigned long long relay_above = grq != nullptr ? direct_wgs : 1;  // gangs wider than this are relayed
     const unsigned long long *req = reinterpret_cast<const unsigned long long *>(
         lead ? static_cast<const void *>(rq) : direct ? static_cast<const void *>(grq) : static_cast<const void *>(box->rec));
     const unsigned long long *greq = reinterpret_cast<const unsigned long long *>(grq);
     unsigned long long last = first_seq - 1;  // requests carry strictly increasing seqs
+    unsigned long long last_gang = 0;          // gang word of request `last` (workgroup 0's idle-exit test)
+    unsigned long long roster = 0;             // members published so far (workgroup 0)
     unsigned long long idle_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long ticks_sum =
         lead ? __hip_atomic_load(&slot->gpu_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
@@ -812,6 +841,7 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
             // (args, gang word, sum, seq); a seq whose hash checks out is whole.
             unsigned long long w = 0, s;
             for (;;) {
+                const bool count = lead && roster < gridDim.x;  // wave-uniform
                 if (tid < 16)
                     w = (lead || direct) ? __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                          : __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -819,6 +849,15 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                     w = __hip_atomic_load(greq + (tid - 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 else if (direct && !lead && tid == 16)
                     w = __hip_atomic_load(&box->rec[15], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // lead's STOP
+                else if (count && tid == 32)
+                    w = __hip_atomic_load(&box->checkin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (count) {
+                    const unsigned long long r = 1 + readlane64(w, 32);
+                    if (r > roster) {  // members counted here are running: requests may name them
+                        if (tid == 0) __hip_atomic_store(&slot->roster, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        roster = r;
+                    }
+                }
                 base = 0;
                 s = readlane64(w, 15);
                 if (direct) {
@@ -841,8 +880,13 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                     continue;  // seq landed before the rest of the record: read it again
                 }
                 if (lead && __builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks) {
-                    s = kServiceStop;
-                    break;
+                    // Leave only once every member the last request named is done
+                    // with it: a member that saw the STOP first would never serve it.
+                    if (service_last_complete(slot, box, proto, last, last_gang)) {
+                        s = kServiceStop;
+                        break;
+                    }
+                    idle_start = __builtin_amdgcn_s_memrealtime();
                 }
                 if (lead || direct)
                     __builtin_amdgcn_s_sleep(8);  // ~0.2 us between PCIe polls
@@ -867,9 +911,10 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
         const unsigned long long s = sh[0];
         if (s == kServiceStop) break;
         const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
-        service_stamp(box, proto, 0);
-        service_serve(sh, s, slot, box, proto);
+        service_stamp(box, proto, id, 0);
+        service_serve(sh, s, slot, box, proto, id);
         last = s;
+        last_gang = sh[1];
         idle_start = __builtin_amdgcn_s_memrealtime();  // every lane: the idle test must stay wave-uniform
         if (lead) {
             // Diagnostic, after `done` so it never delays it: a running sum in a

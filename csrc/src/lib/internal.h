@@ -252,6 +252,21 @@ struct State {
     // wait long for the persistent kernel to leave.
     unsigned long long svc_idle_ticks = 100ull * kServiceIdleUsDefault;
     uint64_t svc_relaunches = 0;    // instances started after an idle exit (ocm_x_service_stats)
+    // Roster (ocm/xfer.h): gangs are sized to the members already running. Right
+    // after a launch a gang op waits up to svc_roster_wait_ns for the grid to check
+    // in before it settles for fewer members (OCM_SERVICE_ROSTER_WAIT_US).
+    uint64_t svc_launch_ns = 0;
+    uint64_t svc_roster_wait_ns = 200000;
+    // Health counters (ocm_x_service_health): gang ops sized below the width they
+    // wanted because fewer members were resident, instances that left with the
+    // posted op unfinished (re-posted), ops abandoned after OCM_SERVICE_TIMEOUT_MS
+    // (drained, then redone by a launch), and whether an instance could not even
+    // be drained (the service is then off for good and the op fails).
+    uint64_t svc_degraded = 0, svc_incomplete_exits = 0, svc_aborts = 0;
+    unsigned long long svc_roster_min = ~0ull;  // smallest roster a gang op was sized to
+    bool svc_wedged = false;
+    uint64_t svc_timeout_ns = 10ull * 1000000000ull;  // OCM_SERVICE_TIMEOUT_MS
+    uint64_t svc_drain_ns = 10ull * 1000000000ull;    // OCM_SERVICE_DRAIN_MS: bound on the STOP drain after a timeout
     // network tier
     std::map<std::string, NetConn> net_conns;  // "ip:port#stream" -> connection
     std::map<int, int> fd_chans;               // owner rank -> mailbox connection for slab fds (MSG_SLAB_FD)
@@ -373,6 +388,8 @@ int service_start(unsigned long long first_seq);
 void service_park();
 void service_stop();
 // strict: an extent is in another GPU's HBM (kServiceGangStrict).
+// 0: done; -1: failed, and no instance holds the request any more (a launch may
+// redo the op); -2: failed and the instance could not be drained (no fallback).
 int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict);
 // Before a library launch: park the service when it may share the launch's hardware queue.
 void before_launch();

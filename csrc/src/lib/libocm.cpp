@@ -144,6 +144,9 @@ int ocm_init(void) {
     s.launch_flags = env_int("OCM_LAUNCH_FLAG", 1) != 0;
     s.svc_park_kernel = env_int("OCM_SERVICE_PARK_KERNEL", 0) != 0;
     s.svc_idle_ticks = 100ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_IDLE_US", kServiceIdleUsDefault));  // 100 MHz clock
+    s.svc_roster_wait_ns = 1000ull * (unsigned long long)std::max(0, env_int("OCM_SERVICE_ROSTER_WAIT_US", 200));
+    s.svc_timeout_ns = 1000000ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_TIMEOUT_MS", 10000));
+    s.svc_drain_ns = 1000000ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_DRAIN_MS", 10000));
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");
     s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
     s.tuning = xfer_tuning_from_env();
@@ -945,6 +948,22 @@ void ocm_x_service_stats(uint64_t out[5]) {
     out[4] = s.svc_relaunches;  // instances started because the previous one left idle
 }
 
+// Copy-service health: {gang ops sized below their wanted width because fewer
+// members were resident, instances that left with the posted op unfinished,
+// ops abandoned after OCM_SERVICE_TIMEOUT_MS (drained, then redone by a launch),
+// 1 if an instance could not be drained (service off, op failed), the smallest
+// roster a gang op was sized to (0: none yet), the current instance's roster}.
+void ocm_x_service_health(uint64_t out[6]) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    out[0] = s.svc_degraded;
+    out[1] = s.svc_incomplete_exits;
+    out[2] = s.svc_aborts;
+    out[3] = s.svc_wedged ? 1 : 0;
+    out[4] = s.svc_roster_min == ~0ull ? 0 : s.svc_roster_min;
+    out[5] = (s.svc && s.svc_running) ? __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE) : 0;
+}
+
 // Copy-service phase stamps of the last request (OCM_SERVICE_PROTO with the
 // TRACE bit): 4 GPU-clock words per workgroup for the first n workgroups.
 int ocm_x_service_trace(uint64_t *out, int n_wgs) {
@@ -1145,6 +1164,44 @@ double ocm_x_time_onesided(ocm_alloc_t a, ocm_param_t p, int iters) {
     clock_gettime(CLOCK_MONOTONIC, &t1);
     double dt = (double)(t1.tv_sec - t0.tv_sec) + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-9;
     return dt / (iters > 0 ? iters : 1);
+}
+
+// Per-op samples of a blocking one-sided op, each timed on its own: up to
+// `iters` ops, stopping early once `cap_ns` have passed (at least `min_iters`
+// ops). Before each op the calling thread stays busy for `gap_ns` without
+// touching the library (an application computing between small ops), so the
+// samples include whatever an idle gap costs the next op (the copy service's
+// idle exit and relaunch). out[i] = seconds of op i; *relaunches = copy-service
+// relaunches during the run. Returns the number of samples, -1 on an op failure.
+int ocm_x_time_onesided_samples(ocm_alloc_t a, ocm_param_t p, int iters, int min_iters, uint64_t gap_ns,
+                                uint64_t cap_ns, double *out, uint64_t *relaunches) {
+    auto ns = []() {
+        struct timespec t;
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+    };
+    uint64_t r0 = 0;
+    {
+        std::lock_guard<std::recursive_mutex> lk(S().mu);
+        r0 = S().svc_relaunches;
+    }
+    const uint64_t start = ns();
+    int n = 0;
+    for (; n < iters; n++) {
+        if (n >= min_iters && ns() - start > cap_ns) break;
+        if (gap_ns) {
+            const uint64_t g0 = ns();
+            while (ns() - g0 < gap_ns) __builtin_ia32_pause();
+        }
+        const uint64_t t0 = ns();
+        if (ocm_copy_onesided(a, p) != 0) return -1;
+        out[n] = (double)(ns() - t0) * 1e-9;
+    }
+    if (relaunches) {
+        std::lock_guard<std::recursive_mutex> lk(S().mu);
+        *relaunches = S().svc_relaunches - r0;
+    }
+    return n;
 }
 
 // Fill / check the deterministic word pattern on device or host memory.

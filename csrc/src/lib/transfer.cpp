@@ -188,7 +188,9 @@ int service_start(unsigned long long first_seq) {
             }
         }
     }
+    if (s.svc_wedged) OCM_FAIL(-1, "copy service: a previous instance could not be drained");
     __atomic_store_n(&s.svc->exited, 0ull, __ATOMIC_RELEASE);
+    __atomic_store_n(&s.svc->roster, 0ull, __ATOMIC_RELEASE);  // the new lead publishes its own
     service_store_seq(s.svc_req, 0ull);  // clear a STOP left by a parked instance
     if (s.svc_greq) service_store_seq(s.svc_greq, 0ull);
     s.svc_gang_total = 0;  // the launch zeroes the device counter
@@ -199,6 +201,7 @@ int service_start(unsigned long long first_seq) {
         OCM_FAIL(-1, "copy service launch failed");
     }
     s.svc_running = true;
+    s.svc_launch_ns = now_ns();
     return 0;
 }
 
@@ -245,6 +248,54 @@ void service_stop() {
     s.svc_stream = nullptr;
 }
 
+// Members of the running instance a gang may name (ocm/xfer.h roster): right
+// after a launch wait up to svc_roster_wait_ns for `want` of them to check in,
+// then settle for the ones that did (at least workgroup 0).
+static unsigned service_roster(unsigned want) {
+    State &s = S();
+    unsigned long long r = __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE);
+    while (r < want && now_ns() - s.svc_launch_ns < s.svc_roster_wait_ns) {
+        __builtin_ia32_pause();
+        r = __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE);
+    }
+    if (r < 1) r = 1;
+    if (r < want) s.svc_degraded++;
+    if (r < s.svc_roster_min) s.svc_roster_min = r;
+    return (unsigned)std::min<unsigned long long>(r, want);
+}
+
+// Give up on the instance holding request `seq`: STOP on both records, then wait
+// (bounded) until the kernel has left, so no member can still run the request
+// when the op is redone by a launch. -1: drained; -2: it would not drain.
+static int service_abort(unsigned long long seq, unsigned long long active, const char *why) {
+    State &s = S();
+    DeviceGuard g(s.device);
+    unsigned long long wg_in = 0;
+    for (unsigned long long i = 0; i < active && i < (unsigned long long)kServiceWgDoneMax; i++)
+        wg_in += __atomic_load_n(&s.svc->wg_done[i], __ATOMIC_ACQUIRE) == seq;
+    const unsigned long long ex = __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE);
+    const unsigned long long roster = __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE);
+    service_store_seq(s.svc_req, kServiceStop);
+    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
+    s.svc_aborts++;
+    const uint64_t t0 = now_ns();
+    hipError_t e;
+    while ((e = hipStreamQuery(s.svc_stream)) == hipErrorNotReady) {
+        if (now_ns() - t0 > s.svc_drain_ns) {
+            s.svc_wedged = true;
+            s.svc_max = 0;
+            OCM_FAIL(-2, "copy service %s (seq %llu, %llu members, %llu done words, roster %llu, exited %llu) "
+                         "and did not leave on STOP: not redoing the op",
+                     why, seq, active, wg_in, roster, ex);
+        }
+        usleep(100);
+    }
+    (void)hipGetLastError();
+    s.svc_running = false;
+    OCM_FAIL(-1, "copy service %s (seq %llu, %llu members, %llu done words, roster %llu, exited %llu); drained",
+             why, seq, active, wg_in, roster, ex);
+}
+
 // Run one normalized transfer through the resident kernel and wait for it.
 int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
     State &s = S();
@@ -264,19 +315,28 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
     }
     if (!s.svc_running && service_start(seq) != 0) return -1;
     // The host sizes the gang and the completion count every workgroup agrees on:
-    // up to the direct pollers (no relay) for ops they copy fast enough.
+    // up to the direct pollers (no relay) for ops they copy fast enough, and never
+    // wider than the members already running (the roster).
     const bool direct = s.svc_greq && x.len <= (hbm ? s.svc_direct_max_hbm : s.svc_direct_max_host);
-    const unsigned width = direct ? std::min(s.svc_direct, s.svc_blocks)
-                                  : (hbm ? s.svc_blocks : std::min(s.svc_gang_host, s.svc_blocks));
-    const unsigned long long active = service_gang_size(x, width, solo_tiles);
-    const bool wgdone = service_wg_done(s.svc_proto, active);
-    auto gang_word = [&]() {
+    unsigned long long active = 1;
+    bool wgdone = false;
+    ServiceReq *rq = s.svc_req;
+    unsigned long long gang = 0;
+    auto size_and_post = [&]() {
+        unsigned width = direct ? std::min(s.svc_direct, s.svc_blocks)
+                                : (hbm ? s.svc_blocks : std::min(s.svc_gang_host, s.svc_blocks));
+        if (service_gang_size(x, width, solo_tiles) > 1) width = service_roster(width);
+        active = service_gang_size(x, width, solo_tiles);
+        wgdone = service_wg_done(s.svc_proto, active);
         unsigned long long target = 0;
         if (active > 1 && !wgdone) {  // WGDONE gangs leave the counter alone
             s.svc_gang_total += active;
             target = s.svc_gang_total;
         }
-        return active | (target << 16) | (strict ? kServiceGangStrict : 0ull);
+        gang = active | (target << 16) | (strict ? kServiceGangStrict : 0ull);
+        // GANGREC: gang requests go to the record the whole gang polls.
+        rq = (active > 1 && s.svc_greq) ? s.svc_greq : s.svc_req;
+        service_post(rq, x, gang, seq);
     };
     // Completed: `done` (a solo op or the gang's last member), or under WGDONE
     // every member's own word.
@@ -286,11 +346,8 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
             if (__atomic_load_n(&s.svc->wg_done[i], __ATOMIC_ACQUIRE) != seq) return false;
         return true;
     };
-    unsigned long long gang = gang_word();
-    // GANGREC: gang requests go to the record the whole gang polls.
-    ServiceReq *rq = (active > 1 && s.svc_greq) ? s.svc_greq : s.svc_req;
     const uint64_t t0 = now_ns();
-    service_post(rq, x, gang, seq);
+    size_and_post();
     const uint64_t t_posted = now_ns();
     for (unsigned spins = 1;; spins++) {
         if (finished()) {
@@ -300,15 +357,23 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
             return 0;
         }
         if ((spins & 1023) == 0) {
-            // The kernel leaves after idle_ticks without work; if it left before
-            // taking this request, start a new one at this seq.
+            // The kernel leaves after idle_ticks without work, and only once the
+            // last request it took is complete. If it left before taking this one
+            // (exited <= seq), start a new instance for it. exited > seq with the
+            // op unfinished is not expected (workgroup 0 waits for its members):
+            // counted, and handled the same way, since after the stream sync no
+            // member of the old instance is left to finish it.
             const unsigned long long ex = __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE);
-            if (ex && ex <= seq) {
+            if (ex) {
                 DeviceGuard g(s.device);
                 (void)hipStreamSynchronize(s.svc_stream);
                 s.svc_running = false;
                 s.svc_relaunches++;
-                if (finished()) return 0;
+                if (finished()) {
+                    s.svc_ops++;
+                    return 0;
+                }
+                if (ex > seq) s.svc_incomplete_exits++;
                 // Re-post under a fresh seq. Direct gang members of the instance that
                 // left may have served part of this request and stored its seq in their
                 // WGDONE words; under the old seq those stale words would count as the
@@ -317,10 +382,9 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
                 // the copy: tests/test_gpu_service.py::test_service_direct_and_relayed_gangs_interleave).
                 seq = ++s.svc_seq;
                 if (service_start(seq) != 0) return -1;
-                gang = gang_word();              // counted afresh by the new instance
-                service_post(rq, x, gang, seq);  // start cleared the doorbell: re-post
+                size_and_post();  // sized to the new instance's roster; start cleared the doorbell
             }
-            if (now_ns() - t0 > 10ull * 1000000000ull) OCM_FAIL(-1, "copy service did not complete a transfer in 10 s");
+            if (now_ns() - t0 > s.svc_timeout_ns) return service_abort(seq, active, "did not complete a transfer in time");
         }
     }
 }
@@ -413,7 +477,11 @@ int xfer(lib_alloc *a, bool put, char *lin, Loc lloc, uint64_t rem_off, uint64_t
         // HBM owners keep small requests on workgroup 0 (profiles/svc_v4_r02.json).
         const unsigned solo = (!put && !a->any_gpu) ? std::min(s.svc_solo_tiles, s.svc_solo_tiles_host_get)
                                                     : s.svc_solo_tiles;
-        if (service_xfer(x, solo, a->any_gpu, a->any_peer || s.svc_force_strict) == 0) return 0;
+        const int rc = service_xfer(x, solo, a->any_gpu, a->any_peer || s.svc_force_strict);
+        if (rc == 0) return 0;
+        // -2: an instance may still hold the request; a launch now would race it.
+        if (rc == -2) return -1;
+        // -1: nothing holds the request any more (never launched, or drained after STOP).
         OCM_WARN("copy service failed (%s); falling back to launches", last_error());
         s.svc_max = 0;
     }

@@ -178,11 +178,14 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_xfer": (i32, [i32, vp, ctypes.POINTER(vp), i32, u64, u64, u64, i32, i32, i32, i32]),
             "ocm_x_time_device_copy": (ctypes.c_double, [i32, vp, vp, u64, i32, i32, i32, i32]),
             "ocm_x_time_onesided": (ctypes.c_double, [vp, ctypes.POINTER(OcmParams), i32]),
+            "ocm_x_time_onesided_samples": (i32, [vp, ctypes.POINTER(OcmParams), i32, i32, u64, u64,
+                                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]),
             "ocm_x_alloc_latency": (i32, [ctypes.POINTER(OcmAllocParams), ctypes.POINTER(OcmAllocExParams), i32,
                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
             "ocm_x_pattern": (ctypes.c_longlong, [vp, u64, u64, ctypes.c_uint32, i32]),
             "ocm_x_counters": (None, [ctypes.POINTER(u64)]),
             "ocm_x_service_stats": (None, [ctypes.POINTER(u64)]),
+            "ocm_x_service_health": (None, [ctypes.POINTER(u64)]),
             "ocm_x_tick_stats": (ctypes.c_int, [ctypes.POINTER(u64)]),
             "ocm_x_quiesce": (None, []),
             "ocm_x_service_trace": (i32, [ctypes.POINTER(u64), i32]),
@@ -373,6 +376,21 @@ def service_stats() -> dict:
     n = int(out[0])
     return {"ops": n, "post_us": out[1] / n / 1e3 if n else None, "wait_us": out[2] / n / 1e3 if n else None,
             "gpu_us": out[3] / 100.0 / n if n else None, "relaunches": int(out[4])}
+
+
+def service_health() -> dict:
+    """Copy-service health of this process (ocm/xfer.h roster): gang ops sized below
+    the width they wanted because fewer of the service's workgroups were running
+    (`degraded`), instances that left with the posted op unfinished and had it
+    re-posted (`incomplete_exits`, expected 0), ops abandoned after
+    OCM_SERVICE_TIMEOUT_MS and redone by a launch once the instance had drained
+    (`aborts`), whether an instance could not be drained at all (`wedged`), the
+    smallest roster a gang op was sized to (`roster_min`, 0: none yet) and the
+    running instance's roster (`roster`, 0: not running)."""
+    out = (ctypes.c_uint64 * 6)()
+    load().ocm_x_service_health(out)
+    return {"degraded": int(out[0]), "incomplete_exits": int(out[1]), "aborts": int(out[2]),
+            "wedged": bool(out[3]), "roster_min": int(out[4]), "roster": int(out[5])}
 
 
 def tick_stats() -> dict | None:
@@ -602,6 +620,22 @@ class Allocation:
         if t < 0:
             raise OcmError("one-sided op failed: " + last_error())
         return t
+
+    def time_onesided_samples(self, op_flag: int, nbytes: int, iters: int, gap_s: float = 0.0,
+                              cap_s: float = 1.0, min_iters: int = 5, local_offset: int = 0,
+                              remote_offset: int = 0) -> tuple[list, int]:
+        """Seconds of each blocking one-sided op, timed one by one inside the native
+        library: up to `iters` ops, stopping after `cap_s` (but not before `min_iters`),
+        each after `gap_s` of busy host time that does not touch the library. Returns
+        (samples, copy-service relaunches during the run)."""
+        p = OcmParams(local_offset, remote_offset, 0, 0, nbytes, op_flag)
+        out = (ctypes.c_double * max(1, iters))()
+        rel = ctypes.c_uint64(0)
+        n = self._c.lib.ocm_x_time_onesided_samples(self.handle, ctypes.byref(p), iters, min_iters,
+                                                    int(gap_s * 1e9), int(cap_s * 1e9), out, ctypes.byref(rel))
+        if n < 0:
+            raise OcmError("one-sided op failed: " + last_error())
+        return list(out[:n]), int(rel.value)
 
     def copy_in(self, src_ptr: int) -> None:
         if self._c.lib.ocm_copy_in(self.handle, ctypes.c_void_p(src_ptr)) != 0:

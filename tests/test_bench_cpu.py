@@ -226,3 +226,69 @@ def test_autotune_drops_a_fast_candidate_that_corrupts_data(native, monkeypatch)
     r = wl.autotune(pair, 1 << 20, gather=gather, candidates=cands)
     assert r["get"] == "reg_b256" and r["put"] == "reg_b256", r
     assert "verification" in r["GiBps"]["fast_but_wrong"]["get"]["error"], r
+
+
+def _fake_autotune(monkeypatch, secs, cands, gather=None):
+    """autotune over a fake pair whose per-config seconds come from secs[(cfg, op)] or secs[cfg]."""
+    from oncilla_amd import api
+    from oncilla_amd.models import workloads as wl
+
+    cur = {}
+    monkeypatch.setattr(api, "set_tuning_dir", lambda op, v, b, nt: cur.__setitem__(op, (v, b, nt)))
+
+    class FakePair(RoundTrip):
+        def time_onesided(self, op, n, iters):
+            v = secs[cur[op]]
+            return v[op] if isinstance(v, tuple) else v
+
+    pair = FakePair()
+    pair.cur = cur
+    return wl.autotune(pair, 1 << 20, gather=gather, candidates=cands), cur
+
+
+def test_autotune_keeps_auto_within_the_margin(native, monkeypatch):
+    """candidates within 3 % of auto (noise at 5 reps) never
+    replace it; one that is 10 % faster on every rank does; the margins are recorded."""
+    cands = {"auto": (0, 0, 1), "reg_b256": (1, 256, 1), "lds_default": (2, 0, 1)}
+    # get: both candidates 2 % faster (a tie); put: lds_default 10 % faster
+    secs = {(0, 0, 1): (1.0, 1.0), (1, 256, 1): (0.98, 0.985), (2, 0, 1): (0.98, 0.90)}
+    r, cur = _fake_autotune(monkeypatch, secs, cands)
+    assert r["get"] == "auto" and r["put"] == "lds_default", r
+    assert r["margin_required"] == 0.03 and r["reps"] == 5
+    assert abs(r["margins"]["get"]["reg_b256"] - 0.02) < 1e-6 and abs(r["margins"]["put"]["lds_default"] - 0.1) < 1e-6
+    assert cur[0] == (0, 0, 1) and cur[1] == (2, 0, 1)
+
+
+def test_autotune_needs_the_margin_on_every_rank(native, monkeypatch):
+    """A candidate 20 % faster on rank 0 but only 1 % faster on rank 1 keeps auto."""
+    cands = {"auto": (0, 0, 1), "reg_b256": (1, 256, 1)}
+    secs = {(0, 0, 1): 1.0, (1, 256, 1): 0.8}
+
+    def gather(obj):  # rank 1: reg_b256 is 0.99 of auto there
+        if isinstance(obj, tuple) and obj[0] == 0.8:
+            return [obj, (0.99, None)]
+        return [obj, obj]
+
+    r, _ = _fake_autotune(monkeypatch, secs, cands, gather=gather)
+    assert r["get"] == "auto" and r["put"] == "auto", r
+    assert abs(r["margins"]["get"]["reg_b256"] - 0.01) < 1e-6, r["margins"]
+
+
+def test_autotune_never_installs_a_get_only_variant_for_puts(native, monkeypatch):
+    """Push-based gets (variant 5) compete for gets only; their 'put' is auto's path."""
+    cands = {"auto": (0, 0, 1), "push": (5, 0, 1), "reg_b256": (1, 256, 1)}
+    secs = {(0, 0, 1): 1.0, (5, 0, 1): 0.5, (1, 256, 1): 0.9}
+    r, _ = _fake_autotune(monkeypatch, secs, cands)
+    assert r["get"] == "push" and r["put"] == "reg_b256", r
+    assert "push" not in r["margins"]["put"], r["margins"]
+
+
+def test_push_candidates_are_opt_in(monkeypatch):
+    """push-based gets stay out of the default candidates until a
+    multi-GPU box has run them (OCM_AUTOTUNE_PUSH=1 opts in)."""
+    from oncilla_amd.models import workloads as wl
+
+    monkeypatch.delenv("OCM_AUTOTUNE_PUSH", raising=False)
+    assert not any(v[0] == 5 for v in wl.default_candidates().values())
+    monkeypatch.setenv("OCM_AUTOTUNE_PUSH", "1")
+    assert {"push", "push_b1024"} <= set(wl.default_candidates())

@@ -349,12 +349,16 @@ def main() -> int:
                     print(json.dumps({"ok": False, "config": name, "error": str(e)}), flush=True)
                     return 1
         print(name, json.dumps(res[name]), flush=True)
-    line = json.dumps({"ok": True, "seed": args.seed, "bytes": args.bytes, "configs": res})
+    # a run is clean only if no copy-service op timed out
+    # (no 10 s stall, no fallback to launches) and no instance left an op unfinished.
+    health = api.service_health()
+    ok = health["aborts"] == 0 and health["incomplete_exits"] == 0 and not health["wedged"]
+    line = json.dumps({"ok": ok, "seed": args.seed, "bytes": args.bytes, "configs": res, "service_health": health})
     if args.out:
         with open(args.out, "w") as f:
             f.write(line + "\n")
     print(line)
-    return 0
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":
