@@ -160,7 +160,8 @@ private:
 
     // dispatch
     void handle_app_msg(Msg &m);
-    void handle_mesh_msg(Msg &m, int from_fd);
+    // via_tick: delivered by the tick transport (from_fd -1); the local queue passes false.
+    void handle_mesh_msg(Msg &m, int from_fd, bool via_tick = false);
     // Shared-memory links of the apps: take their requests (returns how many),
     // and the daemon_polling flag around the event loop's sleeps.
     int poll_links();
@@ -173,6 +174,7 @@ private:
     static constexpr size_t kAppBacklogMax = 4096;
     std::vector<pid_t> overflowed_apps_;
     std::vector<pid_t> link_pids_;  // poll_links scratch
+    int links_backlogged_ = 0;      // apps whose replies wait for ring room (after the last poll_links)
     void reap_overflowed_apps();
     void app_overflowed(App &a);
     // Once a tick transport exists, the allocation protocol's records are
@@ -183,9 +185,17 @@ private:
     // extent; a second DO_ALLOC response would free a live one). Those records
     // are unique by construction (seq, alloc_id, extent index), so a repeat is
     // always such a copy.
-    bool mesh_duplicate(const Msg &m);
-    std::unordered_set<uint64_t> mesh_seen_;    // content hashes (bounded window)
-    std::deque<uint64_t> mesh_seen_order_;      // the same, oldest first
+    // A record that reached us both through a tick and as a kMsgResent TCP copy
+    // (the tick fallback): the second arrival is dropped. Only those two paths are
+    // compared; plain TCP records are never de-duplicated.
+    bool mesh_duplicate(const Msg &m, bool via_tick, bool resent);
+    struct SeenWindow {  // content hashes, bounded, oldest first
+        std::unordered_multiset<uint64_t> set;
+        std::deque<uint64_t> order;
+        void add(uint64_t h);
+        bool take(uint64_t h);  // true (and forgotten) if present
+    };
+    SeenWindow seen_tick_, seen_resent_;
     uint64_t mesh_dups_dropped_ = 0;
     void send_rank(int r, Msg &m);      // to a daemon (self = local queue)
     void send_app(pid_t pid, const Msg &m);

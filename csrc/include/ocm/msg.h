@@ -51,6 +51,10 @@ enum MsgType : uint32_t {
 };
 
 enum MsgStatus : uint32_t { MSG_NO_STATUS = 0, MSG_REQUEST, MSG_RESPONSE };
+// Status bit of a mesh record re-sent over TCP after the tick transport failed
+// (TickTransport::take_unsent): the receiver drops it if the same record already
+// came through a tick, and a later tick copy if it came first. Cleared on receipt.
+constexpr uint32_t kMsgResent = 0x80000000u;
 
 enum Tier : uint32_t { TIER_NONE = 0, TIER_HOST = 1, TIER_GPU = 2 };
 

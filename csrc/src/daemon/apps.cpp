@@ -60,7 +60,16 @@ void Daemon::app_connect(const Msg &m, int fd) {
     pid_t pid = m.pid;
     if (apps_.count(pid)) {
         auto &old = apps_[pid];
-        if (old.fd != fd) app_disconnect(pid, false);
+        if (old.fd != fd) {
+            app_disconnect(pid, false);
+        } else if (old.pidfd >= 0) {
+            // A CONNECT retried on the same socket (the mesh was still joining):
+            // the entry is replaced below with a pidfd of its own (the
+            // old one leaked, with its epoll registration, on every retry).
+            ep_del(old.pidfd);
+            close(old.pidfd);
+            old.pidfd = -1;
+        }
     }
     App a;
     a.pid = pid;

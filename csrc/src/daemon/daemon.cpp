@@ -418,12 +418,18 @@ int Daemon::loop() {
         if (!overflowed_apps_.empty()) reap_overflowed_apps();
         const bool spinning = spin_ns && now_ns() - last_event_ns < spin_ns;
         int wait_ms = (self_q_.empty() && !spinning) ? timeout : 0;
+        // Replies waiting for room in an app's ring: the app frees slots
+        // without waking us, so look again within a millisecond instead of sleeping
+        // up to the loop timeout while it sleeps waiting for them.
+        if (links_backlogged_ && wait_ms > 1) wait_ms = 1;
         if (wait_ms > 0) {
             // About to sleep: from here on an app that posts must wake us; look once more.
             links_polling(false);
             if (poll_links() > 0) {
                 last_event_ns = now_ns();
                 wait_ms = 0;
+            } else if (links_backlogged_) {
+                wait_ms = 1;
             }
         }
         int n = epoll_wait(ep_, evs, 64, wait_ms);
@@ -655,8 +661,8 @@ void Daemon::send_tcp(int r, Msg &m) {
     if (r < 0 || r >= n_ || peer_fd_[r] < 0) {
         OCM_WARN("rank %d: no link to rank %d for %s", rank_, r, msg_type_str(m.type));
         // Bounce the request back as a local failure so the origin can answer the app.
-        if (m.status == MSG_REQUEST && (m.type == MSG_REQ_ALLOC || m.type == MSG_DO_ALLOC || m.type == MSG_DO_FREE ||
-                                        m.type == MSG_STATS)) {
+        if ((m.status & ~kMsgResent) == MSG_REQUEST &&
+            (m.type == MSG_REQ_ALLOC || m.type == MSG_DO_ALLOC || m.type == MSG_DO_FREE || m.type == MSG_STATS)) {
             Msg f = m;
             f.status = MSG_RESPONSE;
             f.err = EHOSTDOWN;
@@ -701,6 +707,7 @@ void Daemon::reap_overflowed_apps() {
 
 int Daemon::poll_links() {
     int n = 0;
+    links_backlogged_ = 0;
     link_pids_.clear();
     for (auto &kv : apps_)
         if (kv.second.link) link_pids_.push_back(kv.first);
@@ -722,6 +729,7 @@ int Daemon::poll_links() {
             w.rank = rank_;
             send_app(pid, w);
         }
+        if (!a.link_backlog.empty()) links_backlogged_++;
         Msg m;
         for (int i = 0; i < 64 && link->take_request(&m); i++) {
             m.pid = pid;  // the connection's SO_PEERCRED pid, never the record's

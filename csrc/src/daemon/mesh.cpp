@@ -45,7 +45,25 @@ uint64_t record_hash(const Msg &m) {
 constexpr size_t kMeshSeenMax = 8192;  // > every rank's unsent window (kTickRing records) together
 }  // namespace
 
-bool Daemon::mesh_duplicate(const Msg &m) {
+void Daemon::SeenWindow::add(uint64_t h) {
+    set.insert(h);
+    order.push_back(h);
+    if (order.size() > kMeshSeenMax) {
+        auto it = set.find(order.front());
+        if (it != set.end()) set.erase(it);
+        order.pop_front();
+    }
+}
+
+bool Daemon::SeenWindow::take(uint64_t h) {
+    auto it = set.find(h);
+    if (it == set.end()) return false;
+    set.erase(it);  // its entry in `order` ages out harmlessly
+    return true;
+}
+
+bool Daemon::mesh_duplicate(const Msg &m, bool via_tick, bool resent) {
+    if (!via_tick && !resent) return false;  // ordinary TCP and local traffic
     switch (m.type) {
     case MSG_REQ_ALLOC:
     case MSG_DO_ALLOC:
@@ -58,22 +76,22 @@ bool Daemon::mesh_duplicate(const Msg &m) {
         return false;
     }
     const uint64_t h = record_hash(m);
-    if (!mesh_seen_.insert(h).second) {
+    SeenWindow &mine = via_tick ? seen_tick_ : seen_resent_;
+    SeenWindow &other = via_tick ? seen_resent_ : seen_tick_;
+    if (other.take(h)) {
         mesh_dups_dropped_++;
         OCM_WARN("rank %d: dropping a second copy of %s/%s seq %llu from rank %d (tick fallback re-send)", rank_,
                  msg_type_str(m.type), msg_status_str(m.status), (unsigned long long)m.seq, m.src_rank);
         return true;
     }
-    mesh_seen_order_.push_back(h);
-    if (mesh_seen_order_.size() > kMeshSeenMax) {
-        mesh_seen_.erase(mesh_seen_order_.front());
-        mesh_seen_order_.pop_front();
-    }
+    mine.add(h);
     return false;
 }
 
-void Daemon::handle_mesh_msg(Msg &m, int from_fd) {
-    if (tick_ && mesh_duplicate(m)) return;
+void Daemon::handle_mesh_msg(Msg &m, int from_fd, bool via_tick) {
+    const bool resent = (m.status & kMsgResent) != 0;
+    m.status &= ~kMsgResent;
+    if (mesh_duplicate(m, via_tick, resent)) return;
     if (from_fd >= 0) {
         // An inbound link is anonymous until its HELLO carries a valid MAC.
         auto it = conns_.find(from_fd);
@@ -863,7 +881,7 @@ void Daemon::start_tick(const uint8_t *id, bool rccl) {
 
 void Daemon::on_tick() {
     if (!tick_) return;
-    for (Msg &m : tick_->drain()) handle_mesh_msg(m, -1);
+    for (Msg &m : tick_->drain()) handle_mesh_msg(m, -1, true);
     if (tick_->up() && tick_deadline_ms_) {
         tick_deadline_ms_ = 0;
         if (join_deferred_) join_now("tick transport up: the join is its first traffic");
@@ -887,7 +905,10 @@ void Daemon::leave_tick(const char *why) {
     if (!tick_) return;
     if (!tick_->failed()) tick_->abort();
     // send_rank: records to ourselves (OCM_TICK_SELF) go back to the local queue
-    for (TickRecord &rec : tick_->take_unsent()) send_rank(rec.dest, rec.msg);
+    for (TickRecord &rec : tick_->take_unsent()) {
+        rec.msg.status |= kMsgResent;  // the receiver compares it with what the ticks delivered
+        send_rank(rec.dest, rec.msg);
+    }
     tick_deadline_ms_ = 0;
     if (join_deferred_) join_now(why);
     if (tick_left_) return;

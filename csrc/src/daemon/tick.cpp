@@ -437,7 +437,11 @@ public:
         bytes_ = bytes;
         send_.assign(bytes, 0);
         const char *tf = std::getenv("OCM_TICK_FAULT");
-        fault_do_alloc_ = tf && std::strcmp(tf, "fail_after_do_alloc") == 0 && bytes == sizeof(TickSlot);
+        // fail_after_do_alloc / fail_after_do_free: see test()
+        if (tf && bytes == sizeof(TickSlot))
+            fault_type_ = std::strcmp(tf, "fail_after_do_alloc") == 0  ? MSG_DO_ALLOC
+                          : std::strcmp(tf, "fail_after_do_free") == 0 ? MSG_DO_FREE
+                                                                        : 0;
         // stall_after=N: from tick N on this rank stops taking part, without an error
         // (a wedged collective): the peers' watchdogs must end the transport.
         if (tf && std::strncmp(tf, "stall_after=", 12) == 0) stall_after_ = std::atoll(tf + 12);
@@ -530,15 +534,16 @@ public:
             error_ = "gathered tick slot failed its tag check";
             return -1;
         }
-        if (fault_do_alloc_ && !fault_fired_) {
-            // OCM_TICK_FAULT=fail_after_do_alloc (tests): the tick that carried one of
-            // our DO_ALLOC requests reached every peer, then fails here, so the
-            // fallback re-sends a record the owner already has.
+        if (fault_type_ && !fault_fired_) {
+            // OCM_TICK_FAULT=fail_after_do_alloc / fail_after_do_free (tests): the tick
+            // that carried one of our DO_ALLOC / DO_FREE requests reached every peer,
+            // then fails here, so the fallback re-sends a record the owner already has.
             const TickSlot *slot = reinterpret_cast<const TickSlot *>(send_.data());
             for (uint32_t r = 0; r < slot->count && r < (uint32_t)kTickMsgs; r++)
-                if (slot->rec[r].msg.type == MSG_DO_ALLOC && slot->rec[r].msg.status == MSG_REQUEST) {
+                if (slot->rec[r].msg.type == fault_type_ && slot->rec[r].msg.status == MSG_REQUEST) {
                     fault_fired_ = true;
-                    error_ = "injected failure after a DO_ALLOC tick (OCM_TICK_FAULT)";
+                    error_ = fault_type_ == MSG_DO_ALLOC ? "injected failure after a DO_ALLOC tick (OCM_TICK_FAULT)"
+                                                         : "injected failure after a DO_FREE tick (OCM_TICK_FAULT)";
                     abort();
                     return -1;
                 }
@@ -591,7 +596,8 @@ private:
     std::unique_ptr<TickRing> outbox_;  // OCM_TICK_SOCKET_SEAL
     uint64_t consumed_ = 0;
     std::atomic<bool> aborted_{false};
-    bool fault_do_alloc_ = false, fault_fired_ = false;
+    uint32_t fault_type_ = 0;  // OCM_TICK_FAULT=fail_after_do_alloc / _do_free: MSG_DO_ALLOC / MSG_DO_FREE
+    bool fault_fired_ = false;
     long long stall_after_ = 0;
     uint64_t started_ = 0;
     uint64_t ticks_ = 0;  // sealed emulation: ticks sealed so far

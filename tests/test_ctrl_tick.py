@@ -139,6 +139,46 @@ def test_tick_failure_after_do_alloc_does_not_duplicate_it(mesh_factory, sealed)
     assert logs.count("leaving the socket tick transport") == 3, logs  # the whole mesh left it together
 
 
+@pytest.mark.parametrize("sealed", ["0", "1"])
+def test_tick_failure_after_do_free_frees_once(mesh_factory, sealed):
+    """the fallback marks re-sent records (kMsgResent) and the receiver
+    compares only those with what the ticks delivered. Here the tick that carried
+    a DO_FREE reaches the owner, then fails, so the owner gets that DO_FREE twice;
+    it must free once, and allocations made afterwards (whose records may repeat
+    earlier ones byte for byte) must all be served."""
+    import time
+
+    m = mesh_factory(3, extra_args=["--ctrl", "socket"],
+                     env={"OCM_TICK_SOCKET_SEAL": sealed, "OCM_TICK_FAULT": "fail_after_do_free",
+                          "OCM_LEASE_BYTES": "0"})
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        _wait_tick_up(c, 3)
+        held = [c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20) for _ in range(4)]
+        for a in held:  # the first DO_FREE trips the fault; the rest ride TCP
+            a.free()
+        deadline = time.time() + 5
+        while sum(c.stats(r)["host_used"] for r in range(3)) and time.time() < deadline:
+            time.sleep(0.05)
+        assert all(c.stats(r)["host_used"] == 0 for r in range(3))
+        again = []
+        for i in range(6):
+            a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20)
+            a.fill(seed=80 + i)
+            a.put(0, 0, 1 << 20)
+            a.fill(seed=0)
+            a.get(0, 0, 1 << 20)
+            assert a.check(seed=80 + i) == 0
+            again.append(a)
+        used = sum(c.stats(r)["host_used"] for r in range(3))
+        assert used == 6 << 20, f"{used} bytes placed for 6 x 1 MiB"
+        for a in again:
+            a.free()
+    logs = m.logs()
+    assert "injected failure after a DO_FREE tick" in logs, logs
+    assert "dropping a second copy of MSG_DO_FREE" in logs, logs
+    assert "dropping a second copy of MSG_DO_ALLOC" not in logs, logs
+
+
 def test_socket_tick_self_loop(mesh_factory):
     # OCM_TICK_SELF routes a daemon's self-addressed records through the collective too.
     m = mesh_factory(1, extra_args=["--ctrl", "socket"], env={"OCM_TICK_SELF": "1"})

@@ -302,6 +302,20 @@ def test_connect_retries_while_the_mesh_joins_keep_the_link_in_step(monkeypatch,
         for _ in range(10):
             c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20).free()
         assert api.counters()["n_link_rpc"] - before >= 20
+        # every retried CONNECT replaced the app's entry without closing
+        # its pidfd; the daemon must hold exactly one pidfd for this app
+        pid0 = m0.daemons[0].proc.pid
+        pidfds = 0
+        for fd in os.listdir(f"/proc/{pid0}/fd"):
+            try:
+                if "pidfd" in os.readlink(f"/proc/{pid0}/fd/{fd}"):
+                    with open(f"/proc/{pid0}/fdinfo/{fd}") as f:
+                        pidfds += f"Pid:\t{os.getpid()}\n" in f.read()
+            except OSError:
+                pass
+        # one for the app, one for --watch-pid (Mesh makes its daemons watch this process);
+        # the old code held one more per retried CONNECT (52 here)
+        assert pidfds == 2, f"ocmd rank 0 holds {pidfds} pidfds on this process"
         c.__exit__(None, None, None)
     finally:
         m1.stop()
