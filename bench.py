@@ -289,12 +289,15 @@ def ctrl_extra(dist, world: int, rank: int, local_rank: int, use_gpu: bool, samp
 
     out = {}
     kind = api.OCM_REMOTE_GPU if use_gpu else api.OCM_REMOTE_RDMA
+    all_gpus = gather_obj(dist, local_rank, world) if use_gpu else []
     for ctrl in ("tcp", "rccl" if use_gpu else "socket"):
+        if ctrl == "rccl" and len(set(all_gpus)) < world:
+            # RCCL needs one rank per GPU: a one-GPU rehearsal (OCM_BENCH_SHARE_GPU) cannot build the communicator
+            out[ctrl] = {"skipped": "ranks share a GPU (RCCL needs one rank per GPU)"}
+            continue
         ports, key = gather_obj(dist, (free_ports(world), secrets.token_hex(16)) if rank == 0 else None, world)[0]
         ns = f"ctrl{ctrl}_{ports[0]}"
-        gpus = [local_rank if use_gpu else None for _ in range(world)]
-        if use_gpu:
-            gpus = gather_obj(dist, local_rank, world)
+        gpus = list(all_gpus) if use_gpu else [None] * world
         mesh = Mesh(world, gpus=gpus, ns=ns, policy="ring", ports=ports, ranks=[rank], key=key,
                     workdir=os.path.join("/tmp", f"ocm_{ns}"), extra_args=["--ctrl", ctrl],
                     env={"OCM_LEASE_BYTES": "0"})

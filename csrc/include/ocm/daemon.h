@@ -228,7 +228,7 @@ private:
     void return_idle_leases();
     int preferred_owner() const;
     bool cross_host(int a, int b) const;
-    void start_tick(const uint8_t *id, bool rccl);
+    void start_tick(const uint8_t *id, bool rccl, uint32_t idle_us);
     // Leave the tick transport (it failed here, a peer died, or a peer left it):
     // abort it, re-send over TCP every record it cannot prove delivered, and tell
     // the peers once (MSG_TICK_STOP) so the whole mesh leaves it together instead
@@ -247,6 +247,12 @@ private:
     bool join_deferred_ = false;        // our join waits for the transport decision / the tick
     long tick_deadline_ms_ = 0;         // bootstrap bound (0: none pending)
     int tick_up_ms_ = 20000;            // OCM_TICK_UP_MS
+    // Idle ticks (OCM_TICK_IDLE_US, default 1000; 0: the round-3 protocol, where an
+    // idle mesh stops and a rank starting a burst wakes its peers over TCP). rank0's
+    // value travels in MSG_TICK_START (pid field) so every rank runs the same ticks.
+    uint32_t tick_idle_us_ = 1000;
+    uint32_t *tick_bell_ = nullptr;     // the host-wide tick doorbell (shared memory), idle ticks only
+    uint64_t tcp_wakes_ = 0;            // MSG_TICK_WAKE records sent (TickStatsWire::tcp_wakes)
     void resolve_ctrl();                // rank0, at init
     void send_ctrl_decision(int r);     // rank0 -> rank r, once its link is up
     void join_now(const char *why);     // the deferred join, over whatever transport is up

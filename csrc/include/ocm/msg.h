@@ -132,6 +132,13 @@ struct TickStatsWire {
     uint64_t starts, start_sum_ns, start_max_ns;  // Collective::start calls and their host time
     uint32_t transport;       // ocm_daemon_stats.ctrl_transport
     uint32_t ticks_per_start; // > 1: ticks queued as captured graphs (OCM_TICK_GRAPH)
+    // Hop breakdown of the own records above (round 4): post -> the carrying tick
+    // queued (wait; 0 when a tick was already queued), its queueing -> completion seen
+    // by the tick thread (exec), and completion -> the event loop took the records
+    // (deliver, over every delivered batch, deliver_n of them).
+    uint64_t wait_sum_ns, exec_sum_ns, deliver_sum_ns, deliver_n;
+    uint64_t lazy_ticks;      // idle ticks (OCM_TICK_IDLE_US): the mesh keeps ticking, no TCP wake-ups
+    uint64_t tcp_wakes;       // MSG_TICK_WAKE records this daemon sent over TCP (0 with idle ticks)
 };
 
 // Topology of one daemon's GPU (hipExtGetLinkTypeAndHopCount to every other

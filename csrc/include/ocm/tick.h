@@ -124,8 +124,12 @@ void tick_slot_seal_tag(TickSlot *s, uint64_t tick);
 // tick completed still rides this one (OCM_TICK_SEAL_WAIT_US). `tick_ctr`
 // (device memory, graph-captured ticks): the seal numbers the tick itself,
 // *tick_ctr + 1, and stores that back; `tick` is then ignored.
+// `bell` / `bell_seen` (idle ticks, device pointers): the host-wide tick doorbell
+// and this stream's last view of it; the wait also ends when the bell moved (any
+// daemon of the host posted into the idle mesh), and the seal stores what it saw.
 hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, uint64_t tick, uint32_t wait_us,
-                            hipStream_t stream, uint64_t *tick_ctr = nullptr);
+                            hipStream_t stream, uint64_t *tick_ctr = nullptr, const uint32_t *bell = nullptr,
+                            uint32_t *bell_seen = nullptr);
 // Queue a one-lane kernel that stores `seq` to `flag` (pinned, device-mapped
 // host memory) at system scope: the host sees a tick end ~6 us sooner than
 // through an event query (tools/launch_probe.hip, profiles/launch_flag_r01.json).
@@ -151,6 +155,14 @@ public:
     virtual void *send_slot(int i) = 0;
     virtual const void *recv_slots(int i) = 0;
     virtual int start(int i) = 0;   // 0 ok
+    // Idle tick (OCM_TICK_IDLE_US): collectives that can wait on the device
+    // (device_idle_wait) queue a tick whose seal waits up to `wait_us` for a record
+    // of ours or a ring of the host-wide bell (set_bell); the others start at once
+    // (the tick thread has waited on the bell on the host already).
+    virtual bool device_idle_wait() const { return false; }
+    virtual int start_idle(int i, uint32_t wait_us) { return start(i); }
+    // The host-wide tick doorbell (a 32-bit word in shared, pinned-able memory).
+    virtual void set_bell(uint32_t *bell) {}
     virtual int test(int i) = 0;    // 1 done, 0 in flight, -1 failed
     virtual void abort() {}
     virtual const char *name() const = 0;
@@ -170,6 +182,13 @@ std::unique_ptr<Collective> make_socket_collective(const std::string &ns, int ra
 
 using CollectiveFactory = std::function<std::unique_ptr<Collective>(std::string *err, const std::atomic<bool> *cancel)>;
 
+// The host-wide tick doorbell of namespace `ns`: one page of POSIX shared memory
+// ("/ocm_<ns>_tickbell") every daemon of the host maps; word 0 is the bell (a
+// futex word). nullptr on failure. Close unmaps it and removes the name (the
+// daemons that still map it keep their mapping).
+uint32_t *tick_bell_open(const std::string &ns);
+void tick_bell_close(uint32_t *bell, const std::string &ns);
+
 class TickTransport {
 public:
     // The collective is created on the tick thread (its construction blocks
@@ -178,6 +197,15 @@ public:
     ~TickTransport();
     // CPUs the tick thread runs on (set before start(); empty: inherit the caller's).
     void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
+    // Idle ticks (set before start()): with `idle_us` > 0 an idle mesh keeps ticking,
+    // one tick per idle_us at most, instead of stopping and waking its peers over TCP
+    // (take_announce never fires). `bell`: the host-wide doorbell every daemon of the
+    // host rings (futex word, shared memory) when it posts into an idle mesh, so the
+    // idle tick ends at once on every rank; nullptr: idle ticks run their full length.
+    void set_idle(uint32_t idle_us, uint32_t *bell) {
+        idle_us_ = idle_us;
+        bell_ = bell;
+    }
     void start();
     void stop();
     void abort();          // a peer died: stop ticking, fall back to TCP
@@ -231,6 +259,15 @@ private:
     uint32_t per_start_ = 1;
     void flush_ring();
     uint64_t unsent() const;
+    void ring_bell();                        // bump the doorbell and wake its futex waiters
+    uint32_t idle_us_ = 0;
+    uint32_t *bell_ = nullptr;
+    std::atomic<bool> lazy_{false};          // the mesh is ticking idle: posts ring the bell
+    uint64_t lazy_ticks_ = 0;
+    // hop breakdown (TickStatsWire): per own record, post -> its tick queued / -> completion;
+    // per delivered batch, completion -> the event loop's drain
+    uint64_t wait_sum_ns_ = 0, exec_sum_ns_ = 0, deliver_sum_ns_ = 0, deliver_n_ = 0;
+    uint64_t ready_ns_ = 0;                  // when the undrained records were completed (under mu_)
     int efd_ = -1;
     std::vector<int> cpus_;
     // Host-filled collectives: records of issued ticks not yet completed here

@@ -152,9 +152,10 @@ hipError_t xfer_batch_graph_node(hipGraph_t graph, hipGraphNode_t dep, const Xfe
 // Roster (round 4): nothing guarantees that all `blocks` workgroups of the
 // launch are resident at once (other processes' kernels hold CUs; a queue can be
 // preempted). Completion must never wait for a workgroup that has not started:
-// a gang member's id is its check-in order (workgroup 0 is member 0, every other
-// workgroup takes a ticket from ServiceBox::checkin when it starts), workgroup 0
-// publishes the number of checked-in members as ServiceSlot::roster, and the host
+// a gang member's id is its check-in order (every workgroup takes a ticket from
+// ServiceBox::checkin when it starts; the first one is member 0, the lead called
+// workgroup 0 above), the lead publishes the number of checked-in members as
+// ServiceSlot::roster, and the host
 // sizes every gang to at most that roster, so each member a request names is
 // already running. A member that checks in later only gets requests posted after
 // it was counted. Workgroup 0 also takes its idle exit only once the last gang
@@ -199,13 +200,19 @@ struct alignas(128) ServiceSlot {
 static_assert(sizeof(ServiceSlot) == 256 + 8 * kServiceWgDoneMax, "service slot layout");
 
 constexpr int kServiceTraceWgs = 64;
-// Device-memory state of the gang (zeroed before every launch).
+// Device-memory state of the gang. Zeroed only at the first launch and after an
+// instance left with a request unfinished: a relaunch after a clean idle exit
+// reuses it as it is (the check-in counter and the gang counter keep growing,
+// the host passes the check-in base; a stale relayed record carries a seq below
+// the new instance's first, and `stop` names the instance that left).
 struct alignas(128) ServiceBox {
     unsigned long long rec[16];       // relayed request record (ServiceReq words), STOP as seq to leave
     unsigned long long cnt;           // gang completions, over all requests (only grows)
     unsigned long long pad1[15];
-    unsigned long long checkin;       // workgroups other than 0 that have started (member id = ticket + 1)
+    unsigned long long checkin;       // workgroups that have started, over every instance (id = ticket - base)
     unsigned long long pad2[15];
+    unsigned long long stop;          // first seq of the instance whose lead has left (its members leave too)
+    unsigned long long pad3[15];
     // OCM_SERVICE_PROTO bit 16 (TRACE): per workgroup, GPU clock (100 MHz) of its
     // last request: seen, copy start, copy drained, counted in / done published.
     unsigned long long trace[kServiceTraceWgs][4];
@@ -260,9 +267,11 @@ constexpr bool service_wg_done(unsigned proto, unsigned long long active) {
 // first_seq >= 1: the first request this instance serves. gang_req: the
 // GANGREC record (nullptr: gang requests are relayed by workgroup 0).
 // direct_wgs: with gang_req, workgroups 0..direct_wgs-1 poll it themselves.
+// checkin_base: ServiceBox::checkin when this instance starts (0 after a reset);
+// reset_box: zero the box first (stream-ordered memset).
 hipError_t service_launch(ServiceReq *req, ServiceReq *gang_req, ServiceSlot *slot, ServiceBox *box,
                           unsigned long long first_seq, unsigned long long idle_ticks, unsigned blocks, unsigned proto,
-                          unsigned direct_wgs, hipStream_t stream);
+                          unsigned direct_wgs, unsigned long long checkin_base, bool reset_box, hipStream_t stream);
 
 // Deterministic 32-bit word pattern (word i of a buffer) for data verification.
 hipError_t pattern_fill(void *p, uint64_t words, uint64_t first_word, uint32_t seed, hipStream_t stream);

@@ -261,6 +261,7 @@ void Daemon::app_tick_stats(Msg &m) {
     std::memset(&st, 0, sizeof(st));
     if (tick_) tick_->stats(&st);
     st.transport = my_config().ctrl;
+    st.tcp_wakes = tcp_wakes_;
     std::memcpy(r.u.raw, &st, sizeof(st));
     send_app(m.pid, r);
 }

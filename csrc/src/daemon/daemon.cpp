@@ -303,6 +303,7 @@ int Daemon::init() {
     }
     probe_links();
     if (const char *v = std::getenv("OCM_TICK_UP_MS"); v && *v) tick_up_ms_ = std::max(1, std::atoi(v));
+    if (const char *v = std::getenv("OCM_TICK_IDLE_US"); v && *v) tick_idle_us_ = (uint32_t)std::max(0, std::min(std::atoi(v), 20000));
     if (rank_ == 0) resolve_ctrl();
     // Join: report our configuration to rank0 (reference notify_rank0, src/main.c:143-160).
     // With a tick transport possible, a peer first waits for rank0's decision so that
@@ -333,7 +334,7 @@ void Daemon::check_ready() {
         if (cfg_.ctrl == "rccl" && rccl_unique_id(uid, &err) != 0)
             OCM_WARN("rccl control plane unavailable (%s); staying on TCP", err.c_str());
         else
-            start_tick(uid, cfg_.ctrl == "rccl");
+            start_tick(uid, cfg_.ctrl == "rccl", tick_idle_us_);
     }
     if (!cfg_.ready_file.empty()) {
         std::string tmp = cfg_.ready_file + ".tmp";
@@ -351,6 +352,10 @@ void Daemon::shutdown() {
     if (tick_) {
         tick_->stop();
         tick_.reset();
+    }
+    if (tick_bell_) {  // after the tick thread (and the collective that mapped it) is gone
+        tick_bell_close(tick_bell_, ns_);
+        tick_bell_ = nullptr;
     }
     if (data_) {
         data_->stop();

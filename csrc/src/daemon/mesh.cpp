@@ -186,7 +186,7 @@ void Daemon::handle_mesh_msg(Msg &m, int from_fd, bool via_tick) {
         break;
     case MSG_TICK_START:
         if (!tick_ && !tick_left_ && cfg_.ctrl != "tcp") {
-            start_tick(m.u.raw, m.seq == 1);
+            start_tick(m.u.raw, m.seq == 1, (uint32_t)std::max(0, m.pid));  // rank0's idle-tick setting
             if (!tick_ && join_deferred_) join_now("this rank cannot run the chosen tick transport");
         }
         break;
@@ -815,10 +815,11 @@ void Daemon::send_ctrl_decision(int r) {
     } else {
         t.type = MSG_TICK_START;
         t.seq = ctrl_mode_ == "rccl" ? 1 : 2;
+        t.pid = (int32_t)tick_idle_us_;  // every rank must run the same ticks: rank0's setting
         std::memcpy(t.u.raw, tick_uid_, sizeof(tick_uid_));
     }
     send_tcp(r, t);
-    if (t.type == MSG_TICK_START && !tick_) start_tick(tick_uid_, ctrl_mode_ == "rccl");
+    if (t.type == MSG_TICK_START && !tick_) start_tick(tick_uid_, ctrl_mode_ == "rccl", tick_idle_us_);
 }
 
 void Daemon::join_now(const char *why) {
@@ -841,8 +842,9 @@ void Daemon::check_tick_bootstrap() {
     }
 }
 
-void Daemon::start_tick(const uint8_t *id, bool rccl) {
+void Daemon::start_tick(const uint8_t *id, bool rccl, uint32_t idle_us) {
     if (tick_) return;
+    tick_idle_us_ = idle_us;
     CollectiveFactory f;
     if (rccl) {
         if (gpu_ < 0) {
@@ -874,9 +876,17 @@ void Daemon::start_tick(const uint8_t *id, bool rccl) {
         else if (mode != "loop")
             tick_->set_cpus(near_cpus_.empty() ? orig_cpus_ : near_cpus_);
     }
+    if (idle_us) {
+        // Idle ticks instead of TCP wake-ups; the doorbell is shared by the daemons of
+        // this host (a peer on another host simply waits out its idle tick).
+        if (!tick_bell_) tick_bell_ = tick_bell_open(ns_);
+        if (!tick_bell_) OCM_WARN("rank %d: no tick doorbell (shared memory); idle ticks run their full length", rank_);
+        tick_->set_idle(idle_us, tick_bell_);
+    }
     ep_add(tick_->event_fd(), EPOLLIN, tag(T_TICK, 0));
     tick_->start();
-    OCM_INFO("rank %d: control records will ride the %s tick transport", rank_, rccl ? "rccl" : "socket");
+    OCM_INFO("rank %d: control records will ride the %s tick transport (%s)", rank_, rccl ? "rccl" : "socket",
+             idle_us ? "idle ticks, no TCP wake-ups" : "idle mesh woken over TCP");
 }
 
 void Daemon::on_tick() {
@@ -896,7 +906,10 @@ void Daemon::on_tick() {
         w.rank = rank_;
         w.u.req.bytes = t;
         for (int r = 0; r < n_; r++)
-            if (r != rank_) send_tcp(r, w);
+            if (r != rank_) {
+                send_tcp(r, w);
+                tcp_wakes_++;
+            }
     }
     if (tick_->failed()) leave_tick("the collective failed here");
 }

@@ -7,15 +7,20 @@
 #include "ocm/affinity.h"
 
 #include <hip/hip_runtime_api.h>
+#include <linux/futex.h>
 #include <poll.h>
 #include <rccl/rccl.h>
+#include <fcntl.h>
 #include <sys/eventfd.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
+#include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <cerrno>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 
@@ -128,6 +133,8 @@ public:
         }
         if (out_) (void)hipHostFree(out_);
         if (done_) (void)hipHostFree(done_);
+        if (bell_seen_) (void)hipFree(bell_seen_);
+        if (bell_page_) (void)hipHostUnregister(bell_page_);
         if (consumed_) (void)hipFree(consumed_);
         if (stream2_) (void)hipStreamDestroy(stream2_);
         if (stream_) (void)hipStreamDestroy(stream_);
@@ -302,6 +309,31 @@ public:
         return 0;
     }
     void request_abort() { abort_req_ = true; }
+    // Idle ticks wait on the device: the seal polls our ring and the host-wide bell.
+    bool device_idle_wait() const override { return sealed_ && !graph_k_ && nstreams_ == 1 && bell_dev_; }
+    void set_bell(uint32_t *bell) override {
+        if (!bell || bell_dev_) return;
+        (void)hipSetDevice(gpu_);
+        // the bell's page, shared by every daemon of the host, mapped for this GPU
+        void *page = reinterpret_cast<void *>(reinterpret_cast<uintptr_t>(bell) & ~(uintptr_t)4095);
+        if (hipHostRegister(page, 4096, hipHostRegisterMapped) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void **>(&bell_dev_), bell, 0) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&bell_seen_), sizeof(uint32_t)) != hipSuccess ||
+            hipMemset(bell_seen_, 0, sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            OCM_WARN("rccl idle ticks: the tick doorbell cannot be mapped for gpu %d; idle ticks wait on the host", gpu_);
+            bell_dev_ = nullptr;
+            return;
+        }
+        bell_page_ = page;
+    }
+    int start_idle(int i, uint32_t wait_us) override {
+        if (!device_idle_wait()) return start(i);
+        idle_next_ = wait_us;
+        const int rc = start(i);
+        idle_next_ = 0;
+        return rc;
+    }
     int depth() const override { return graph_k_ ? 2 * graph_k_ : plain_depth_; }
     int ticks_per_start() const override { return graph_k_ ? graph_k_ : 1; }
     int tick_quantum() const override { return quantum_; }
@@ -331,7 +363,9 @@ public:
                 if (hipStreamWaitEvent(st, prev.sealed, 0) != hipSuccess) return why("seal ordering");
             }
             const hipError_t e =
-                tick_seal_launch(out_dev_, consumed_, static_cast<TickSlot *>(sl.dsend), seq, wait_us_, st);
+                idle_next_ ? tick_seal_launch(out_dev_, consumed_, static_cast<TickSlot *>(sl.dsend), seq, idle_next_,
+                                              st, nullptr, bell_dev_, bell_seen_)
+                           : tick_seal_launch(out_dev_, consumed_, static_cast<TickSlot *>(sl.dsend), seq, wait_us_, st);
             if (e != hipSuccess) return why(std::string("seal launch: ") + hipGetErrorString(e));
             if (nstreams_ == 2 && hipEventRecord(sl.sealed, st) != hipSuccess) return why("seal event");
         } else if (!mapped_ && hipMemcpyAsync(sl.dsend, sl.hsend, bytes_, hipMemcpyHostToDevice, st) != hipSuccess) {
@@ -413,6 +447,10 @@ private:
     int quantum_ = 1;                      // the configured K, kept if capturing fails
     hipGraphExec_t gexec_[2] = {nullptr, nullptr};
     uint64_t *tick_ctr_ = nullptr;            // graph ticks: the last tick number a seal took (HBM)
+    uint32_t *bell_dev_ = nullptr;            // idle ticks: the host-wide doorbell, device view
+    uint32_t *bell_seen_ = nullptr;           // the bell value the last idle seal saw (HBM)
+    void *bell_page_ = nullptr;               // registered page of the bell
+    uint32_t idle_next_ = 0;                  // start(): this tick is idle, its seal waits up to this long
     std::atomic<bool> abort_req_{false};
     bool aborted_ = false;
 };
@@ -607,6 +645,25 @@ private:
 
 }  // namespace
 
+uint32_t *tick_bell_open(const std::string &ns) {
+    const std::string name = "/ocm_" + ns + "_tickbell";
+    const int fd = shm_open(name.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0600);
+    if (fd < 0) return nullptr;
+    if (ftruncate(fd, 4096) != 0) {
+        close(fd);
+        return nullptr;
+    }
+    void *p = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    return p == MAP_FAILED ? nullptr : static_cast<uint32_t *>(p);
+}
+
+void tick_bell_close(uint32_t *bell, const std::string &ns) {
+    if (!bell) return;
+    munmap(bell, 4096);
+    (void)shm_unlink(("/ocm_" + ns + "_tickbell").c_str());
+}
+
 int rccl_unique_id(uint8_t out[128], std::string *err) {
     ncclUniqueId id;
     ncclResult_t r = ncclGetUniqueId(&id);
@@ -683,6 +740,19 @@ void TickTransport::stats(TickStatsWire *out) {
     out->start_sum_ns = start_sum_ns_;
     out->start_max_ns = start_max_ns_;
     out->ticks_per_start = per_start_;
+    out->wait_sum_ns = wait_sum_ns_;
+    out->exec_sum_ns = exec_sum_ns_;
+    out->deliver_sum_ns = deliver_sum_ns_;
+    out->deliver_n = deliver_n_;
+    out->lazy_ticks = lazy_ticks_;
+}
+
+// Bump the host-wide doorbell and wake every tick thread sleeping on it (idle ticks).
+void TickTransport::ring_bell() {
+    if (!bell_) return;
+    __atomic_fetch_add(bell_, 1u, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
+    (void)syscall(SYS_futex, bell_, FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
 }
 
 void TickTransport::stop() {
@@ -730,6 +800,9 @@ bool TickTransport::post(int dest, const Msg &m) {
         flush_ring();
     }
     cv_.notify_all();
+    // An idle mesh: every rank's idle tick ends when the bell moves (their seals and
+    // tick threads watch it), so this record leaves now instead of at the end of it.
+    if (lazy_.load()) ring_bell();
     return true;
 }
 
@@ -766,6 +839,11 @@ std::vector<Msg> TickTransport::drain() {
     std::vector<Msg> out;
     out.swap(in_);
     in_ready_.store(false, std::memory_order_relaxed);
+    if (!out.empty() && ready_ns_) {
+        deliver_sum_ns_ += mono_now_ns() - ready_ns_;
+        deliver_n_++;
+        ready_ns_ = 0;
+    }
     return out;
 }
 
@@ -824,11 +902,17 @@ void TickTransport::run() {
         signal();
         return;
     }
+    if (idle_us_ && bell_) c->set_bell(bell_);
     {
         std::lock_guard<std::mutex> lk(mu_);
         coll_ = std::move(c);
     }
     Collective *coll = coll_.get();
+    // Idle ticks: the seal waits on the GPU (RCCL), or this thread waits on the
+    // bell before starting the tick (the socket ring, graph-captured ticks).
+    const bool dev_idle = idle_us_ && coll->device_idle_wait();
+    uint64_t idle_tick = 0;     // number of the idle tick in flight (0: none)
+    uint32_t idle_bell = 0;     // the bell when it was queued
     const uint64_t depth = (uint64_t)std::max(1, coll->depth());
     // Ticks are queued `per` at a time (a captured graph of `per` ticks); every
     // rank rounds its target up to the same multiple of `quantum`.
@@ -871,7 +955,36 @@ void TickTransport::run() {
     while (!stop_) {
         {
             std::unique_lock<std::mutex> lk(mu_);
-            if (done == issued && issued >= target) {
+            bool idle_now = false;
+            if (done == issued && issued >= target && idle_us_) {
+                // Idle mesh, idle ticks: every rank issues the next tick anyway (each
+                // decides from the same gathered ticks), so nobody needs waking over
+                // TCP. Its seal (or this thread, below) waits up to idle_us for a
+                // record of ours or the host-wide bell.
+                lazy_ = true;
+                if (unsent() > 0) ring_bell();  // posted before lazy_ was set: tell the peers
+                if (!dev_idle) {
+                    const uint64_t t_end = mono_ns() + (uint64_t)idle_us_ * 1000ull;
+                    const uint32_t b0 = bell_ ? __atomic_load_n(bell_, __ATOMIC_ACQUIRE) : 0u;
+                    while (!stop_ && unsent() == 0 && (!bell_ || __atomic_load_n(bell_, __ATOMIC_ACQUIRE) == b0)) {
+                        const uint64_t now = mono_ns();
+                        if (now >= t_end) break;
+                        const uint64_t left = t_end - now;
+                        if (bell_) {
+                            lk.unlock();
+                            struct timespec ts = {(time_t)(left / 1000000000ull), (long)(left % 1000000000ull)};
+                            (void)syscall(SYS_futex, bell_, FUTEX_WAIT, b0, &ts, nullptr, 0);
+                            lk.lock();
+                        } else {
+                            cv_.wait_for(lk, std::chrono::nanoseconds(left));
+                        }
+                    }
+                    if (stop_) break;
+                }
+                target = issued + 1;
+                idle_now = true;
+                lazy_ticks_++;
+            } else if (done == issued && issued >= target) {
                 // Idle: sleep until there is something to send or a peer calls a tick.
                 cv_.wait(lk, [&] { return stop_.load() || unsent() > 0 || wake_upto_.load() > target; });
                 if (stop_) break;
@@ -902,9 +1015,15 @@ void TickTransport::run() {
                     slot->busy = out_.empty() ? 0 : 1;
                 }
                 if (announce_.load()) signal();  // let the event loop wake the peers first
+                const bool idle_start = idle_now && dev_idle;
+                if (idle_start) {
+                    idle_tick = issued + 1;
+                    idle_bell = bell_ ? __atomic_load_n(bell_, __ATOMIC_ACQUIRE) : 0u;
+                }
+                idle_now = false;  // only the first tick queued from idle
                 lk.unlock();
                 const uint64_t t0 = mono_ns();
-                const int rc = coll->start(i);
+                const int rc = idle_start ? coll->start_idle(i, idle_us_) : coll->start(i);
                 const uint64_t t1 = mono_ns();
                 lk.lock();
                 if (rc != 0) break;
@@ -935,6 +1054,22 @@ void TickTransport::run() {
                 break;
             }
             if (issued - done + per <= depth && (spins & 15) == 15) break;
+            // An idle tick in flight, nothing of ours to send and the bell silent: it
+            // runs up to idle_us on the GPU, so sleep on the bell (a post anywhere on
+            // the host wakes us) instead of spinning a core for it.
+            if (idle_tick == done + 1 && bell_ && __atomic_load_n(bell_, __ATOMIC_ACQUIRE) == idle_bell &&
+                !in_ready_.load(std::memory_order_relaxed)) {
+                bool quiet;
+                {
+                    std::lock_guard<std::mutex> lk(mu_);
+                    quiet = unsent() == 0;
+                }
+                if (quiet) {
+                    // a ring wakes us at once; otherwise look at the tick a few times per idle period
+                    struct timespec ts = {0, (long)std::max<uint32_t>(50, idle_us_ / 4) * 1000};
+                    (void)syscall(SYS_futex, bell_, FUTEX_WAIT, idle_bell, &ts, nullptr, 0);
+                }
+            }
         }
         if (t < 0) {
             if (timed_out_ && !stop_)
@@ -954,11 +1089,15 @@ void TickTransport::run() {
                 const TickSlot &mine = got[rank_];
                 {
                     const uint64_t t = mono_now_ns();
+                    const uint64_t q = issued_at[(size_t)i];
                     for (uint32_t r = 0; r < std::min<uint32_t>(mine.count, kTickMsgs); r++) {
-                        const uint64_t d = t - post_ns_[(mine.first + r) & (kTickRing - 1)];
+                        const uint64_t p = post_ns_[(mine.first + r) & (kTickRing - 1)];
+                        const uint64_t d = t - p;
                         lat_sum_ns_ += d;
                         lat_n_++;
                         lat_max_ns_ = std::max(lat_max_ns_, d);
+                        wait_sum_ns_ += q > p ? q - p : 0;  // no tick was queued when it was posted
+                        exec_sum_ns_ += t - std::max(p, q);
                     }
                     if (last_done_ns_) {
                         period_sum_ns_ += t - last_done_ns_;
@@ -970,13 +1109,17 @@ void TickTransport::run() {
                 flush_ring();
             } else if (!inflight_n_.empty()) {
                 const uint64_t t = mono_now_ns();
+                const uint64_t q = issued_at[(size_t)i];
                 for (uint32_t r = 0; r < inflight_n_.front() && !inflight_.empty(); r++) {
                     inflight_.pop_front();
-                    const uint64_t d = t - inflight_ns_.front();  // host-filled: post -> this tick completed here
+                    const uint64_t p = inflight_ns_.front();
+                    const uint64_t d = t - p;  // host-filled: post -> this tick completed here
                     inflight_ns_.pop_front();
                     lat_sum_ns_ += d;
                     lat_n_++;
                     lat_max_ns_ = std::max(lat_max_ns_, d);
+                    wait_sum_ns_ += q > p ? q - p : 0;
+                    exec_sum_ns_ += t - std::max(p, q);
                 }
                 inflight_n_.pop_front();
             }
@@ -989,11 +1132,18 @@ void TickTransport::run() {
                         delivered++;
                     }
             }
-            if (delivered) in_ready_.store(true, std::memory_order_release);
+            if (delivered) {
+                if (!ready_ns_) ready_ns_ = mono_now_ns();
+                in_ready_.store(true, std::memory_order_release);
+            }
         }
         done++;
         ticks_ = done;
-        if (traffic) target = std::max(target, done + kBusyTicks);
+        if (idle_tick && done >= idle_tick) idle_tick = 0;
+        if (traffic) {
+            target = std::max(target, done + kBusyTicks);
+            lazy_ = false;  // a burst: ticks run back to back, posts need no bell
+        }
         if (delivered) signal();
     }
 }

@@ -78,7 +78,8 @@ __global__ __launch_bounds__(64) void tick_seal2_kernel(const TickRing *ring, ui
 // number is the device counter + 1, stored back by the seal (seals run in
 // stream order, one at a time).
 __global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uint64_t *consumed, TickSlot *slot,
-                                                      uint64_t tick, uint64_t wait, uint64_t *ctr) {
+                                                      uint64_t tick, uint64_t wait, uint64_t *ctr, const uint32_t *bell,
+                                                      uint32_t *bell_seen) {
     const int lane = threadIdx.x;
     // Seals run one at a time (one stream, or two alternating streams ordered by an
     // event), but possibly on different queues: agent-scope (sc1) load and store.
@@ -88,19 +89,26 @@ __global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uin
     const uint64_t j = c + (uint64_t)lane;
     const uint64_t *src = reinterpret_cast<const uint64_t *>(&ring->rec[j & (kTickRing - 1)]);
     const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + wait;
+    // Idle ticks: the host-wide doorbell, read in the same round trip as the ring.
+    const uint32_t seen = bell ? __hip_atomic_load(bell_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    uint32_t rung = seen;
     for (;;) {
         uint64_t pub_l = 0;
+        uint32_t bell_l = 0;
         if (lane < kTickMsgs) {
 #pragma unroll
             for (int k = 0; k < kTickRecordWords; k++) w[k] = sys_load(src + k);
             tag = sys_load(&ring->tag[j & (kTickRing - 1)]);
         }
         if (lane == 63) pub_l = sys_load(&ring->published);
+        if (lane == 62 && bell) bell_l = __hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         pub = ((uint64_t)__builtin_amdgcn_readlane((int)(pub_l >> 32), 63) << 32) |
               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pub_l, 63);
-        // Uniform exit: pub is read-lane broadcast and the clock is scalar.
-        if (pub > c || wait == 0 || (int64_t)(__builtin_amdgcn_s_memrealtime() - t_end) >= 0) break;
+        if (bell) rung = (uint32_t)__builtin_amdgcn_readlane((int)bell_l, 62);
+        // Uniform exit: pub and the bell are read-lane broadcasts and the clock is scalar.
+        if (pub > c || wait == 0 || rung != seen || (int64_t)(__builtin_amdgcn_s_memrealtime() - t_end) >= 0) break;
     }
+    if (bell && lane == 0) __hip_atomic_store(bell_seen, rung, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t pending = pub > c ? pub - c : 0;
     const uint32_t n = pending < (uint64_t)kTickMsgs ? (uint32_t)pending : (uint32_t)kTickMsgs;
     const bool mine = (uint32_t)lane < n;
@@ -145,15 +153,18 @@ hipError_t tick_done_launch(uint64_t *flag, uint64_t seq, hipStream_t stream) {
 }
 
 hipError_t tick_seal_launch(const TickRing *ring, uint64_t *consumed, TickSlot *slot, uint64_t tick, uint32_t wait_us,
-                            hipStream_t stream, uint64_t *tick_ctr) {
+                            hipStream_t stream, uint64_t *tick_ctr, const uint32_t *bell, uint32_t *bell_seen) {
     (void)hipGetLastError();  // report this launch, not an earlier call's error
     static const bool spec = [] {
         const char *v = std::getenv("OCM_TICK_SEAL_SPEC");
         return !(v && std::strcmp(v, "0") == 0);
     }();
-    const uint64_t wait = (uint64_t)std::min<uint32_t>(wait_us, 1000) * 100;  // s_memrealtime: 100 MHz
-    if (spec)
-        hipLaunchKernelGGL(tick_seal_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot, tick, wait, tick_ctr);
+    // s_memrealtime: 100 MHz; idle ticks wait up to 20 ms, busy ones a few us
+    const uint64_t wait = (uint64_t)std::min<uint32_t>(wait_us, 20000) * 100;
+    if (!bell_seen) bell = nullptr;
+    if (spec || bell)
+        hipLaunchKernelGGL(tick_seal_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot, tick, wait, tick_ctr,
+                           bell, bell_seen);
     else
         hipLaunchKernelGGL(tick_seal2_kernel, dim3(1), dim3(64), 0, stream, ring, consumed, slot, tick, tick_ctr);
     return hipGetLastError();

@@ -805,24 +805,30 @@ __device__ __forceinline__ bool service_last_complete(ServiceSlot *slot, Service
 // relays only gangs wider than direct_wgs to the others. 16 direct pollers
 // cost small ops nothing measurable; 32 cost them ~1 us
 // (profiles/svc_direct_gang_ab_r02.json).
-// Members are numbered in check-in order and workgroup 0 publishes how many
-// have checked in (the roster, see ocm/xfer.h): lane 32 of its poll reads the
+// Members are numbered in check-in order; member 0 (the first workgroup to
+// start) is "workgroup 0" of the protocol above and publishes how many have
+// checked in (the roster, see ocm/xfer.h): lane 32 of its poll reads the
 // check-in counter until the whole grid is in.
 __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq, const ServiceReq *grq,
                                                            ServiceSlot *slot, ServiceBox *box,
                                                            unsigned long long first_seq,
                                                            unsigned long long idle_ticks, unsigned proto,
-                                                           unsigned direct_wgs) {
+                                                           unsigned direct_wgs, unsigned long long checkin_base) {
     __shared__ __attribute__((aligned(16))) unsigned long long sh[16];
     __shared__ unsigned sh_id;
     const int tid = threadIdx.x;
-    const bool lead = blockIdx.x == 0;
+    // Member ids in check-in order. The first workgroup to start is workgroup 0 of
+    // the protocol (the lead), whichever block it is: the dispatcher spreads blocks
+    // over the XCDs, and block 0's XCD may have no room while others do (measured
+    // under tests/test_gpu_service.py's CU hog: block 0 waited for the hog to end).
+    // The counter only grows across instances (the box is not cleared between
+    // launches): tickets of this instance start at checkin_base.
     if (tid == 0)
-        sh_id = lead ? 0u
-                     : 1u + (unsigned)__hip_atomic_fetch_add(&box->checkin, 1ull, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT);
+        sh_id = (unsigned)(__hip_atomic_fetch_add(&box->checkin, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                           checkin_base);
     __syncthreads();
     const unsigned id = __builtin_amdgcn_readfirstlane(sh_id);  // this workgroup's member id
+    const bool lead = id == 0;
     const bool direct = grq != nullptr && id < direct_wgs;  // polls the host gang record itself
     const unsigned long long relay_above = grq != nullptr ? direct_wgs : 1;  // gangs wider than this are relayed
     const unsigned long long *req = reinterpret_cast<const unsigned long long *>(
@@ -832,6 +838,12 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
     unsigned long long last_gang = 0;          // gang word of request `last` (workgroup 0's idle-exit test)
     unsigned long long roster = 0;             // members published so far (workgroup 0)
     unsigned long long idle_start = __builtin_amdgcn_s_memrealtime();
+    // The host launches an instance only for a request it is about to post, and it
+    // may first wait for the roster: no idle exit before the first request (with a
+    // 1 us idle window the lead left before every post, and host and kernel
+    // relaunched each other until the op timed out), unless none comes in 20 ms.
+    const unsigned long long started = idle_start;
+    bool served = false;
     unsigned long long ticks_sum =
         lead ? __hip_atomic_load(&slot->gpu_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
     for (;;) {
@@ -847,12 +859,12 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                                          : __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 else if (direct && lead && tid < 32)
                     w = __hip_atomic_load(greq + (tid - 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                else if (direct && !lead && tid == 16)
-                    w = __hip_atomic_load(&box->rec[15], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // lead's STOP
+                else if (!lead && tid == 16)
+                    w = __hip_atomic_load(&box->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the lead left
                 else if (count && tid == 32)
                     w = __hip_atomic_load(&box->checkin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (count) {
-                    const unsigned long long r = 1 + readlane64(w, 32);
+                    const unsigned long long r = readlane64(w, 32) - checkin_base;  // check-ins, the lead's included
                     if (r > roster) {  // members counted here are running: requests may name them
                         if (tid == 0) __hip_atomic_store(&slot->roster, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         roster = r;
@@ -860,13 +872,17 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                 }
                 base = 0;
                 s = readlane64(w, 15);
-                if (direct) {
-                    const unsigned long long s2 = readlane64(w, 31 - 15 * (int)!lead);  // gang seq / box STOP
-                    if (s2 == kServiceStop) {  // the host parked it / workgroup 0 left
+                if (!lead && readlane64(w, 16) == first_seq) {  // the lead of THIS instance left
+                    s = kServiceStop;
+                    break;
+                }
+                if (direct && lead) {
+                    const unsigned long long s2 = readlane64(w, 31);  // the gang record's seq
+                    if (s2 == kServiceStop) {  // the host parked it
                         s = kServiceStop;
                         break;
                     }
-                    if (lead && s2 > last && s2 != 0) {
+                    if (s2 > last && s2 != 0) {
                         s = s2;  // the host posts one request at a time: at most one record is new
                         base = 16;
                     }
@@ -879,7 +895,8 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                     if (h == readlane64(w, base + 14)) break;
                     continue;  // seq landed before the rest of the record: read it again
                 }
-                if (lead && __builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks) {
+                if (lead && __builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks &&
+                    (served || __builtin_amdgcn_s_memrealtime() - started > 2000000ull)) {
                     // Leave only once every member the last request named is done
                     // with it: a member that saw the STOP first would never serve it.
                     if (service_last_complete(slot, box, proto, last, last_gang)) {
@@ -915,6 +932,7 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
         service_serve(sh, s, slot, box, proto, id);
         last = s;
         last_gang = sh[1];
+        served = true;
         idle_start = __builtin_amdgcn_s_memrealtime();  // every lane: the idle test must stay wave-uniform
         if (lead) {
             // Diagnostic, after `done` so it never delays it: a running sum in a
@@ -925,8 +943,9 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
         __syncthreads();  // sh is rewritten by the next poll
     }
     if (lead && tid == 0) {
-        // Every member leaves on this seq (a STOP in the relayed record).
-        __hip_atomic_store(&box->rec[15], kServiceStop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // Every member leaves when it sees this instance's first seq here (an
+        // earlier instance's value never matches, so the box needs no clearing).
+        __hip_atomic_store(&box->stop, first_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&slot->exited, last + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -962,13 +981,15 @@ void service_store_seq(ServiceReq *req, unsigned long long seq) {
 
 hipError_t service_launch(ServiceReq *req, ServiceReq *gang_req, ServiceSlot *slot, ServiceBox *box,
                           unsigned long long first_seq, unsigned long long idle_ticks, unsigned blocks, unsigned proto,
-                          unsigned direct_wgs, hipStream_t stream) {
+                          unsigned direct_wgs, unsigned long long checkin_base, bool reset_box, hipStream_t stream) {
     if (!req || !slot || !box || blocks == 0 || first_seq == 0 || (gang_req && direct_wgs == 0))
         return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(box, 0, sizeof(ServiceBox), stream);
-    if (e != hipSuccess) return e;
+    if (reset_box) {
+        hipError_t e = hipMemsetAsync(box, 0, sizeof(ServiceBox), stream);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(service_kernel, dim3(blocks), dim3(kThreads), 0, stream, req, gang_req, slot, box, first_seq,
-                       idle_ticks, proto, direct_wgs);
+                       idle_ticks, proto, direct_wgs, checkin_base);
     return hipGetLastError();
 }
 // ---- verification patterns (benchmarks and tests check data without a host round trip) ----

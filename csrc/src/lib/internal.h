@@ -256,6 +256,12 @@ struct State {
     // after a launch a gang op waits up to svc_roster_wait_ns for the grid to check
     // in before it settles for fewer members (OCM_SERVICE_ROSTER_WAIT_US).
     uint64_t svc_launch_ns = 0;
+    // The gang's device box is zeroed only when it must be (ocm/xfer.h): at the
+    // first launch, after an instance left a request unfinished, or always with
+    // OCM_SERVICE_BOX_RESET=1. Otherwise the next instance's check-in tickets start
+    // at svc_checkins (every workgroup of every drained instance took one).
+    bool svc_box_dirty = true, svc_box_reset_always = false;
+    unsigned long long svc_checkins = 0;
     uint64_t svc_roster_wait_ns = 200000;
     // Health counters (ocm_x_service_health): gang ops sized below the width they
     // wanted because fewer members were resident, instances that left with the

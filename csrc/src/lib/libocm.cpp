@@ -147,6 +147,7 @@ int ocm_init(void) {
     s.svc_roster_wait_ns = 1000ull * (unsigned long long)std::max(0, env_int("OCM_SERVICE_ROSTER_WAIT_US", 200));
     s.svc_timeout_ns = 1000000ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_TIMEOUT_MS", 10000));
     s.svc_drain_ns = 1000000ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_DRAIN_MS", 10000));
+    s.svc_box_reset_always = env_int("OCM_SERVICE_BOX_RESET", 0) != 0;
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");
     s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
     s.tuning = xfer_tuning_from_env();
@@ -915,10 +916,12 @@ void ocm_x_quiesce(void) {
     service_park();
 }
 
-// The local daemon's tick control transport statistics (TickStatsWire as 10
+// The local daemon's tick control transport statistics (TickStatsWire as 16
 // words: ticks, own records, latency sum / max ns, periods, period sum ns,
-// start() calls, their sum / max ns, transport | ticks_per_start << 32).
-int ocm_x_tick_stats(uint64_t out[10]) {
+// start() calls, their sum / max ns, transport | ticks_per_start << 32, then the
+// hop breakdown: wait sum ns, exec sum ns, deliver sum ns, deliveries, idle ticks,
+// TCP wake-ups sent).
+int ocm_x_tick_stats(uint64_t out[16]) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (!s.inited || !out) return -1;
@@ -927,9 +930,11 @@ int ocm_x_tick_stats(uint64_t out[10]) {
     if (rpc(m, &r, s.rpc_timeout_ms) != 0) return -1;
     TickStatsWire st;
     std::memcpy(&st, r.u.raw, sizeof(st));
-    const uint64_t v[10] = {st.ticks, st.own_records, st.lat_sum_ns, st.lat_max_ns, st.periods, st.period_sum_ns,
+    const uint64_t v[16] = {st.ticks, st.own_records, st.lat_sum_ns, st.lat_max_ns, st.periods, st.period_sum_ns,
                             st.starts, st.start_sum_ns, st.start_max_ns,
-                            (uint64_t)st.transport | ((uint64_t)st.ticks_per_start << 32)};
+                            (uint64_t)st.transport | ((uint64_t)st.ticks_per_start << 32),
+                            st.wait_sum_ns, st.exec_sum_ns, st.deliver_sum_ns, st.deliver_n, st.lazy_ticks,
+                            st.tcp_wakes};
     std::memcpy(out, v, sizeof(v));
     return 0;
 }

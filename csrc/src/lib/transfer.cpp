@@ -193,13 +193,19 @@ int service_start(unsigned long long first_seq) {
     __atomic_store_n(&s.svc->roster, 0ull, __ATOMIC_RELEASE);  // the new lead publishes its own
     service_store_seq(s.svc_req, 0ull);  // clear a STOP left by a parked instance
     if (s.svc_greq) service_store_seq(s.svc_greq, 0ull);
-    s.svc_gang_total = 0;  // the launch zeroes the device counter
+    const bool reset = s.svc_box_dirty || s.svc_box_reset_always;
+    if (reset) {
+        s.svc_gang_total = 0;  // the launch zeroes the device counters
+        s.svc_checkins = 0;
+    }
     if (service_launch(s.svc_req, s.svc_greq, s.svc, s.svc_box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_proto,
-                       std::min(s.svc_direct, s.svc_blocks), s.svc_stream) != hipSuccess) {
+                       std::min(s.svc_direct, s.svc_blocks), s.svc_checkins, reset, s.svc_stream) != hipSuccess) {
         (void)hipGetLastError();
         s.svc_max = 0;
         OCM_FAIL(-1, "copy service launch failed");
     }
+    s.svc_box_dirty = false;
+    s.svc_checkins += s.svc_blocks;  // every workgroup takes one ticket before the instance drains
     s.svc_running = true;
     s.svc_launch_ns = now_ns();
     return 0;
@@ -292,6 +298,7 @@ static int service_abort(unsigned long long seq, unsigned long long active, cons
     }
     (void)hipGetLastError();
     s.svc_running = false;
+    s.svc_box_dirty = true;
     OCM_FAIL(-1, "copy service %s (seq %llu, %llu members, %llu done words, roster %llu, exited %llu); drained",
              why, seq, active, wg_in, roster, ex);
 }
@@ -374,6 +381,8 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
                     return 0;
                 }
                 if (ex > seq) s.svc_incomplete_exits++;
+                // Members may have counted part of the request in: start from a clean box.
+                s.svc_box_dirty = true;
                 // Re-post under a fresh seq. Direct gang members of the instance that
                 // left may have served part of this request and stored its seq in their
                 // WGDONE words; under the old seq those stale words would count as the

@@ -396,17 +396,24 @@ def service_health() -> dict:
 def tick_stats() -> dict | None:
     """The local daemon's tick control transport (RCCL or socket collective):
     ticks completed, this rank's own records from post to delivery (mean / max
-    microseconds), the mean gap between completed ticks, and the host time per
-    Collective::start. None when the call fails; zeros on a TCP-only daemon."""
-    out = (ctypes.c_uint64 * 10)()
+    microseconds) and that hop split into its stages, the mean gap between
+    completed ticks, the host time per Collective::start, idle ticks run and TCP
+    wake-ups sent. None when the call fails; zeros on a TCP-only daemon."""
+    out = (ctypes.c_uint64 * 16)()
     if load().ocm_x_tick_stats(out) != 0:
         return None
-    n, p, k = int(out[1]), int(out[4]), int(out[6])
+    n, p, k, d = int(out[1]), int(out[4]), int(out[6]), int(out[13])
     return {"ticks": int(out[0]), "own_records": n,
             "hop_mean_us": round(out[2] / n / 1e3, 2) if n else None, "hop_max_us": round(out[3] / 1e3, 1),
+            # the hop, split: post -> its tick queued (0 when one was already queued),
+            # queued -> completion seen by the tick thread, completion -> the event loop took it
+            "hop_wait_mean_us": round(out[10] / n / 1e3, 2) if n else None,
+            "hop_exec_mean_us": round(out[11] / n / 1e3, 2) if n else None,
+            "deliver_mean_us": round(out[12] / d / 1e3, 2) if d else None,
             "tick_period_mean_us": round(out[5] / p / 1e3, 2) if p else None,
             "start_mean_us": round(out[7] / k / 1e3, 2) if k else None, "start_max_us": round(out[8] / 1e3, 1),
-            "transport": int(out[9] & 0xFFFFFFFF), "ticks_per_start": int(out[9] >> 32)}
+            "transport": int(out[9] & 0xFFFFFFFF), "ticks_per_start": int(out[9] >> 32),
+            "idle_ticks": int(out[14]), "tcp_wakes": int(out[15])}
 
 
 def service_totals() -> dict:

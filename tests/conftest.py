@@ -19,6 +19,7 @@ if REPO not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line("markers", "expects_abort: the test provokes a copy-service timeout on purpose")
 
 
 @pytest.fixture(scope="session")

@@ -370,3 +370,39 @@ def test_tick_stats_on_tcp(mesh_factory):
     with api.Client(daemon_rank=0, ns=m.ns) as c:
         st = api.tick_stats()
         assert st is not None and st["ticks"] == 0 and st["transport"] == 0, st
+
+
+@pytest.mark.parametrize("idle_us", ["1000", "0"])
+def test_idle_mesh_ticks_instead_of_tcp_wakes(mesh_factory, idle_us):
+    """the tick control plane must not depend on TCP. With idle
+    ticks (OCM_TICK_IDLE_US, default 1000) an idle 8-rank mesh keeps ticking, and a
+    rank that posts into it rings the host-wide doorbell instead of sending
+    MSG_TICK_WAKE over TCP: after bursts separated by idle gaps, no rank has sent a
+    single TCP wake-up. With 0 (the round-3 protocol) every burst after idle starts
+    with TCP wake-ups, which the counter shows."""
+    import time
+
+    m = mesh_factory(8, env={"OCM_CTRL_AUTO_SOCKET": "1", "OCM_TICK_SOCKET_SEAL": "1", "OCM_LEASE_BYTES": "0",
+                             "OCM_TICK_IDLE_US": idle_us})
+    with api.Client(daemon_rank=0, ns=m.ns) as c:
+        assert _ctrl(c, 8) == ["socket"] * 8
+        for i in range(5):
+            time.sleep(0.03)  # past the 64 busy ticks: the mesh is idle again
+            t0 = time.perf_counter()
+            a = c.alloc(api.OCM_REMOTE_RDMA, local_bytes=4096, remote_bytes=1 << 20, remote_rank=1 + i)
+            took = time.perf_counter() - t0
+            a.free()
+            assert took < 1.0, f"alloc after an idle gap took {took * 1e3:.1f} ms"
+    wakes, idle = [], []
+    for r in range(8):
+        with api.Client(daemon_rank=r, ns=m.ns):
+            st = api.tick_stats()
+            wakes.append(st["tcp_wakes"])
+            idle.append(st["idle_ticks"])
+    if idle_us == "0":
+        assert sum(wakes) > 0 and sum(idle) == 0, (wakes, idle)
+    else:
+        assert wakes == [0] * 8 and all(x > 0 for x in idle), (wakes, idle)
+        assert "idle ticks, no TCP wake-ups" in m.logs()
+    logs = m.logs()
+    assert "falling back to TCP" not in logs and "leaving the" not in logs

@@ -212,6 +212,11 @@ def test_bench_on_real_gpus():
         assert row["owner_gpu"] == int(p) and row["put_GiBps"] > 0 and row["link"] is not None, row
     cp = res["control_plane"]
     assert cp["tcp"]["alloc_p50_us"] > 0 and cp["rccl"]["ticks_rank0"] > 0, cp
+    # a clean run - no library warning on any rank (a copy-service
+    # fallback, a tick transport leaving for TCP, a refused IPC import ...)
+    assert res["service_clean"] is True, res["ranks"]
+    warns = [l for l in (r.stdout + r.stderr).splitlines() if "[ocm W" in l or "[ocm E" in l]
+    assert not warns, warns[:20]
 
 
 def test_torch_tensors_in_another_gpus_hbm(mesh_factory):
