@@ -252,6 +252,7 @@ struct State {
     // wait long for the persistent kernel to leave.
     unsigned long long svc_idle_ticks = 100ull * kServiceIdleUsDefault;
     uint64_t svc_relaunches = 0;    // instances started after an idle exit (ocm_x_service_stats)
+    uint64_t svc_ns_relaunch = 0;   // host time of those restarts (reap + launch), ocm_x_service_health
     // Roster (ocm/xfer.h): gangs are sized to the members already running. Right
     // after a launch a gang op waits up to svc_roster_wait_ns for the grid to check
     // in before it settles for fewer members (OCM_SERVICE_ROSTER_WAIT_US).

@@ -957,8 +957,9 @@ void ocm_x_service_stats(uint64_t out[5]) {
 // members were resident, instances that left with the posted op unfinished,
 // ops abandoned after OCM_SERVICE_TIMEOUT_MS (drained, then redone by a launch),
 // 1 if an instance could not be drained (service off, op failed), the smallest
-// roster a gang op was sized to (0: none yet), the current instance's roster}.
-void ocm_x_service_health(uint64_t out[6]) {
+// roster a gang op was sized to (0: none yet), the current instance's roster,
+// relaunches after an idle exit, and the host ns they took (reap + launch)}.
+void ocm_x_service_health(uint64_t out[8]) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     out[0] = s.svc_degraded;
@@ -967,6 +968,8 @@ void ocm_x_service_health(uint64_t out[6]) {
     out[3] = s.svc_wedged ? 1 : 0;
     out[4] = s.svc_roster_min == ~0ull ? 0 : s.svc_roster_min;
     out[5] = (s.svc && s.svc_running) ? __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE) : 0;
+    out[6] = s.svc_relaunches;
+    out[7] = s.svc_ns_relaunch;
 }
 
 // Copy-service phase stamps of the last request (OCM_SERVICE_PROTO with the

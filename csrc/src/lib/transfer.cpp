@@ -312,15 +312,25 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
         if (sh >= 12 && sh < x.tile_shift) x.tile_shift = sh;
     }
     unsigned long long seq = ++s.svc_seq;
+    const uint64_t t_enter = now_ns();
+    bool relaunched = false;
     if (s.svc_running && __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE) != 0) {
         // The instance left on its idle timeout (OCM_SERVICE_IDLE_US): reap it and
-        // start the next one right away instead of posting to nobody.
+        // start the next one right away instead of posting to nobody. Its members
+        // leave within microseconds of its lead: a query usually finds the stream
+        // drained, and only then may the next request be posted (a member still
+        // polling the gang record must not take it).
         DeviceGuard g(s.device);
-        (void)hipStreamSynchronize(s.svc_stream);
+        if (hipStreamQuery(s.svc_stream) != hipSuccess) (void)hipStreamSynchronize(s.svc_stream);
+        (void)hipGetLastError();
         s.svc_running = false;
         s.svc_relaunches++;
+        relaunched = true;
     }
-    if (!s.svc_running && service_start(seq) != 0) return -1;
+    if (!s.svc_running) {
+        if (service_start(seq) != 0) return -1;
+        if (relaunched) s.svc_ns_relaunch += now_ns() - t_enter;
+    }
     // The host sizes the gang and the completion count every workgroup agrees on:
     // up to the direct pollers (no relay) for ops they copy fast enough, and never
     // wider than the members already running (the roster).

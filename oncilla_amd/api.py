@@ -385,12 +385,15 @@ def service_health() -> dict:
     re-posted (`incomplete_exits`, expected 0), ops abandoned after
     OCM_SERVICE_TIMEOUT_MS and redone by a launch once the instance had drained
     (`aborts`), whether an instance could not be drained at all (`wedged`), the
-    smallest roster a gang op was sized to (`roster_min`, 0: none yet) and the
-    running instance's roster (`roster`, 0: not running)."""
-    out = (ctypes.c_uint64 * 6)()
+    smallest roster a gang op was sized to (`roster_min`, 0: none yet), the
+    running instance's roster (`roster`, 0: not running), and the relaunches after
+    an idle exit with their mean host time (reap + launch, microseconds)."""
+    out = (ctypes.c_uint64 * 8)()
     load().ocm_x_service_health(out)
+    n = int(out[6])
     return {"degraded": int(out[0]), "incomplete_exits": int(out[1]), "aborts": int(out[2]),
-            "wedged": bool(out[3]), "roster_min": int(out[4]), "roster": int(out[5])}
+            "wedged": bool(out[3]), "roster_min": int(out[4]), "roster": int(out[5]), "relaunches": n,
+            "relaunch_host_us_mean": round(out[7] / n / 1e3, 2) if n else None}
 
 
 def tick_stats() -> dict | None:

@@ -105,11 +105,17 @@ def idle_gap_latency(alloc: api.Allocation, nbytes: int = 4096, gaps=IDLE_GAPS, 
     for gap, iters in gaps:
         row = {}
         for op, key in ((0, "get"), (1, "put")):
+            h0 = api.service_health()
             xs, rel = alloc.time_onesided_samples(op, nbytes, iters, gap_s=gap, cap_s=cap_s, min_iters=10)
+            h1 = api.service_health()
             row[f"{key}_p50_us"] = round(percentile(xs, 50) * 1e6, 2)
             row[f"{key}_p99_us"] = round(percentile(xs, 99) * 1e6, 2)
             row[f"{key}_relaunches"] = rel
             row[f"{key}_n"] = len(xs)
+            if rel and h0["relaunches"] < h1["relaunches"]:
+                # host time per relaunch (reap + launch); the rest of the cost is the kernel's start
+                tot = lambda h: (h["relaunch_host_us_mean"] or 0) * h["relaunches"]  # noqa: E731
+                row[f"{key}_relaunch_host_us"] = round((tot(h1) - tot(h0)) / (h1["relaunches"] - h0["relaunches"]), 2)
         out[str(int(round(gap * 1e6)))] = row
     return out
 

@@ -63,7 +63,10 @@ def _measure(m, tick_self):
             time.sleep(0.05)
         r = wl.alloc_latency(c, api.OCM_REMOTE_GPU, 300, local_bytes=4096, remote_bytes=1 << 20)
         r["ticks"] = c.stats(0)["ctrl_ticks"]
-        return {k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()}
+        r = {k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()}
+        if tick_self:
+            r["tick"] = api.tick_stats()  # the hop split into queue wait / tick / delivery
+        return r
 
 
 VARIANTS = {
@@ -112,6 +115,11 @@ VARIANTS = {
     "rccl_graph8_w3": ("rccl", True, {"OCM_TICK_GRAPH": "8", "OCM_TICK_SEAL_WAIT_US": "3", "OCM_TICK_STATS": "1"}),
     "rccl_nograph": ("rccl", True, {"OCM_TICK_GRAPH": "0", "OCM_TICK_STATS": "1"}),
     "rccl_spec_ccd_spin300": ("rccl", True, {"OCM_RPC_SPIN_US": "300", "OCM_DAEMON_SPIN_US": "300"}),
+    # round 4: idle ticks (default) vs the round-3 stop-and-wake protocol
+    "rccl_idle0": ("rccl", True, {"OCM_TICK_IDLE_US": "0"}),
+    "rccl_2s_idle": ("rccl", True, {"OCM_TICK_STREAMS": "2"}),
+    "rccl_w2": ("rccl", True, {"OCM_TICK_SEAL_WAIT_US": "2"}),
+    "rccl_w12": ("rccl", True, {"OCM_TICK_SEAL_WAIT_US": "12"}),
 }
 
 
