@@ -150,6 +150,7 @@ int service_start(unsigned long long first_seq) {
             s.svc_max = 0;
             OCM_FAIL(-1, "copy service: no device mailbox");
         }
+        s.svc_box_dirty = true;  // fresh device memory: the first launch clears it
         // A stream of its own priority: HIP shares its few hardware queues
         // (GPU_MAX_HW_QUEUES) among a process's streams, and a launch on a stream
         // that shares the service's queue waits behind the persistent kernel until
@@ -251,6 +252,8 @@ void service_stop() {
     if (s.svc_box) (void)hipFree(s.svc_box);
     s.svc = nullptr;
     s.svc_box = nullptr;
+    s.svc_box_dirty = true;
+    s.svc_checkins = 0;
     s.svc_stream = nullptr;
 }
 
