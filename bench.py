@@ -594,6 +594,25 @@ def main() -> int:
                 row = {k: (max(x[gap][k] for x in igs) if k.endswith("_us") else sum(x[gap][k] for x in igs))
                        for k in ig[gap]}
                 idle_gap[gap] = row
+            # the headline small-op rows run pinned (OCM_PIN=1, set above for GPU runs);
+            # the library default leaves apps unpinned, so time 4 KiB ops unpinned too
+            def unpinned():
+                mask = os.sched_getaffinity(0)
+                try:
+                    os.sched_setaffinity(0, range(os.cpu_count() or 1))
+                    out = {}
+                    for op, key in ((0, "get"), (1, "put")):
+                        xs, _ = pair.time_onesided_samples(op, 4096, 300, cap_s=0.5)
+                        out[f"{key}_p50_us"] = round(wl.percentile(xs, 50) * 1e6, 2)
+                    return out
+                finally:
+                    os.sched_setaffinity(0, mask)
+
+            if use_gpu and os.environ.get("OCM_PIN") == "1":
+                up, _ = _local(unpinned)
+                ups = gather_obj(dist, up, world)
+                if all(ups):
+                    idle_gap["unpinned_back_to_back"] = {k: max(u[k] for u in ups) for k in ups[0]}
             base = idle_gap.get("0")
             if base and "1000" in idle_gap:
                 idle_gap["ratio_1ms_vs_back_to_back"] = {

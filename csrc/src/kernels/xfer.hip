@@ -895,8 +895,12 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                     if (h == readlane64(w, base + 14)) break;
                     continue;  // seq landed before the rest of the record: read it again
                 }
+                // Nor while part of the grid has not started (the roster is short): the
+                // kernel cannot complete before those workgroups get CUs and leave, so
+                // leaving would not release a device-wide sync any sooner, and the next
+                // op would have to wait for them before a new instance could start.
                 if (lead && __builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks &&
-                    (served || __builtin_amdgcn_s_memrealtime() - started > 2000000ull)) {
+                    (served ? roster >= gridDim.x : __builtin_amdgcn_s_memrealtime() - started > 2000000ull)) {
                     // Leave only once every member the last request named is done
                     // with it: a member that saw the STOP first would never serve it.
                     if (service_last_complete(slot, box, proto, last, last_gang)) {
