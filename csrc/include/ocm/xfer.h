@@ -172,7 +172,14 @@ constexpr int kServiceReqGang = 13;  // record word: active | target << 16 | STR
 // takes the fenced hand-off (system acquire before the copy, release before
 // `done`) whatever the protocol bits say.
 constexpr unsigned long long kServiceGangStrict = 1ull << 63;
-constexpr unsigned long long kServiceGangTargetMask = (1ull << 47) - 1;  // bits 16..62
+constexpr unsigned long long kServiceGangTargetMask = (1ull << 31) - 1;  // bits 16..46
+// Bits 47..62: the epoch of the instance the request is for (its launch number,
+// mod 2^16). Instances run on a small pool of streams, so a relaunch need not wait
+// for workgroups of an earlier instance that never got a CU (another process holds
+// them): such a workgroup that starts late polls the same host gang record, and
+// must leave a newer instance's request alone.
+constexpr int kServiceGangEpochShift = 47;
+constexpr unsigned long long kServiceGangEpochMask = 0xFFFFull;
 static_assert(kServiceArgWords <= kServiceReqGang, "service request record holds 13 argument words");
 
 struct alignas(128) ServiceReq {
@@ -269,9 +276,12 @@ constexpr bool service_wg_done(unsigned proto, unsigned long long active) {
 // direct_wgs: with gang_req, workgroups 0..direct_wgs-1 poll it themselves.
 // checkin_base: ServiceBox::checkin when this instance starts (0 after a reset);
 // reset_box: zero the box first (stream-ordered memset).
+// epoch: this instance's launch number (mod 2^16, see kServiceGangEpochShift).
+// degraded_idle_ticks: the idle exit while part of the grid has not started yet.
 hipError_t service_launch(ServiceReq *req, ServiceReq *gang_req, ServiceSlot *slot, ServiceBox *box,
                           unsigned long long first_seq, unsigned long long idle_ticks, unsigned blocks, unsigned proto,
-                          unsigned direct_wgs, unsigned long long checkin_base, bool reset_box, hipStream_t stream);
+                          unsigned direct_wgs, unsigned long long checkin_base, bool reset_box, unsigned epoch,
+                          unsigned long long degraded_idle_ticks, hipStream_t stream);
 
 // Deterministic 32-bit word pattern (word i of a buffer) for data verification.
 hipError_t pattern_fill(void *p, uint64_t words, uint64_t first_word, uint32_t seed, hipStream_t stream);

@@ -813,7 +813,8 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                                                            ServiceSlot *slot, ServiceBox *box,
                                                            unsigned long long first_seq,
                                                            unsigned long long idle_ticks, unsigned proto,
-                                                           unsigned direct_wgs, unsigned long long checkin_base) {
+                                                           unsigned direct_wgs, unsigned long long checkin_base,
+                                                           unsigned epoch, unsigned long long degraded_idle_ticks) {
     __shared__ __attribute__((aligned(16))) unsigned long long sh[16];
     __shared__ unsigned sh_id;
     const int tid = threadIdx.x;
@@ -892,15 +893,20 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                     unsigned long long h = service_mix(0, s);
 #pragma unroll
                     for (int i = 0; i <= kServiceReqGang; i++) h = service_mix(h, readlane64(w, base + i));
-                    if (h == readlane64(w, base + 14)) break;
-                    continue;  // seq landed before the rest of the record: read it again
+                    if (h != readlane64(w, base + 14)) continue;  // seq landed before the rest: read it again
+                    // whole; a member of an earlier instance (started late) leaves a newer one's request alone
+                    if (lead || ((readlane64(w, base + kServiceReqGang) >> kServiceGangEpochShift) &
+                                 kServiceGangEpochMask) == epoch)
+                        break;
                 }
-                // Nor while part of the grid has not started (the roster is short): the
-                // kernel cannot complete before those workgroups get CUs and leave, so
-                // leaving would not release a device-wide sync any sooner, and the next
-                // op would have to wait for them before a new instance could start.
-                if (lead && __builtin_amdgcn_s_memrealtime() - idle_start > idle_ticks &&
-                    (served ? roster >= gridDim.x : __builtin_amdgcn_s_memrealtime() - started > 2000000ull)) {
+                // While part of the grid has not started (the roster is short) it waits
+                // longer (degraded_idle_ticks): the kernel cannot complete before those
+                // workgroups get CUs and leave anyway, so leaving early would release a
+                // device-wide sync no sooner, and every relaunch would need another
+                // stream while they wait (the pool is small).
+                if (lead &&
+                    __builtin_amdgcn_s_memrealtime() - idle_start > (roster >= gridDim.x ? idle_ticks : degraded_idle_ticks) &&
+                    (served || __builtin_amdgcn_s_memrealtime() - started > 2000000ull)) {
                     // Leave only once every member the last request named is done
                     // with it: a member that saw the STOP first would never serve it.
                     if (service_last_complete(slot, box, proto, last, last_gang)) {
@@ -985,7 +991,8 @@ void service_store_seq(ServiceReq *req, unsigned long long seq) {
 
 hipError_t service_launch(ServiceReq *req, ServiceReq *gang_req, ServiceSlot *slot, ServiceBox *box,
                           unsigned long long first_seq, unsigned long long idle_ticks, unsigned blocks, unsigned proto,
-                          unsigned direct_wgs, unsigned long long checkin_base, bool reset_box, hipStream_t stream) {
+                          unsigned direct_wgs, unsigned long long checkin_base, bool reset_box, unsigned epoch,
+                          unsigned long long degraded_idle_ticks, hipStream_t stream) {
     if (!req || !slot || !box || blocks == 0 || first_seq == 0 || (gang_req && direct_wgs == 0))
         return hipErrorInvalidValue;
     if (reset_box) {
@@ -993,7 +1000,8 @@ hipError_t service_launch(ServiceReq *req, ServiceReq *gang_req, ServiceSlot *sl
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(service_kernel, dim3(blocks), dim3(kThreads), 0, stream, req, gang_req, slot, box, first_seq,
-                       idle_ticks, proto, direct_wgs, checkin_base);
+                       idle_ticks, proto, direct_wgs, checkin_base, epoch & (unsigned)kServiceGangEpochMask,
+                       degraded_idle_ticks);
     return hipGetLastError();
 }
 // ---- verification patterns (benchmarks and tests check data without a host round trip) ----

@@ -211,10 +211,28 @@ struct State {
     ServiceReq *svc_req = nullptr;   // request record (&svc->req)
     ServiceReq *svc_greq = nullptr;  // GANGREC: gang requests' record, a page of its own
     char *svc_rec_pages = nullptr;   // separately allocated record pages (GANGREC / WCREQ), freed at stop
-    unsigned long long svc_gang_total = 0;  // gang completions this instance counts to (device counter mirror)
-    ServiceBox *svc_box = nullptr;   // device-memory mailbox of the gang
+    ServiceBox *svc_box = nullptr;   // device-memory mailbox of the gang (the current lane's)
     unsigned long long *pattern_bad = nullptr;  // device counter of ocm_x_pattern checks
-    hipStream_t svc_stream = nullptr;
+    hipStream_t svc_stream = nullptr;  // the current lane's stream
+    // Lanes of the service: a stream and a gang box each. An instance whose lead has
+    // left may still have workgroups that never got a CU (another process holds
+    // them); the next instance starts on a lane whose stream has drained, a new lane
+    // (up to OCM_SERVICE_STREAMS, default 4), or waits for one. Requests carry the
+    // instance's epoch (ocm/xfer.h), so such a late workgroup never takes one.
+    struct SvcLane {
+        hipStream_t stream = nullptr;
+        ServiceBox *box = nullptr;
+        bool dirty = true;                  // clear the box before its next launch
+        unsigned long long checkins = 0;    // the box's check-in counter once its instances drained
+        unsigned long long gang_total = 0;  // the box's gang completion counter (mirror)
+    };
+    std::vector<SvcLane> svc_lanes;
+    int svc_lane = -1;
+    unsigned svc_lanes_max = 4;
+    unsigned svc_epoch = 0;
+    int svc_stream_prio = 0;
+    bool svc_prio_ok = false;
+    uint64_t svc_degraded_idle_ticks = 100ull * 5000;  // OCM_SERVICE_DEGRADED_IDLE_US (5 ms)
     unsigned svc_blocks = kServiceBlocksDefault;          // gang size (OCM_SERVICE_BLOCKS)
     unsigned svc_solo_tiles = kServiceSoloTilesDefault;  // requests of <= this many tiles stay on workgroup 0
     unsigned svc_solo_tiles_host_get = 1;  // ... for gets from the host tier (OCM_SERVICE_SOLO_TILES_HOST_GET)
@@ -253,16 +271,17 @@ struct State {
     unsigned long long svc_idle_ticks = 100ull * kServiceIdleUsDefault;
     uint64_t svc_relaunches = 0;    // instances started after an idle exit (ocm_x_service_stats)
     uint64_t svc_ns_relaunch = 0;   // host time of those restarts (reap + launch), ocm_x_service_health
+    uint64_t svc_ns_pick = 0, svc_ns_launch = 0, svc_epoch_starts = 0;  // every start: choosing a lane, the launch call
+    bool svc_relaunch_query = false;  // OCM_SERVICE_RELAUNCH_QUERY=1: always ask the runtime which lane drained
     // Roster (ocm/xfer.h): gangs are sized to the members already running. Right
     // after a launch a gang op waits up to svc_roster_wait_ns for the grid to check
     // in before it settles for fewer members (OCM_SERVICE_ROSTER_WAIT_US).
     uint64_t svc_launch_ns = 0;
-    // The gang's device box is zeroed only when it must be (ocm/xfer.h): at the
-    // first launch, after an instance left a request unfinished, or always with
+    // A lane's gang box is zeroed only when it must be (ocm/xfer.h): at its first
+    // launch, after an instance left a request unfinished, or always with
     // OCM_SERVICE_BOX_RESET=1. Otherwise the next instance's check-in tickets start
-    // at svc_checkins (every workgroup of every drained instance took one).
-    bool svc_box_dirty = true, svc_box_reset_always = false;
-    unsigned long long svc_checkins = 0;
+    // at the lane's `checkins` (every workgroup of every earlier instance took one).
+    bool svc_box_reset_always = false;
     uint64_t svc_roster_wait_ns = 200000;
     // Health counters (ocm_x_service_health): gang ops sized below the width they
     // wanted because fewer members were resident, instances that left with the

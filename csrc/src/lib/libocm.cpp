@@ -148,6 +148,9 @@ int ocm_init(void) {
     s.svc_timeout_ns = 1000000ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_TIMEOUT_MS", 10000));
     s.svc_drain_ns = 1000000ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_DRAIN_MS", 10000));
     s.svc_box_reset_always = env_int("OCM_SERVICE_BOX_RESET", 0) != 0;
+    s.svc_lanes_max = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_STREAMS", 4), 16));
+    s.svc_relaunch_query = env_int("OCM_SERVICE_RELAUNCH_QUERY", 0) != 0;
+    s.svc_degraded_idle_ticks = 100ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_DEGRADED_IDLE_US", 5000));
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");
     s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
     s.tuning = xfer_tuning_from_env();
@@ -958,8 +961,9 @@ void ocm_x_service_stats(uint64_t out[5]) {
 // ops abandoned after OCM_SERVICE_TIMEOUT_MS (drained, then redone by a launch),
 // 1 if an instance could not be drained (service off, op failed), the smallest
 // roster a gang op was sized to (0: none yet), the current instance's roster,
-// relaunches after an idle exit, and the host ns they took (reap + launch)}.
-void ocm_x_service_health(uint64_t out[8]) {
+// relaunches after an idle exit, and the host ns they took (reap + launch), then
+// over every start: ns choosing a lane, ns in the launch call, starts}.
+void ocm_x_service_health(uint64_t out[11]) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     out[0] = s.svc_degraded;
@@ -970,6 +974,9 @@ void ocm_x_service_health(uint64_t out[8]) {
     out[5] = (s.svc && s.svc_running) ? __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE) : 0;
     out[6] = s.svc_relaunches;
     out[7] = s.svc_ns_relaunch;
+    out[8] = s.svc_ns_pick;
+    out[9] = s.svc_ns_launch;
+    out[10] = s.svc_epoch_starts;
 }
 
 // Copy-service phase stamps of the last request (OCM_SERVICE_PROTO with the

@@ -131,6 +131,26 @@ int sync_stream() {
 
 // ---- persistent copy service ----
 
+// A new lane: a stream of the service's priority and a gang box. -1 on failure.
+static int service_new_lane() {
+    State &s = S();
+    State::SvcLane l;
+    hipError_t e = s.svc_prio_ok ? hipStreamCreateWithPriority(&l.stream, hipStreamNonBlocking, s.svc_stream_prio)
+                                 : hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    if (hipMalloc(reinterpret_cast<void **>(&l.box), sizeof(ServiceBox)) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipStreamDestroy(l.stream);
+        return -1;
+    }
+    l.dirty = true;  // fresh device memory: its first launch clears it
+    s.svc_lanes.push_back(l);
+    return (int)s.svc_lanes.size() - 1;
+}
+
 int service_start(unsigned long long first_seq) {
     State &s = S();
     DeviceGuard g(s.device);
@@ -144,14 +164,7 @@ int service_start(unsigned long long first_seq) {
         }
         std::memset(s.svc, 0, sizeof(ServiceSlot));
         s.svc_req = &s.svc->req;
-        if (hipMalloc(reinterpret_cast<void **>(&s.svc_box), sizeof(ServiceBox)) != hipSuccess) {
-            (void)hipGetLastError();
-            s.svc_box = nullptr;
-            s.svc_max = 0;
-            OCM_FAIL(-1, "copy service: no device mailbox");
-        }
-        s.svc_box_dirty = true;  // fresh device memory: the first launch clears it
-        // A stream of its own priority: HIP shares its few hardware queues
+        // Streams of their own priority: HIP shares its few hardware queues
         // (GPU_MAX_HW_QUEUES) among a process's streams, and a launch on a stream
         // that shares the service's queue waits behind the persistent kernel until
         // its idle exit (2 ms per large op in bench.py with torch's streams around, when
@@ -159,18 +172,19 @@ int service_start(unsigned long long first_seq) {
         // Queues are pooled per priority, so the service's is not shared with the
         // normal-priority streams of the library and the application.
         int lo = 0, hi = 0;
-        hipError_t pe = hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if (pe != hipSuccess || lo == hi ||
-            hipStreamCreateWithPriority(&s.svc_stream, hipStreamNonBlocking, env_int("OCM_SERVICE_STREAM_PRIO", hi)) !=
-                hipSuccess) {
-            (void)hipGetLastError();
+        s.svc_prio_ok = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && lo != hi;
+        (void)hipGetLastError();
+        s.svc_stream_prio = env_int("OCM_SERVICE_STREAM_PRIO", hi);
+        if (service_new_lane() < 0 && s.svc_prio_ok) {
+            s.svc_prio_ok = false;
             s.svc_shared_queue = true;  // launches park the service first (see xfer)
-            if (hipStreamCreateWithFlags(&s.svc_stream, hipStreamNonBlocking) != hipSuccess) {
-                (void)hipGetLastError();
-                s.svc_max = 0;
-                OCM_FAIL(-1, "copy service: no stream");
-            }
+            service_new_lane();
         }
+        if (s.svc_lanes.empty()) {
+            s.svc_max = 0;
+            OCM_FAIL(-1, "copy service: no stream or device mailbox");
+        }
+        s.svc_lane = 0;
         const bool gangrec = (s.svc_proto & kServiceProtoGangRec) && s.svc_blocks > 1;
         const bool wc = (s.svc_proto & kServiceProtoWCReq) != 0;
         if (gangrec || wc) {
@@ -190,23 +204,58 @@ int service_start(unsigned long long first_seq) {
         }
     }
     if (s.svc_wedged) OCM_FAIL(-1, "copy service: a previous instance could not be drained");
+    // A lane whose stream has drained: the current one normally (its last instance's
+    // workgroups leave microseconds after its lead), another drained one, a new one,
+    // or - every lane still holding workgroups that found no CU - wait for the current.
+    // When the last instance had its whole grid resident (its roster is still in the
+    // slot), its workgroups leave right behind its lead: stay on its lane without a
+    // runtime query (stream order starts the new instance after them; they ignore
+    // the new epoch meanwhile). A query costs a relaunch ~10 us of host time.
+    const uint64_t tq = now_ns();
+    int pick = -1;
+    const int n = (int)s.svc_lanes.size();
+    if (s.svc_lane >= 0 && !s.svc_relaunch_query &&
+        __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE) >= (unsigned long long)s.svc_blocks)
+        pick = s.svc_lane;
+    for (int k = 0; k < n && pick < 0; k++) {
+        const int i = (s.svc_lane + k) % n;
+        if (hipStreamQuery(s.svc_lanes[(size_t)i].stream) == hipSuccess) pick = i;
+    }
+    (void)hipGetLastError();
+    if (pick < 0 && (unsigned)n < s.svc_lanes_max) pick = service_new_lane();
+    if (pick < 0) {
+        pick = s.svc_lane;
+        (void)hipStreamSynchronize(s.svc_lanes[(size_t)pick].stream);
+        (void)hipGetLastError();
+    }
+    s.svc_lane = pick;
+    State::SvcLane &l = s.svc_lanes[(size_t)pick];
+    s.svc_stream = l.stream;
+    s.svc_box = l.box;
     __atomic_store_n(&s.svc->exited, 0ull, __ATOMIC_RELEASE);
     __atomic_store_n(&s.svc->roster, 0ull, __ATOMIC_RELEASE);  // the new lead publishes its own
     service_store_seq(s.svc_req, 0ull);  // clear a STOP left by a parked instance
     if (s.svc_greq) service_store_seq(s.svc_greq, 0ull);
-    const bool reset = s.svc_box_dirty || s.svc_box_reset_always;
+    // the gang counter mirror stays below the 31-bit target field (ocm/xfer.h)
+    const bool reset = l.dirty || s.svc_box_reset_always || l.gang_total > (1ull << 30);
     if (reset) {
-        s.svc_gang_total = 0;  // the launch zeroes the device counters
-        s.svc_checkins = 0;
+        l.gang_total = 0;  // the launch zeroes the device counters
+        l.checkins = 0;
     }
-    if (service_launch(s.svc_req, s.svc_greq, s.svc, s.svc_box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_proto,
-                       std::min(s.svc_direct, s.svc_blocks), s.svc_checkins, reset, s.svc_stream) != hipSuccess) {
+    s.svc_epoch = (s.svc_epoch + 1) & (unsigned)kServiceGangEpochMask;
+    const uint64_t tl = now_ns();
+    s.svc_ns_pick += tl - tq;
+    if (service_launch(s.svc_req, s.svc_greq, s.svc, l.box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_proto,
+                       std::min(s.svc_direct, s.svc_blocks), l.checkins, reset, s.svc_epoch,
+                       s.svc_degraded_idle_ticks, l.stream) != hipSuccess) {
         (void)hipGetLastError();
         s.svc_max = 0;
         OCM_FAIL(-1, "copy service launch failed");
     }
-    s.svc_box_dirty = false;
-    s.svc_checkins += s.svc_blocks;  // every workgroup takes one ticket before the instance drains
+    s.svc_ns_launch += now_ns() - tl;
+    s.svc_epoch_starts++;
+    l.dirty = false;
+    l.checkins += s.svc_blocks;  // every workgroup takes one ticket before the instance drains
     s.svc_running = true;
     s.svc_launch_ns = now_ns();
     return 0;
@@ -240,20 +289,22 @@ void service_stop() {
     if (s.svc_running) {
         service_store_seq(s.svc_req, kServiceStop);
         if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
-        (void)hipStreamSynchronize(s.svc_stream);
         s.svc_running = false;
     }
-    (void)hipStreamDestroy(s.svc_stream);
+    for (State::SvcLane &l : s.svc_lanes) {  // every lane drained before its box goes
+        (void)hipStreamSynchronize(l.stream);
+        (void)hipStreamDestroy(l.stream);
+        if (l.box) (void)hipFree(l.box);
+    }
+    s.svc_lanes.clear();
+    s.svc_lane = -1;
     s.svc_req = nullptr;
     if (s.svc_rec_pages) (void)hipHostFree(s.svc_rec_pages);
     s.svc_rec_pages = nullptr;
     s.svc_greq = nullptr;
     (void)hipHostFree(s.svc);
-    if (s.svc_box) (void)hipFree(s.svc_box);
     s.svc = nullptr;
     s.svc_box = nullptr;
-    s.svc_box_dirty = true;
-    s.svc_checkins = 0;
     s.svc_stream = nullptr;
 }
 
@@ -301,7 +352,7 @@ static int service_abort(unsigned long long seq, unsigned long long active, cons
     }
     (void)hipGetLastError();
     s.svc_running = false;
-    s.svc_box_dirty = true;
+    if (s.svc_lane >= 0) s.svc_lanes[(size_t)s.svc_lane].dirty = true;
     OCM_FAIL(-1, "copy service %s (seq %llu, %llu members, %llu done words, roster %llu, exited %llu); drained",
              why, seq, active, wg_in, roster, ex);
 }
@@ -318,14 +369,10 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
     const uint64_t t_enter = now_ns();
     bool relaunched = false;
     if (s.svc_running && __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE) != 0) {
-        // The instance left on its idle timeout (OCM_SERVICE_IDLE_US): reap it and
-        // start the next one right away instead of posting to nobody. Its members
-        // leave within microseconds of its lead: a query usually finds the stream
-        // drained, and only then may the next request be posted (a member still
-        // polling the gang record must not take it).
-        DeviceGuard g(s.device);
-        if (hipStreamQuery(s.svc_stream) != hipSuccess) (void)hipStreamSynchronize(s.svc_stream);
-        (void)hipGetLastError();
+        // The instance left on its idle timeout (OCM_SERVICE_IDLE_US), its last request
+        // complete: start the next one right away instead of posting to nobody. No wait
+        // for its stream: the next instance takes a drained lane, and a workgroup of the
+        // old one still polling (or starting late) leaves requests of a newer epoch alone.
         s.svc_running = false;
         s.svc_relaunches++;
         relaunched = true;
@@ -350,10 +397,12 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
         wgdone = service_wg_done(s.svc_proto, active);
         unsigned long long target = 0;
         if (active > 1 && !wgdone) {  // WGDONE gangs leave the counter alone
-            s.svc_gang_total += active;
-            target = s.svc_gang_total;
+            State::SvcLane &l = s.svc_lanes[(size_t)s.svc_lane];
+            l.gang_total += active;
+            target = l.gang_total;
         }
-        gang = active | (target << 16) | (strict ? kServiceGangStrict : 0ull);
+        gang = active | (target << 16) | ((unsigned long long)s.svc_epoch << kServiceGangEpochShift) |
+               (strict ? kServiceGangStrict : 0ull);
         // GANGREC: gang requests go to the record the whole gang polls.
         rq = (active > 1 && s.svc_greq) ? s.svc_greq : s.svc_req;
         service_post(rq, x, gang, seq);
@@ -395,7 +444,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
                 }
                 if (ex > seq) s.svc_incomplete_exits++;
                 // Members may have counted part of the request in: start from a clean box.
-                s.svc_box_dirty = true;
+                s.svc_lanes[(size_t)s.svc_lane].dirty = true;
                 // Re-post under a fresh seq. Direct gang members of the instance that
                 // left may have served part of this request and stored its seq in their
                 // WGDONE words; under the old seq those stale words would count as the

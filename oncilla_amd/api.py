@@ -388,12 +388,15 @@ def service_health() -> dict:
     smallest roster a gang op was sized to (`roster_min`, 0: none yet), the
     running instance's roster (`roster`, 0: not running), and the relaunches after
     an idle exit with their mean host time (reap + launch, microseconds)."""
-    out = (ctypes.c_uint64 * 8)()
+    out = (ctypes.c_uint64 * 11)()
     load().ocm_x_service_health(out)
-    n = int(out[6])
+    n, k = int(out[6]), int(out[10])
     return {"degraded": int(out[0]), "incomplete_exits": int(out[1]), "aborts": int(out[2]),
             "wedged": bool(out[3]), "roster_min": int(out[4]), "roster": int(out[5]), "relaunches": n,
-            "relaunch_host_us_mean": round(out[7] / n / 1e3, 2) if n else None}
+            "relaunch_host_us_mean": round(out[7] / n / 1e3, 2) if n else None,
+            # every start, split: choosing a lane (runtime stream queries) / the launch call itself
+            "start_pick_us_mean": round(out[8] / k / 1e3, 2) if k else None,
+            "start_launch_us_mean": round(out[9] / k / 1e3, 2) if k else None}
 
 
 def tick_stats() -> dict | None:
