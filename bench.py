@@ -339,8 +339,14 @@ def ctrl_extra(dist, world: int, rank: int, local_rank: int, use_gpu: bool, samp
         ticks = [x["r"].get("tick") for x in res]
         if any(ticks):
             out[ctrl]["hop_mean_us_per_rank"] = [t["hop_mean_us"] if t else None for t in ticks]
+            # the hop split: waiting for a tick / the tick itself / the event loop's pickup
+            out[ctrl]["hop_split_us_rank0"] = ({k: ticks[0][k] for k in ("hop_wait_mean_us", "hop_exec_mean_us",
+                                                                          "deliver_mean_us")} if ticks[0] else None)
             out[ctrl]["tick_period_mean_us_rank0"] = ticks[0]["tick_period_mean_us"] if ticks[0] else None
             out[ctrl]["start_mean_us_rank0"] = ticks[0]["start_mean_us"] if ticks[0] else None
+            # idle ticks instead of TCP wake-ups (OCM_TICK_IDLE_US): no rank woke a peer over TCP
+            out[ctrl]["tcp_wakes_all_ranks"] = sum(t["tcp_wakes"] for t in ticks if t)
+            out[ctrl]["idle_ticks_rank0"] = ticks[0]["idle_ticks"] if ticks[0] else None
     return out
 
 

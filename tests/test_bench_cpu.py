@@ -65,6 +65,8 @@ def test_bench_multi_rank(native, n, mode):
     hops = cp["socket"]["hop_mean_us_per_rank"]
     assert len(hops) == n and all(h is None or h > 0 for h in hops) and any(hops), cp
     assert cp["socket"]["start_mean_us_rank0"] > 0, cp
+    # idle ticks: the socket control plane woke nobody over TCP
+    assert cp["socket"]["tcp_wakes_all_ranks"] == 0 and cp["socket"]["idle_ticks_rank0"] > 0, cp
 
 
 def test_bench_extras_helpers_run(native):

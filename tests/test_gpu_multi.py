@@ -212,6 +212,8 @@ def test_bench_on_real_gpus():
         assert row["owner_gpu"] == int(p) and row["put_GiBps"] > 0 and row["link"] is not None, row
     cp = res["control_plane"]
     assert cp["tcp"]["alloc_p50_us"] > 0 and cp["rccl"]["ticks_rank0"] > 0, cp
+    # the RCCL control plane stands on its own (idle ticks, no TCP wake-ups)
+    assert cp["rccl"]["transport_up_all_ranks"] and cp["rccl"]["tcp_wakes_all_ranks"] == 0, cp
     # a clean run - no library warning on any rank (a copy-service
     # fallback, a tick transport leaving for TCP, a refused IPC import ...)
     assert res["service_clean"] is True, res["ranks"]
