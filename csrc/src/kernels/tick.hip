@@ -88,27 +88,43 @@ __global__ __launch_bounds__(64) void tick_seal_kernel(const TickRing *ring, uin
     uint64_t tag = 0, pub = 0;
     const uint64_t j = c + (uint64_t)lane;
     const uint64_t *src = reinterpret_cast<const uint64_t *>(&ring->rec[j & (kTickRing - 1)]);
-    const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + wait;
-    // Idle ticks: the host-wide doorbell, read in the same round trip as the ring.
-    const uint32_t seen = bell ? __hip_atomic_load(bell_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    uint32_t rung = seen;
+    uint64_t t_end = __builtin_amdgcn_s_memrealtime() + wait;
+    if (bell) {
+        // Idle tick: poll only `published` and the host-wide doorbell (two words over
+        // PCIe, ~0.6 us apart) until one moves or the idle period ends, then read the
+        // records once below. Polling the whole outbox for up to a millisecond would
+        // pull ~1 GB/s over the GPU's PCIe link the whole time the mesh is idle.
+        const uint32_t seen = __hip_atomic_load(bell_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t rung = seen;
+        for (;;) {
+            uint64_t pub_l = 0;
+            uint32_t bell_l = 0;
+            if (lane == 63) pub_l = sys_load(&ring->published);
+            if (lane == 62) bell_l = __hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            pub = ((uint64_t)__builtin_amdgcn_readlane((int)(pub_l >> 32), 63) << 32) |
+                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pub_l, 63);
+            rung = (uint32_t)__builtin_amdgcn_readlane((int)bell_l, 62);
+            // Uniform exit: pub and the bell are read-lane broadcasts and the clock is scalar.
+            if (pub > c || rung != seen || (int64_t)(__builtin_amdgcn_s_memrealtime() - t_end) >= 0) break;
+            __builtin_amdgcn_s_sleep(16);
+        }
+        if (lane == 0) __hip_atomic_store(bell_seen, rung, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wait = 0;  // one read of the outbox now
+        t_end = 0;
+    }
     for (;;) {
         uint64_t pub_l = 0;
-        uint32_t bell_l = 0;
         if (lane < kTickMsgs) {
 #pragma unroll
             for (int k = 0; k < kTickRecordWords; k++) w[k] = sys_load(src + k);
             tag = sys_load(&ring->tag[j & (kTickRing - 1)]);
         }
         if (lane == 63) pub_l = sys_load(&ring->published);
-        if (lane == 62 && bell) bell_l = __hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         pub = ((uint64_t)__builtin_amdgcn_readlane((int)(pub_l >> 32), 63) << 32) |
               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pub_l, 63);
-        if (bell) rung = (uint32_t)__builtin_amdgcn_readlane((int)bell_l, 62);
-        // Uniform exit: pub and the bell are read-lane broadcasts and the clock is scalar.
-        if (pub > c || wait == 0 || rung != seen || (int64_t)(__builtin_amdgcn_s_memrealtime() - t_end) >= 0) break;
+        // Uniform exit: pub is read-lane broadcast and the clock is scalar.
+        if (pub > c || wait == 0 || (int64_t)(__builtin_amdgcn_s_memrealtime() - t_end) >= 0) break;
     }
-    if (bell && lane == 0) __hip_atomic_store(bell_seen, rung, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t pending = pub > c ? pub - c : 0;
     const uint32_t n = pending < (uint64_t)kTickMsgs ? (uint32_t)pending : (uint32_t)kTickMsgs;
     const bool mine = (uint32_t)lane < n;
