@@ -191,16 +191,39 @@ static_assert(sizeof(ServiceReq) == 128, "service request layout");
 static_assert(__builtin_offsetof(ServiceReq, seq) == 120 && __builtin_offsetof(ServiceReq, sum) == 112,
               "the kernel reads seq/sum as words 15/14");
 
+// Lone lead (round 4, OCM_SERVICE_LONE_US): after the idle window the members
+// leave and the lead stays alone for lone_ticks more, polling only the small-op
+// record at a slower rate, and serves solo requests at hot latency. It never takes
+// a gang request: the host sees `lone` and starts a full instance (a new epoch),
+// whereupon the lone lead leaves without touching the slot. Only an instance on
+// the library's own AQL queue runs lone: HIP does not know that queue, so a
+// device-wide synchronize never waits for it (on a HIP stream it would).
+//
+// Device -> host status words (exited, roster, lone) carry the epoch of the
+// instance that wrote them in bits 48..63, so a word left by an earlier instance
+// is never read as the current one's.
+constexpr int kServiceTagShift = 48;
+constexpr unsigned long long kServiceTagValueMask = (1ull << kServiceTagShift) - 1;
+constexpr unsigned long long service_tag(unsigned epoch, unsigned long long v) {
+    return ((unsigned long long)(epoch & 0xFFFFu) << kServiceTagShift) | (v & kServiceTagValueMask);
+}
+// The value of a tagged word if instance `epoch` wrote it, else 0.
+constexpr unsigned long long service_untag(unsigned epoch, unsigned long long w) {
+    return (w >> kServiceTagShift) == (epoch & 0xFFFFu) ? (w & kServiceTagValueMask) : 0ull;
+}
+
 constexpr int kServiceWgDoneMax = 128;  // WGDONE: gangs of at most this many workgroups
 struct alignas(128) ServiceSlot {
     ServiceReq req;                   // the request record
     unsigned long long done;          // device -> host (own cache line)
-    unsigned long long exited;        // device -> host: first seq NOT served when it left
+    unsigned long long exited;        // device -> host, tagged: first seq NOT served when it left
     unsigned long long gpu_ticks;     // device -> host: sum of request-seen -> done ticks of workgroup 0 (100 MHz)
-    // device -> host: gang members resident so far (workgroup 0 included); the
-    // host zeroes it before a launch and sizes every gang to at most this many.
+    // device -> host, tagged: gang members resident so far (workgroup 0 included);
+    // the host sizes every gang to at most this many.
     unsigned long long roster;
-    unsigned long long pad[12];
+    unsigned long long lone;          // device -> host, tagged: first seq after which the members left
+    unsigned long long epoch_now;     // host -> device: the current instance's epoch (a lone lead of another leaves)
+    unsigned long long pad[10];
     // WGDONE: gang member i stores the seq it finished here (device -> host)
     unsigned long long wg_done[kServiceWgDoneMax];
 };
@@ -278,10 +301,28 @@ constexpr bool service_wg_done(unsigned proto, unsigned long long active) {
 // reset_box: zero the box first (stream-ordered memset).
 // epoch: this instance's launch number (mod 2^16, see kServiceGangEpochShift).
 // degraded_idle_ticks: the idle exit while part of the grid has not started yet.
-hipError_t service_launch(ServiceReq *req, ServiceReq *gang_req, ServiceSlot *slot, ServiceBox *box,
-                          unsigned long long first_seq, unsigned long long idle_ticks, unsigned blocks, unsigned proto,
-                          unsigned direct_wgs, unsigned long long checkin_base, bool reset_box, unsigned epoch,
-                          unsigned long long degraded_idle_ticks, hipStream_t stream);
+// lone_ticks: how long the lead stays alone after the members left (0: it leaves with them).
+struct ServiceKernelArgs {
+    const ServiceReq *req;
+    const ServiceReq *gang_req;
+    ServiceSlot *slot;
+    ServiceBox *box;
+    unsigned long long first_seq;
+    unsigned long long idle_ticks;
+    unsigned proto;
+    unsigned direct_wgs;
+    unsigned long long checkin_base;
+    unsigned epoch;
+    unsigned pad0;
+    unsigned long long degraded_idle_ticks;
+    unsigned long long lone_ticks;
+};
+// The kernel takes ServiceKernelArgs as its explicit kernel arguments, in this
+// order (an AQL dispatch copies the struct into the kernarg segment as is).
+static_assert(sizeof(ServiceKernelArgs) == 88, "service kernel argument layout");
+hipError_t service_launch(const ServiceKernelArgs &args, unsigned blocks, bool reset_box, hipStream_t stream);
+// The service kernel's symbol in the device code object embedded in libocm (AQL dispatch).
+constexpr const char *kServiceKernelSymbol = "ocm_service_kernel";
 
 // Deterministic 32-bit word pattern (word i of a buffer) for data verification.
 hipError_t pattern_fill(void *p, uint64_t words, uint64_t first_word, uint32_t seed, hipStream_t stream);

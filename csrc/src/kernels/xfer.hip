@@ -809,12 +809,17 @@ __device__ __forceinline__ bool service_last_complete(ServiceSlot *slot, Service
 // start) is "workgroup 0" of the protocol above and publishes how many have
 // checked in (the roster, see ocm/xfer.h): lane 32 of its poll reads the
 // check-in counter until the whole grid is in.
-__global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq, const ServiceReq *grq,
-                                                           ServiceSlot *slot, ServiceBox *box,
-                                                           unsigned long long first_seq,
-                                                           unsigned long long idle_ticks, unsigned proto,
-                                                           unsigned direct_wgs, unsigned long long checkin_base,
-                                                           unsigned epoch, unsigned long long degraded_idle_ticks) {
+}  // namespace
+
+// The copy service. extern "C": libocm also dispatches it by name from the device
+// code object embedded in the library, on an AQL queue of its own (ocm/aql.h).
+extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(ServiceKernelArgs ka) {
+    const ServiceReq *rq = ka.req, *grq = ka.gang_req;
+    ServiceSlot *slot = ka.slot;
+    ServiceBox *box = ka.box;
+    const unsigned long long first_seq = ka.first_seq, idle_ticks = ka.idle_ticks, checkin_base = ka.checkin_base;
+    const unsigned long long degraded_idle_ticks = ka.degraded_idle_ticks, lone_ticks = ka.lone_ticks;
+    const unsigned proto = ka.proto, direct_wgs = ka.direct_wgs, epoch = ka.epoch;
     __shared__ __attribute__((aligned(16))) unsigned long long sh[16];
     __shared__ unsigned sh_id;
     const int tid = threadIdx.x;
@@ -845,6 +850,8 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
     // relaunched each other until the op timed out), unless none comes in 20 ms.
     const unsigned long long started = idle_start;
     bool served = false;
+    bool lone = false;        // the lead alone: the members have left (lone_ticks)
+    bool superseded = false;  // the lead saw a newer instance: it leaves without touching the slot
     unsigned long long ticks_sum =
         lead ? __hip_atomic_load(&slot->gpu_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
     for (;;) {
@@ -854,20 +861,24 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
             // (args, gang word, sum, seq); a seq whose hash checks out is whole.
             unsigned long long w = 0, s;
             for (;;) {
-                const bool count = lead && roster < gridDim.x;  // wave-uniform
+                const bool count = lead && !lone && roster < gridDim.x;  // wave-uniform
                 if (tid < 16)
                     w = (lead || direct) ? __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                          : __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else if (direct && lead && tid < 32)
+                else if (direct && lead && !lone && tid < 32)
                     w = __hip_atomic_load(greq + (tid - 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 else if (!lead && tid == 16)
                     w = __hip_atomic_load(&box->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the lead left
                 else if (count && tid == 32)
                     w = __hip_atomic_load(&box->checkin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if (lone && tid == 48)
+                    w = __hip_atomic_load(&slot->epoch_now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (count) {
                     const unsigned long long r = readlane64(w, 32) - checkin_base;  // check-ins, the lead's included
                     if (r > roster) {  // members counted here are running: requests may name them
-                        if (tid == 0) __hip_atomic_store(&slot->roster, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        if (tid == 0)
+                            __hip_atomic_store(&slot->roster, service_tag(epoch, r), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
                         roster = r;
                     }
                 }
@@ -877,7 +888,12 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                     s = kServiceStop;
                     break;
                 }
-                if (direct && lead) {
+                if (lone && (readlane64(w, 48) & kServiceGangEpochMask) != epoch) {  // replaced by a full instance
+                    s = kServiceStop;
+                    superseded = true;
+                    break;
+                }
+                if (direct && lead && !lone) {
                     const unsigned long long s2 = readlane64(w, 31);  // the gang record's seq
                     if (s2 == kServiceStop) {  // the host parked it
                         s = kServiceStop;
@@ -894,10 +910,18 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
 #pragma unroll
                     for (int i = 0; i <= kServiceReqGang; i++) h = service_mix(h, readlane64(w, base + i));
                     if (h != readlane64(w, base + 14)) continue;  // seq landed before the rest: read it again
-                    // whole; a member of an earlier instance (started late) leaves a newer one's request alone
-                    if (lead || ((readlane64(w, base + kServiceReqGang) >> kServiceGangEpochShift) &
-                                 kServiceGangEpochMask) == epoch)
+                    // Whole. A member of an earlier instance (started late) leaves a newer one's
+                    // request alone; a lead that sees one has been replaced and leaves. A lone
+                    // lead takes no gang request (its members are gone: the host starts a
+                    // full instance for it).
+                    const unsigned long long g = readlane64(w, base + kServiceReqGang);
+                    const bool mine = ((g >> kServiceGangEpochShift) & kServiceGangEpochMask) == epoch;
+                    if (lead && !mine) {
+                        s = kServiceStop;
+                        superseded = true;
                         break;
+                    }
+                    if (mine && !(lone && (g & 0xFFFFull) > 1)) break;
                 }
                 // While part of the grid has not started (the roster is short) it waits
                 // longer (degraded_idle_ticks): the kernel cannot complete before those
@@ -905,17 +929,30 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
                 // device-wide sync no sooner, and every relaunch would need another
                 // stream while they wait (the pool is small).
                 if (lead &&
-                    __builtin_amdgcn_s_memrealtime() - idle_start > (roster >= gridDim.x ? idle_ticks : degraded_idle_ticks) &&
+                    __builtin_amdgcn_s_memrealtime() - idle_start >
+                        (lone ? lone_ticks : roster >= gridDim.x ? idle_ticks : degraded_idle_ticks) &&
                     (served || __builtin_amdgcn_s_memrealtime() - started > 2000000ull)) {
                     // Leave only once every member the last request named is done
                     // with it: a member that saw the STOP first would never serve it.
                     if (service_last_complete(slot, box, proto, last, last_gang)) {
-                        s = kServiceStop;
-                        break;
+                        if (lone || lone_ticks == 0) {
+                            s = kServiceStop;
+                            break;
+                        }
+                        // The members leave; the lead stays alone and says so (the host
+                        // then sizes no gang on this instance).
+                        lone = true;
+                        if (tid == 0) {
+                            __hip_atomic_store(&box->stop, first_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(&slot->lone, service_tag(epoch, last + 1), __ATOMIC_RELEASE,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                        }
                     }
                     idle_start = __builtin_amdgcn_s_memrealtime();
                 }
-                if (lead || direct)
+                if (lone)
+                    __builtin_amdgcn_s_sleep(24);  // ~0.6 us: one PCIe read of the record per poll
+                else if (lead || direct)
                     __builtin_amdgcn_s_sleep(8);  // ~0.2 us between PCIe polls
                 else
                     __builtin_amdgcn_s_sleep(1);
@@ -956,11 +993,10 @@ __global__ __launch_bounds__(kThreads) void service_kernel(const ServiceReq *rq,
         // Every member leaves when it sees this instance's first seq here (an
         // earlier instance's value never matches, so the box needs no clearing).
         __hip_atomic_store(&box->stop, first_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&slot->exited, last + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (!superseded)
+            __hip_atomic_store(&slot->exited, service_tag(epoch, last + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
-
-}  // namespace
 
 uint32_t service_gang_size(const XferArgs &a, unsigned blocks, unsigned solo_tiles) {
     const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
@@ -989,19 +1025,15 @@ void service_store_seq(ServiceReq *req, unsigned long long seq) {
     __builtin_ia32_sfence();
 }
 
-hipError_t service_launch(ServiceReq *req, ServiceReq *gang_req, ServiceSlot *slot, ServiceBox *box,
-                          unsigned long long first_seq, unsigned long long idle_ticks, unsigned blocks, unsigned proto,
-                          unsigned direct_wgs, unsigned long long checkin_base, bool reset_box, unsigned epoch,
-                          unsigned long long degraded_idle_ticks, hipStream_t stream) {
-    if (!req || !slot || !box || blocks == 0 || first_seq == 0 || (gang_req && direct_wgs == 0))
+hipError_t service_launch(const ServiceKernelArgs &args, unsigned blocks, bool reset_box, hipStream_t stream) {
+    if (!args.req || !args.slot || !args.box || blocks == 0 || args.first_seq == 0 ||
+        (args.gang_req && args.direct_wgs == 0) || args.epoch > kServiceGangEpochMask)
         return hipErrorInvalidValue;
     if (reset_box) {
-        hipError_t e = hipMemsetAsync(box, 0, sizeof(ServiceBox), stream);
+        hipError_t e = hipMemsetAsync(args.box, 0, sizeof(ServiceBox), stream);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(service_kernel, dim3(blocks), dim3(kThreads), 0, stream, req, gang_req, slot, box, first_seq,
-                       idle_ticks, proto, direct_wgs, checkin_base, epoch & (unsigned)kServiceGangEpochMask,
-                       degraded_idle_ticks);
+    hipLaunchKernelGGL(ocm_service_kernel, dim3(blocks), dim3(kThreads), 0, stream, args);
     return hipGetLastError();
 }
 // ---- verification patterns (benchmarks and tests check data without a host round trip) ----

@@ -31,6 +31,7 @@
 #include "ocm/shmlink.h"
 #include "ocm/sock.h"
 #include "ocm/trace.h"
+#include "ocm/aql.h"
 #include "ocm/xfer.h"
 
 
@@ -220,6 +221,8 @@ struct State {
     // (up to OCM_SERVICE_STREAMS, default 4), or waits for one. Requests carry the
     // instance's epoch (ocm/xfer.h), so such a late workgroup never takes one.
     struct SvcLane {
+        bool aql = false;                   // an AQL queue of the library's own (else `stream`)
+        AqlLane q;
         hipStream_t stream = nullptr;
         ServiceBox *box = nullptr;
         bool dirty = true;                  // clear the box before its next launch
@@ -227,6 +230,14 @@ struct State {
         unsigned long long gang_total = 0;  // the box's gang completion counter (mirror)
     };
     std::vector<SvcLane> svc_lanes;
+    // OCM_SERVICE_QUEUE=aql (default): lanes are AQL queues when the embedded code
+    // object loads (svc_aql), =hip: HIP streams.
+    bool svc_queue_aql = true, svc_aql = false;
+    AqlKernel svc_kernel;
+    // Lone lead (ocm/xfer.h): the lead stays resident alone this long after the
+    // members left (OCM_SERVICE_LONE_US; AQL lanes only, 100 MHz ticks).
+    unsigned long long svc_lone_ticks = 100ull * 200000;
+    uint64_t svc_promotions = 0;  // gang ops that replaced a lone lead with a full instance
     int svc_lane = -1;
     unsigned svc_lanes_max = 4;
     unsigned svc_epoch = 0;

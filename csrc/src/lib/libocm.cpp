@@ -151,6 +151,8 @@ int ocm_init(void) {
     s.svc_lanes_max = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_STREAMS", 4), 16));
     s.svc_relaunch_query = env_int("OCM_SERVICE_RELAUNCH_QUERY", 0) != 0;
     s.svc_degraded_idle_ticks = 100ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_DEGRADED_IDLE_US", 5000));
+    if (const char *v = std::getenv("OCM_SERVICE_QUEUE"); v && *v) s.svc_queue_aql = std::strcmp(v, "hip") != 0;
+    s.svc_lone_ticks = 100ull * (unsigned long long)std::max(0, env_int("OCM_SERVICE_LONE_US", 200000));
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");
     s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
     s.tuning = xfer_tuning_from_env();
@@ -963,20 +965,27 @@ void ocm_x_service_stats(uint64_t out[5]) {
 // roster a gang op was sized to (0: none yet), the current instance's roster,
 // relaunches after an idle exit, and the host ns they took (reap + launch), then
 // over every start: ns choosing a lane, ns in the launch call, starts}.
-void ocm_x_service_health(uint64_t out[11]) {
+// Then: 1 if the lanes are AQL queues of the library's own (0: HIP streams),
+// gang ops that replaced a lone lead with a full instance, 1 if the running
+// instance's lead is alone (its members left), and the lanes created.
+void ocm_x_service_health(uint64_t out[14]) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
+    const bool run = s.svc && s.svc_running;
     out[0] = s.svc_degraded;
     out[1] = s.svc_incomplete_exits;
     out[2] = s.svc_aborts;
     out[3] = s.svc_wedged ? 1 : 0;
     out[4] = s.svc_roster_min == ~0ull ? 0 : s.svc_roster_min;
-    out[5] = (s.svc && s.svc_running) ? __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE) : 0;
+    out[5] = run ? service_untag(s.svc_epoch, __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE)) : 0;
     out[6] = s.svc_relaunches;
     out[7] = s.svc_ns_relaunch;
     out[8] = s.svc_ns_pick;
     out[9] = s.svc_ns_launch;
     out[10] = s.svc_epoch_starts;
+    out[11] = s.svc_aql ? 1 : 0;
+    out[12] = s.svc_promotions;
+    out[13] = (run && service_untag(s.svc_epoch, __atomic_load_n(&s.svc->lone, __ATOMIC_ACQUIRE)) != 0) ? 1 : 0;
 }
 
 // Copy-service phase stamps of the last request (OCM_SERVICE_PROTO with the

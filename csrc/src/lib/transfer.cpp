@@ -130,20 +130,59 @@ int sync_stream() {
 }
 
 // ---- persistent copy service ----
+// Instances run on lanes: an AQL queue of the library's own (ocm/aql.h; HIP does
+// not know it, so a device-wide synchronize never waits for the service and the
+// lead may stay resident alone between bursts, OCM_SERVICE_LONE_US) or, when that
+// is unavailable or OCM_SERVICE_QUEUE=hip, a HIP stream of the service's priority
+// (then the whole instance leaves after OCM_SERVICE_IDLE_US).
 
-// A new lane: a stream of the service's priority and a gang box. -1 on failure.
+static bool lane_idle(State::SvcLane &l) {
+    if (l.aql) return aql_lane_idle(&l.q);
+    const hipError_t e = hipStreamQuery(l.stream);
+    (void)hipGetLastError();
+    return e == hipSuccess;
+}
+
+// Wait until every workgroup of the lane's last instance has left. 0: drained;
+// -1: not within timeout_ns.
+static int lane_drain(State::SvcLane &l, uint64_t timeout_ns) {
+    if (l.aql) return aql_lane_wait(&l.q, timeout_ns);
+    const uint64_t t0 = now_ns();
+    hipError_t e;
+    while ((e = hipStreamQuery(l.stream)) == hipErrorNotReady) {
+        if (now_ns() - t0 > timeout_ns) return -1;
+        usleep(20);
+    }
+    (void)hipGetLastError();
+    return 0;
+}
+
+// The current instance's tagged status words (ocm/xfer.h): 0 unless it wrote them.
+static unsigned long long svc_word(const unsigned long long *w) {
+    return service_untag(S().svc_epoch, __atomic_load_n(w, __ATOMIC_ACQUIRE));
+}
+
+// A new lane: an AQL queue or a stream of the service's priority, and a gang box. -1 on failure.
 static int service_new_lane() {
     State &s = S();
     State::SvcLane l;
-    hipError_t e = s.svc_prio_ok ? hipStreamCreateWithPriority(&l.stream, hipStreamNonBlocking, s.svc_stream_prio)
-                                 : hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        return -1;
+    if (s.svc_aql) {
+        if (aql_lane_create(&l.q, true) != 0) return -1;
+        l.aql = true;
+    } else {
+        hipError_t e = s.svc_prio_ok ? hipStreamCreateWithPriority(&l.stream, hipStreamNonBlocking, s.svc_stream_prio)
+                                     : hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return -1;
+        }
     }
     if (hipMalloc(reinterpret_cast<void **>(&l.box), sizeof(ServiceBox)) != hipSuccess) {
         (void)hipGetLastError();
-        (void)hipStreamDestroy(l.stream);
+        if (l.aql)
+            aql_lane_destroy(&l.q);
+        else
+            (void)hipStreamDestroy(l.stream);
         return -1;
     }
     l.dirty = true;  // fresh device memory: its first launch clears it
@@ -164,6 +203,21 @@ int service_start(unsigned long long first_seq) {
         }
         std::memset(s.svc, 0, sizeof(ServiceSlot));
         s.svc_req = &s.svc->req;
+        // The library's own AQL queue when the embedded code object loads for this
+        // device; otherwise HIP streams (and no lone lead: a device-wide synchronize
+        // would wait for it).
+        s.svc_aql = false;
+        if (s.svc_queue_aql) {
+            const char *why = nullptr;
+            if (aql_open(s.device, &why) != 0)
+                OCM_INFO("copy service on HIP streams: AQL queue unavailable (%s)", why ? why : "?");
+            else if (aql_kernel(kServiceKernelSymbol, &s.svc_kernel) != 0 ||
+                     s.svc_kernel.kernarg_bytes < sizeof(ServiceKernelArgs))
+                OCM_INFO("copy service on HIP streams: no usable %s in the embedded code object", kServiceKernelSymbol);
+            else
+                s.svc_aql = true;
+        }
+        if (!s.svc_aql) s.svc_lone_ticks = 0;
         // Streams of their own priority: HIP shares its few hardware queues
         // (GPU_MAX_HW_QUEUES) among a process's streams, and a launch on a stream
         // that shares the service's queue waits behind the persistent kernel until
@@ -175,7 +229,13 @@ int service_start(unsigned long long first_seq) {
         s.svc_prio_ok = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && lo != hi;
         (void)hipGetLastError();
         s.svc_stream_prio = env_int("OCM_SERVICE_STREAM_PRIO", hi);
-        if (service_new_lane() < 0 && s.svc_prio_ok) {
+        if (service_new_lane() < 0 && s.svc_aql) {
+            OCM_INFO("copy service on HIP streams: no AQL queue could be created");
+            s.svc_aql = false;
+            s.svc_lone_ticks = 0;
+            service_new_lane();
+        }
+        if (s.svc_lanes.empty() && s.svc_prio_ok) {
             s.svc_prio_ok = false;
             s.svc_shared_queue = true;  // launches park the service first (see xfer)
             service_new_lane();
@@ -204,36 +264,49 @@ int service_start(unsigned long long first_seq) {
         }
     }
     if (s.svc_wedged) OCM_FAIL(-1, "copy service: a previous instance could not be drained");
-    // A lane whose stream has drained: the current one normally (its last instance's
-    // workgroups leave microseconds after its lead), another drained one, a new one,
-    // or - every lane still holding workgroups that found no CU - wait for the current.
-    // When the last instance had its whole grid resident (its roster is still in the
-    // slot), its workgroups leave right behind its lead: stay on its lane without a
-    // runtime query (stream order starts the new instance after them; they ignore
-    // the new epoch meanwhile). A query costs a relaunch ~10 us of host time.
+    // A lane whose last instance has drained: the current one normally (its last
+    // instance's workgroups leave microseconds after its lead), another drained one,
+    // a new one, or - every lane still holding workgroups that found no CU, or a
+    // lone lead that has not yet seen it was replaced - wait for the current.
+    // HIP lanes: when the last instance had its whole grid resident (its roster is
+    // still in the slot), its workgroups leave right behind its lead: stay on its
+    // lane without a runtime query (stream order starts the new instance after them;
+    // they ignore the new epoch meanwhile). A stream query costs ~10 us of host
+    // time; an AQL lane's is one load of its completion signal.
     const uint64_t tq = now_ns();
     int pick = -1;
     const int n = (int)s.svc_lanes.size();
-    if (s.svc_lane >= 0 && !s.svc_relaunch_query &&
-        __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE) >= (unsigned long long)s.svc_blocks)
+    if (!s.svc_aql && s.svc_lane >= 0 && !s.svc_relaunch_query && svc_word(&s.svc->roster) >= s.svc_blocks)
         pick = s.svc_lane;
     for (int k = 0; k < n && pick < 0; k++) {
         const int i = (s.svc_lane + k) % n;
-        if (hipStreamQuery(s.svc_lanes[(size_t)i].stream) == hipSuccess) pick = i;
+        if (lane_idle(s.svc_lanes[(size_t)i])) pick = i;
     }
-    (void)hipGetLastError();
     if (pick < 0 && (unsigned)n < s.svc_lanes_max) pick = service_new_lane();
     if (pick < 0) {
         pick = s.svc_lane;
-        (void)hipStreamSynchronize(s.svc_lanes[(size_t)pick].stream);
-        (void)hipGetLastError();
+        if (s.svc_lanes[(size_t)pick].aql) {
+            // a lone lead on it leaves once it sees the new epoch
+            __atomic_store_n(&s.svc->epoch_now, (unsigned long long)((s.svc_epoch + 1) & (unsigned)kServiceGangEpochMask),
+                             __ATOMIC_RELEASE);
+            __builtin_ia32_sfence();
+        }
+        if (lane_drain(s.svc_lanes[(size_t)pick], s.svc_drain_ns) != 0) {
+            s.svc_wedged = true;
+            s.svc_max = 0;
+            OCM_FAIL(-1, "copy service: no lane drained within OCM_SERVICE_DRAIN_MS");
+        }
     }
     s.svc_lane = pick;
     State::SvcLane &l = s.svc_lanes[(size_t)pick];
     s.svc_stream = l.stream;
     s.svc_box = l.box;
+    s.svc_epoch = (s.svc_epoch + 1) & (unsigned)kServiceGangEpochMask;
     __atomic_store_n(&s.svc->exited, 0ull, __ATOMIC_RELEASE);
     __atomic_store_n(&s.svc->roster, 0ull, __ATOMIC_RELEASE);  // the new lead publishes its own
+    __atomic_store_n(&s.svc->lone, 0ull, __ATOMIC_RELEASE);
+    // A lone lead of an earlier instance (another lane) leaves when it sees this.
+    __atomic_store_n(&s.svc->epoch_now, (unsigned long long)s.svc_epoch, __ATOMIC_RELEASE);
     service_store_seq(s.svc_req, 0ull);  // clear a STOP left by a parked instance
     if (s.svc_greq) service_store_seq(s.svc_greq, 0ull);
     // the gang counter mirror stays below the 31-bit target field (ocm/xfer.h)
@@ -242,12 +315,35 @@ int service_start(unsigned long long first_seq) {
         l.gang_total = 0;  // the launch zeroes the device counters
         l.checkins = 0;
     }
-    s.svc_epoch = (s.svc_epoch + 1) & (unsigned)kServiceGangEpochMask;
+    ServiceKernelArgs ka;
+    std::memset(&ka, 0, sizeof(ka));
+    ka.req = s.svc_req;
+    ka.gang_req = s.svc_greq;
+    ka.slot = s.svc;
+    ka.box = l.box;
+    ka.first_seq = first_seq;
+    ka.idle_ticks = s.svc_idle_ticks;
+    ka.proto = s.svc_proto;
+    ka.direct_wgs = std::min(s.svc_direct, s.svc_blocks);
+    ka.checkin_base = l.checkins;
+    ka.epoch = s.svc_epoch;
+    ka.degraded_idle_ticks = s.svc_degraded_idle_ticks;
+    ka.lone_ticks = l.aql ? s.svc_lone_ticks : 0;
     const uint64_t tl = now_ns();
     s.svc_ns_pick += tl - tq;
-    if (service_launch(s.svc_req, s.svc_greq, s.svc, l.box, first_seq, s.svc_idle_ticks, s.svc_blocks, s.svc_proto,
-                       std::min(s.svc_direct, s.svc_blocks), l.checkins, reset, s.svc_epoch,
-                       s.svc_degraded_idle_ticks, l.stream) != hipSuccess) {
+    if (l.aql) {
+        // the box is cleared before the dispatch (the queue is not a HIP stream)
+        if (reset && (hipMemsetAsync(l.box, 0, sizeof(ServiceBox), s.stream) != hipSuccess ||
+                      hipStreamSynchronize(s.stream) != hipSuccess)) {
+            (void)hipGetLastError();
+            s.svc_max = 0;
+            OCM_FAIL(-1, "copy service: clearing the gang box failed");
+        }
+        if (aql_dispatch(&l.q, s.svc_kernel, &ka, sizeof(ka), s.svc_blocks, 256) != 0) {
+            s.svc_max = 0;
+            OCM_FAIL(-1, "copy service dispatch failed");
+        }
+    } else if (service_launch(ka, s.svc_blocks, reset, l.stream) != hipSuccess) {
         (void)hipGetLastError();
         s.svc_max = 0;
         OCM_FAIL(-1, "copy service launch failed");
@@ -278,7 +374,16 @@ void service_park() {
     DeviceGuard g(s.device);
     service_store_seq(s.svc_req, kServiceStop);
     if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
-    (void)hipStreamSynchronize(s.svc_stream);
+    State::SvcLane &l = s.svc_lanes[(size_t)s.svc_lane];
+    if (l.aql) {
+        if (lane_drain(l, s.svc_drain_ns) != 0) {
+            s.svc_wedged = true;
+            s.svc_max = 0;
+            OCM_WARN("copy service did not leave on STOP within OCM_SERVICE_DRAIN_MS; the service is off");
+        }
+    } else {
+        (void)hipStreamSynchronize(l.stream);
+    }
     s.svc_running = false;
 }
 
@@ -286,14 +391,21 @@ void service_stop() {
     State &s = S();
     if (!s.svc) return;
     DeviceGuard g(s.device);
-    if (s.svc_running) {
-        service_store_seq(s.svc_req, kServiceStop);
-        if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
-        s.svc_running = false;
-    }
+    service_store_seq(s.svc_req, kServiceStop);
+    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
+    s.svc_running = false;
     for (State::SvcLane &l : s.svc_lanes) {  // every lane drained before its box goes
-        (void)hipStreamSynchronize(l.stream);
-        (void)hipStreamDestroy(l.stream);
+        if (l.aql) {
+            if (lane_drain(l, s.svc_drain_ns) != 0) {
+                // never free what a kernel that did not leave may still touch
+                OCM_WARN("copy service: a lane did not drain at shutdown; its queue and box are leaked");
+                continue;
+            }
+            aql_lane_destroy(&l.q);
+        } else {
+            (void)hipStreamSynchronize(l.stream);
+            (void)hipStreamDestroy(l.stream);
+        }
         if (l.box) (void)hipFree(l.box);
     }
     s.svc_lanes.clear();
@@ -313,10 +425,10 @@ void service_stop() {
 // then settle for the ones that did (at least workgroup 0).
 static unsigned service_roster(unsigned want) {
     State &s = S();
-    unsigned long long r = __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE);
+    unsigned long long r = svc_word(&s.svc->roster);
     while (r < want && now_ns() - s.svc_launch_ns < s.svc_roster_wait_ns) {
         __builtin_ia32_pause();
-        r = __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE);
+        r = svc_word(&s.svc->roster);
     }
     if (r < 1) r = 1;
     if (r < want) s.svc_degraded++;
@@ -333,24 +445,18 @@ static int service_abort(unsigned long long seq, unsigned long long active, cons
     unsigned long long wg_in = 0;
     for (unsigned long long i = 0; i < active && i < (unsigned long long)kServiceWgDoneMax; i++)
         wg_in += __atomic_load_n(&s.svc->wg_done[i], __ATOMIC_ACQUIRE) == seq;
-    const unsigned long long ex = __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE);
-    const unsigned long long roster = __atomic_load_n(&s.svc->roster, __ATOMIC_ACQUIRE);
+    const unsigned long long ex = svc_word(&s.svc->exited);
+    const unsigned long long roster = svc_word(&s.svc->roster);
     service_store_seq(s.svc_req, kServiceStop);
     if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
     s.svc_aborts++;
-    const uint64_t t0 = now_ns();
-    hipError_t e;
-    while ((e = hipStreamQuery(s.svc_stream)) == hipErrorNotReady) {
-        if (now_ns() - t0 > s.svc_drain_ns) {
-            s.svc_wedged = true;
-            s.svc_max = 0;
-            OCM_FAIL(-2, "copy service %s (seq %llu, %llu members, %llu done words, roster %llu, exited %llu) "
-                         "and did not leave on STOP: not redoing the op",
-                     why, seq, active, wg_in, roster, ex);
-        }
-        usleep(100);
+    if (lane_drain(s.svc_lanes[(size_t)s.svc_lane], s.svc_drain_ns) != 0) {
+        s.svc_wedged = true;
+        s.svc_max = 0;
+        OCM_FAIL(-2, "copy service %s (seq %llu, %llu members, %llu done words, roster %llu, exited %llu) "
+                     "and did not leave on STOP: not redoing the op",
+                 why, seq, active, wg_in, roster, ex);
     }
-    (void)hipGetLastError();
     s.svc_running = false;
     if (s.svc_lane >= 0) s.svc_lanes[(size_t)s.svc_lane].dirty = true;
     OCM_FAIL(-1, "copy service %s (seq %llu, %llu members, %llu done words, roster %llu, exited %llu); drained",
@@ -368,7 +474,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
     unsigned long long seq = ++s.svc_seq;
     const uint64_t t_enter = now_ns();
     bool relaunched = false;
-    if (s.svc_running && __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE) != 0) {
+    if (s.svc_running && svc_word(&s.svc->exited) != 0) {
         // The instance left on its idle timeout (OCM_SERVICE_IDLE_US), its last request
         // complete: start the next one right away instead of posting to nobody. No wait
         // for its stream: the next instance takes a drained lane, and a workgroup of the
@@ -389,10 +495,18 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
     bool wgdone = false;
     ServiceReq *rq = s.svc_req;
     unsigned long long gang = 0;
-    auto size_and_post = [&]() {
+    auto size_and_post = [&]() -> int {
         unsigned width = direct ? std::min(s.svc_direct, s.svc_blocks)
                                 : (hbm ? s.svc_blocks : std::min(s.svc_gang_host, s.svc_blocks));
-        if (service_gang_size(x, width, solo_tiles) > 1) width = service_roster(width);
+        if (service_gang_size(x, width, solo_tiles) > 1) {
+            // A lone lead takes no gang: a full instance replaces it (the lead leaves
+            // on the new epoch by itself; it holds no request of ours).
+            if (svc_word(&s.svc->lone) != 0) {
+                s.svc_promotions++;
+                if (service_start(seq) != 0) return -1;
+            }
+            width = service_roster(width);
+        }
         active = service_gang_size(x, width, solo_tiles);
         wgdone = service_wg_done(s.svc_proto, active);
         unsigned long long target = 0;
@@ -406,6 +520,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
         // GANGREC: gang requests go to the record the whole gang polls.
         rq = (active > 1 && s.svc_greq) ? s.svc_greq : s.svc_req;
         service_post(rq, x, gang, seq);
+        return 0;
     };
     // Completed: `done` (a solo op or the gang's last member), or under WGDONE
     // every member's own word.
@@ -416,7 +531,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
         return true;
     };
     const uint64_t t0 = now_ns();
-    size_and_post();
+    if (size_and_post() != 0) return -1;
     const uint64_t t_posted = now_ns();
     for (unsigned spins = 1;; spins++) {
         if (finished()) {
@@ -430,12 +545,20 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
             // last request it took is complete. If it left before taking this one
             // (exited <= seq), start a new instance for it. exited > seq with the
             // op unfinished is not expected (workgroup 0 waits for its members):
-            // counted, and handled the same way, since after the stream sync no
-            // member of the old instance is left to finish it.
-            const unsigned long long ex = __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE);
-            if (ex) {
+            // counted, and handled the same way, since after the drain no member
+            // of the old instance is left to finish it. The same when the members
+            // of the instance left (a lone lead) before this gang request: the lead
+            // is told to leave too, and the op goes to a new instance.
+            const unsigned long long ex = svc_word(&s.svc->exited);
+            const unsigned long long ln = active > 1 ? svc_word(&s.svc->lone) : 0;
+            if (ex || (ln && ln <= seq)) {
                 DeviceGuard g(s.device);
-                (void)hipStreamSynchronize(s.svc_stream);
+                if (!ex) {
+                    service_store_seq(s.svc_req, kServiceStop);
+                    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
+                }
+                if (lane_drain(s.svc_lanes[(size_t)s.svc_lane], s.svc_drain_ns) != 0)
+                    return service_abort(seq, active, "left part of a request behind and did not drain");
                 s.svc_running = false;
                 s.svc_relaunches++;
                 if (finished()) {
@@ -453,7 +576,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
                 // the copy: tests/test_gpu_service.py::test_service_direct_and_relayed_gangs_interleave).
                 seq = ++s.svc_seq;
                 if (service_start(seq) != 0) return -1;
-                size_and_post();  // sized to the new instance's roster; start cleared the doorbell
+                if (size_and_post() != 0) return -1;  // sized to the new instance's roster; start cleared the doorbell
             }
             if (now_ns() - t0 > s.svc_timeout_ns) return service_abort(seq, active, "did not complete a transfer in time");
         }

@@ -358,11 +358,13 @@ def xgmi_diag() -> dict:
 
 
 def quiesce() -> None:
-    """Park this process's resident copy service now. Optional: the service
-    leaves by itself OCM_SERVICE_IDLE_US (50 us) after its last op, so a
-    device-wide synchronize (torch.cuda.synchronize) right after a small blocking
-    op waits at most that long; quiesce() removes even that wait. The next op
-    relaunches the service. No-op without a GPU or before any op."""
+    """Park this process's resident copy service now. Optional: on the library's
+    AQL queues (the default) a device-wide synchronize never waits for the
+    service; on HIP streams (OCM_SERVICE_QUEUE=hip) the service leaves by itself
+    OCM_SERVICE_IDLE_US (50 us) after its last op, so torch.cuda.synchronize right
+    after a small blocking op waits at most that long, and quiesce() removes even
+    that wait. The next op relaunches the service. No-op without a GPU or before
+    any op."""
     load().ocm_x_quiesce()
 
 
@@ -387,8 +389,13 @@ def service_health() -> dict:
     (`aborts`), whether an instance could not be drained at all (`wedged`), the
     smallest roster a gang op was sized to (`roster_min`, 0: none yet), the
     running instance's roster (`roster`, 0: not running), and the relaunches after
-    an idle exit with their mean host time (reap + launch, microseconds)."""
-    out = (ctypes.c_uint64 * 11)()
+    an idle exit with their mean host time (reap + launch, microseconds). `queue`:
+    "aql" when the service runs on the library's own AQL queues (a device-wide
+    synchronize never waits for it, and its lead may stay resident alone between
+    bursts, OCM_SERVICE_LONE_US), "hip" on HIP streams; `promotions`: gang ops that
+    replaced a lone lead with a full instance; `lone`: the running instance's lead
+    is alone."""
+    out = (ctypes.c_uint64 * 14)()
     load().ocm_x_service_health(out)
     n, k = int(out[6]), int(out[10])
     return {"degraded": int(out[0]), "incomplete_exits": int(out[1]), "aborts": int(out[2]),
@@ -396,7 +403,8 @@ def service_health() -> dict:
             "relaunch_host_us_mean": round(out[7] / n / 1e3, 2) if n else None,
             # every start, split: choosing a lane (runtime stream queries) / the launch call itself
             "start_pick_us_mean": round(out[8] / k / 1e3, 2) if k else None,
-            "start_launch_us_mean": round(out[9] / k / 1e3, 2) if k else None}
+            "start_launch_us_mean": round(out[9] / k / 1e3, 2) if k else None,
+            "queue": "aql" if out[11] else "hip", "promotions": int(out[12]), "lone": bool(out[13])}
 
 
 def tick_stats() -> dict | None:

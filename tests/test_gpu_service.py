@@ -74,13 +74,19 @@ def test_service_never_reads_stale_bytes(mesh_factory, rounds):
             a.free()
 
 
-def test_service_restarts_after_idle_exit(mesh_factory):
-    # The service leaves after OCM_SERVICE_IDLE_US without work (workgroup 0 stores
-    # STOP for the gang); the next op relaunches it. Alternate gang-sized and solo ops across exits.
+@pytest.mark.parametrize("queue", ["aql", "hip"])
+def test_service_restarts_after_idle_exit(mesh_factory, monkeypatch, queue):
+    # After OCM_SERVICE_IDLE_US without work the members leave (workgroup 0 stores
+    # STOP for the gang). On HIP streams the lead leaves with them and the next op
+    # relaunches the service; on the library's AQL queue the lead stays alone
+    # (lone) and serves solo ops itself, and a gang op replaces it with a full
+    # instance (a promotion). Alternate gang-sized and solo ops across idle gaps.
+    monkeypatch.setenv("OCM_SERVICE_QUEUE", queue)
     m = mesh_factory(1, gpus=[0])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         n = 1 << 20
         a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_LOOPBACK)
+        st0, h0 = api.service_stats(), api.service_health()
         for i in range(12):
             size = n if i % 2 else 8192
             a.fill(seed=50 + i, nbytes=size)
@@ -89,10 +95,113 @@ def test_service_restarts_after_idle_exit(mesh_factory):
             a.get(0, 0, size)
             assert a.check(seed=50 + i, nbytes=size) == 0, f"op pair {i}"
             time.sleep(0.005)
-        st = api.service_stats()
-        assert st["ops"] >= 24
-        assert st["relaunches"] >= 10, st  # every 5 ms sleep outlasted the idle exit
+        st, h = api.service_stats(), api.service_health()
+        assert st["ops"] - st0["ops"] >= 24
+        if h["queue"] == "aql":
+            assert h["promotions"] - h0["promotions"] >= 5, h  # every gang op after a gap replaced the lone lead
+            assert st["relaunches"] == st0["relaunches"], st  # the lone lead never left (200 ms window)
+        else:
+            assert queue == "hip", f"the AQL queue did not come up: {h}"
+            assert st["relaunches"] - st0["relaunches"] >= 10, st  # every 5 ms sleep outlasted the idle exit
         a.free()
+
+
+def test_service_lanes_are_aql_queues(mesh_factory):
+    # The default lanes are AQL queues of the library's own, running the service
+    # kernel from the device code object embedded in libocm.so (ocm/aql.h).
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=4096, flags=api.OCM_ALLOC_HOST_TIER)
+        a.fill(seed=5, nbytes=4096)
+        a.put(0, 0, 4096)
+        a.fill(seed=0, nbytes=4096)
+        a.get(0, 0, 4096)
+        assert a.check(seed=5, nbytes=4096) == 0
+        h = api.service_health()
+        assert h["queue"] == "aql", h
+        a.free()
+
+
+def _busy_wait(s):
+    t = time.perf_counter() + s
+    while time.perf_counter() < t:
+        pass
+
+
+@pytest.mark.parametrize("tier", ["host", "hbm"])
+def test_small_ops_after_idle_gaps_stay_hot(mesh_factory, tier):
+    # a 4 KiB op after 1 ms of host idle must cost at most twice
+    # a back-to-back one. The lone lead stays resident on the AQL queue, so the op
+    # after the gap is a poll away (no relaunch), and meanwhile a device-wide
+    # synchronize does not wait for it.
+    m = mesh_factory(1, gpus=[0])
+    flags = api.OCM_ALLOC_HOST_TIER if tier == "host" else api.OCM_ALLOC_LOOPBACK
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 4096
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=flags)
+        hot, _ = a.time_onesided_samples(0, n, 200)
+        r0 = api.service_stats()["relaunches"]
+        gap, rel = a.time_onesided_samples(0, n, 100, gap_s=1e-3)
+        hot.sort()
+        gap.sort()
+        h = api.service_health()
+        syncs = []
+        for _ in range(20):
+            a.get(0, 0, n)
+            _busy_wait(1e-3)  # the members have left; the lead is alone and resident
+            t0 = time.perf_counter()
+            torch.cuda.synchronize()
+            syncs.append(time.perf_counter() - t0)
+        syncs.sort()
+        lone = api.service_health()["lone"]
+        a.fill(seed=8, nbytes=n)
+        a.put(0, 0, n)
+        a.fill(seed=0, nbytes=n)
+        a.get(0, 0, n)
+        assert a.check(seed=8, nbytes=n) == 0
+        p50_hot, p50_gap = hot[len(hot) // 2], gap[len(gap) // 2]
+        print(f"{tier}: 4 KiB get p50 {p50_hot * 1e6:.2f} us back to back, {p50_gap * 1e6:.2f} us after 1 ms idle; "
+              f"relaunches {rel}; device sync with the lone lead resident: median {syncs[10] * 1e6:.1f} us; {h}")
+        assert h["queue"] == "aql", h
+        assert lone, "the lead did not stay resident through a 1 ms gap"
+        assert rel == 0 and api.service_stats()["relaunches"] == r0
+        assert p50_gap <= 2 * p50_hot, (p50_hot, p50_gap)
+        assert syncs[10] < 200e-6, f"device sync waited for the resident service: {syncs[10] * 1e6:.0f} us"
+        a.free()
+
+
+@pytest.mark.parametrize("idle_us", ["50", "5"])
+def test_gang_ops_racing_the_lone_transition(mesh_factory, monkeypatch, idle_us):
+    # Gang ops posted right around the moment the members leave (host gaps drawn
+    # around the idle window): a gang request can land after the lead decided to go
+    # lone but before the host saw it. The library then stops the lone lead, waits
+    # for its lane to drain (a direct member may have served part of the request)
+    # and re-posts to a full instance. Every byte is checked; no op may time out.
+    import random
+
+    monkeypatch.setenv("OCM_SERVICE_IDLE_US", idle_us)
+    rng = random.Random(int(idle_us))
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 4 << 20
+        hbm = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_LOOPBACK)
+        host = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_HOST_TIER)
+        h0 = api.service_health()
+        for i in range(60):
+            a = hbm if i % 2 else host
+            size = rng.choice([8192, 96 << 10, 512 << 10, 2 << 20, 4 << 20])
+            a.fill(seed=700 + i, nbytes=size)
+            _busy_wait(rng.uniform(0.5, 1.5) * int(idle_us) * 1e-6)
+            a.put(0, 0, size)
+            a.fill(seed=0, nbytes=size)
+            _busy_wait(rng.uniform(0.5, 1.5) * int(idle_us) * 1e-6)
+            a.get(0, 0, size)
+            assert a.check(seed=700 + i, nbytes=size) == 0, f"op pair {i} ({size} B)"
+        h = api.service_health()
+        print(f"idle {idle_us} us: {h}")
+        assert h["promotions"] > h0["promotions"], h
+        hbm.free()
+        host.free()
 
 
 @pytest.mark.parametrize("idle_us", ["50", "1"])

@@ -59,3 +59,31 @@ def test_example_nodefiles_parse(native, tool):
     rc, out = tool([f"{native}/ocm_unit_tests", "--nodefile", *files])
     assert rc == 0, out
     assert "OK" in out and "16 daemons" in out and "8 daemons" in out
+
+
+def test_embedded_service_code_object_layout(native):
+    # libocm dispatches the copy service on its own AQL queue from a device code
+    # object embedded at build time (ocm/aql.h), writing the explicit arguments
+    # (ServiceKernelArgs, 88 bytes) and then the COv5 hidden arguments the kernel
+    # reads at fixed offsets after them. Check those offsets in the code object's
+    # metadata, and that the object is inside libocm.so.
+    import os
+    import re
+    import subprocess
+
+    from oncilla_amd.utils.paths import lib_path
+
+    co = os.path.join(os.path.dirname(os.path.dirname(lib_path())), "ocm_devcode.co")
+    notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co], capture_output=True, text=True,
+                           check=True).stdout
+    assert "amdgcn-amd-amdhsa--gfx950" in notes
+    kern = [k for k in re.split(r"\n  - ", notes) if re.search(r"\.name:\s+ocm_service_kernel\s", k)]
+    assert len(kern) == 1, "ocm_service_kernel missing from the embedded code object"
+    args = {kind: (int(off), int(size)) for off, size, kind in
+            re.findall(r"\.offset:\s+(\d+)\s+\.size:\s+(\d+)\s+\.value_kind:\s+(\S+)", kern[0])}
+    assert args["by_value"] == (0, 88), args
+    assert args["hidden_block_count_x"][0] == 88 and args["hidden_group_size_x"][0] == 100, args
+    assert args["hidden_grid_dims"][0] == 88 + 64, args
+    assert int(re.search(r"\.kernarg_segment_size:\s+(\d+)", kern[0]).group(1)) <= 4096
+    blob = open(co, "rb").read()
+    assert blob[:4] == b"\x7fELF" and blob in open(lib_path(), "rb").read()

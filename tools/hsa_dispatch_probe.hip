@@ -50,6 +50,7 @@ extern "C" __global__ __launch_bounds__(256) void probe_persist_kernel(const uns
         if (s || __builtin_amdgcn_s_memrealtime() - t0 > max_ticks) break;
         __builtin_amdgcn_s_sleep(8);
     }
+    if (threadIdx.x == 0 && blockIdx.x == 0) __hip_atomic_store(alive, 2ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 #define CHK(x)                                                                                 \
@@ -288,38 +289,51 @@ int main(int argc, char **argv) {
     unsigned long long bad = 0;
     for (unsigned long long i = 0; i < words; i++) bad += host[i] != (unsigned)(i * 2654435761u);
     // ---- device sync while a persistent kernel is resident ----
-    auto persist_sync = [&](bool on_hsa) -> double {
-        flags[32] = 0;  // stop
-        flags[48] = 0;  // alive
+    // stop word in `stopw` (coherent or write-combined host memory); returns the device
+    // sync time and, in *stop_us, the time from the host's stop store to the kernel's exit flag
+    unsigned long long *wc = nullptr;
+    if (hipHostMalloc((void **)&wc, 4096, hipHostMallocWriteCombined | hipHostMallocMapped) != hipSuccess) return 1;
+    wc[0] = 0;
+    auto persist_sync = [&](bool on_hsa, unsigned long long *stopw, double *stop_us) -> double {
+        __atomic_store_n(stopw, 0ull, __ATOMIC_RELEASE);
+        flags[48] = 0;  // alive: 1 running, 2 left
         struct {
             const unsigned long long *stop;
             unsigned long long *alive;
             unsigned long long max_ticks;
-        } args{flags + 32, flags + 48, 100ull * 200000};  // 200 ms
+        } args{stopw, flags + 48, 100ull * 200000};  // 200 ms
         hsa_signal_store_relaxed(sig, 1);
         if (on_hsa)
             dispatch(q, kpers, ka, &args, sizeof(args), 4, sig);
         else
-            hipLaunchKernelGGL(probe_persist_kernel, dim3(4), dim3(256), 0, st, flags + 32, flags + 48, 100ull * 200000);
+            hipLaunchKernelGGL(probe_persist_kernel, dim3(4), dim3(256), 0, st, stopw, flags + 48, 100ull * 200000);
         if (!spin_until(flags + 48, 1)) return -1;
+        clk::time_point ts;
         std::thread stopper([&]() {
             std::this_thread::sleep_for(std::chrono::milliseconds(5));
-            __atomic_store_n(flags + 32, 1ull, __ATOMIC_RELEASE);
+            ts = clk::now();
+            __atomic_store_n(stopw, 1ull, __ATOMIC_RELEASE);
+            __builtin_ia32_sfence();
         });
         const auto a = clk::now();
         (void)hipDeviceSynchronize();
         const double t = std::chrono::duration<double>(clk::now() - a).count();
         stopper.join();
+        fails += !spin_until(flags + 48, 2);
+        *stop_us = std::chrono::duration<double>(clk::now() - ts).count() * 1e6;
         if (on_hsa) fails += !wait_sig();
         (void)hipDeviceSynchronize();
         return t * 1e6;
     };
-    const double s_hsa = persist_sync(true);
-    const double s_hip = persist_sync(false);
+    double stop_hsa = 0, stop_hip = 0, stop_wc = 0;
+    const double s_hsa = persist_sync(true, flags + 32, &stop_hsa);
+    const double s_hip = persist_sync(false, flags + 32, &stop_hip);
+    double s_wc = persist_sync(true, wc, &stop_wc);
     std::printf("{\"hip_flag_us\": %.2f, \"hsa_flag_us\": %.2f, \"hip_launch_cpu_us\": %.2f, \"hsa_dispatch_cpu_us\": %.2f, "
-                "\"sync_while_hsa_resident_us\": %.1f, \"sync_while_hip_resident_us\": %.1f, \"interop_bad\": %llu, "
+                "\"sync_while_hsa_resident_us\": %.1f, \"sync_while_hip_resident_us\": %.1f, \"sync_hsa_wc_us\": %.1f, "
+                "\"stop_seen_us\": [%.1f, %.1f, %.1f], \"interop_bad\": %llu, "
                 "\"kernarg_bytes\": [%u, %u, %u], \"fails\": %d}\n",
-                p50(t_hip), p50(t_hsa), p50(c_hip), p50(c_hsa), s_hsa, s_hip, bad, kflag.kernarg, kfill.kernarg,
+                p50(t_hip), p50(t_hsa), p50(c_hip), p50(c_hsa), s_hsa, s_hip, s_wc, stop_hsa, stop_hip, stop_wc, bad, kflag.kernarg, kfill.kernarg,
                 kpers.kernarg, fails);
     (void)hsa_signal_destroy(sig);
     (void)hsa_amd_memory_pool_free(ka);
@@ -329,6 +343,7 @@ int main(int argc, char **argv) {
     (void)hsa_shut_down();
     (void)hipFree(dbuf);
     (void)hipHostFree(flags);
+    (void)hipHostFree(wc);
     return (fails || bad) ? 1 : 0;
 }
 

@@ -19,6 +19,7 @@ VARIANTS = {
     "query": {"OCM_SERVICE_RELAUNCH_QUERY": "1"},        # round-4 first cut: ask the runtime on every relaunch
     "reset": {"OCM_SERVICE_BOX_RESET": "1", "OCM_SERVICE_RELAUNCH_QUERY": "1"},  # + clear the box (round 3)
     "idle200": {"OCM_SERVICE_IDLE_US": "200"},
+    "hip": {"OCM_SERVICE_QUEUE": "hip"},  # round-4 start: HIP stream lanes, no lone lead
 }
 
 
