@@ -151,7 +151,10 @@ int ocm_init(void) {
     s.svc_lanes_max = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_STREAMS", 4), 16));
     s.svc_relaunch_query = env_int("OCM_SERVICE_RELAUNCH_QUERY", 0) != 0;
     s.svc_degraded_idle_ticks = 100ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_DEGRADED_IDLE_US", 5000));
-    if (const char *v = std::getenv("OCM_SERVICE_QUEUE"); v && *v) s.svc_queue_aql = std::strcmp(v, "hip") != 0;
+    {
+        const char *v = std::getenv("OCM_SERVICE_QUEUE");  // State outlives ocm_tini: set it on every init
+        s.svc_queue_aql = !(v && std::strcmp(v, "hip") == 0);
+    }
     s.svc_lone_ticks = 100ull * (unsigned long long)std::max(0, env_int("OCM_SERVICE_LONE_US", 200000));
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");
     s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
