@@ -935,7 +935,11 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
                     // Leave only once every member the last request named is done
                     // with it: a member that saw the STOP first would never serve it.
                     if (service_last_complete(slot, box, proto, last, last_gang)) {
-                        if (lone || lone_ticks == 0) {
+                        // Only an instance whose whole grid has started goes lone: one with
+                        // workgroups still waiting for a CU leaves whole, as its lane drains
+                        // only once they have started (and left at once), and the full
+                        // instance that would replace a lone lead needs a drained lane.
+                        if (lone || lone_ticks == 0 || roster < gridDim.x) {
                             s = kServiceStop;
                             break;
                         }
