@@ -313,7 +313,7 @@ struct ServiceKernelArgs {
     unsigned direct_wgs;
     unsigned long long checkin_base;
     unsigned epoch;
-    unsigned pad0;
+    unsigned blocks;  // the grid (the kernel never reads gridDim: a hidden argument it would reload in its loops)
     unsigned long long degraded_idle_ticks;
     unsigned long long lone_ticks;
 };

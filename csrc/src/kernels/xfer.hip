@@ -819,7 +819,7 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
     ServiceBox *box = ka.box;
     const unsigned long long first_seq = ka.first_seq, idle_ticks = ka.idle_ticks, checkin_base = ka.checkin_base;
     const unsigned long long degraded_idle_ticks = ka.degraded_idle_ticks, lone_ticks = ka.lone_ticks;
-    const unsigned proto = ka.proto, direct_wgs = ka.direct_wgs, epoch = ka.epoch;
+    const unsigned proto = ka.proto, direct_wgs = ka.direct_wgs, epoch = ka.epoch, grid = ka.blocks;
     __shared__ __attribute__((aligned(16))) unsigned long long sh[16];
     __shared__ unsigned sh_id;
     const int tid = threadIdx.x;
@@ -861,7 +861,7 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
             // (args, gang word, sum, seq); a seq whose hash checks out is whole.
             unsigned long long w = 0, s;
             for (;;) {
-                const bool count = lead && !lone && roster < gridDim.x;  // wave-uniform
+                const bool count = lead && !lone && roster < grid;  // wave-uniform
                 if (tid < 16)
                     w = (lead || direct) ? __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                          : __hip_atomic_load(req + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -930,7 +930,7 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
                 // stream while they wait (the pool is small).
                 if (lead &&
                     __builtin_amdgcn_s_memrealtime() - idle_start >
-                        (lone ? lone_ticks : roster >= gridDim.x ? idle_ticks : degraded_idle_ticks) &&
+                        (lone ? lone_ticks : roster >= grid ? idle_ticks : degraded_idle_ticks) &&
                     (served || __builtin_amdgcn_s_memrealtime() - started > 2000000ull)) {
                     // Leave only once every member the last request named is done
                     // with it: a member that saw the STOP first would never serve it.
@@ -939,7 +939,7 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
                         // workgroups still waiting for a CU leaves whole, as its lane drains
                         // only once they have started (and left at once), and the full
                         // instance that would replace a lone lead needs a drained lane.
-                        if (lone || lone_ticks == 0 || roster < gridDim.x) {
+                        if (lone || lone_ticks == 0 || roster < grid) {
                             s = kServiceStop;
                             break;
                         }
@@ -1030,7 +1030,7 @@ void service_store_seq(ServiceReq *req, unsigned long long seq) {
 }
 
 hipError_t service_launch(const ServiceKernelArgs &args, unsigned blocks, bool reset_box, hipStream_t stream) {
-    if (!args.req || !args.slot || !args.box || blocks == 0 || args.first_seq == 0 ||
+    if (!args.req || !args.slot || !args.box || blocks == 0 || blocks != args.blocks || args.first_seq == 0 ||
         (args.gang_req && args.direct_wgs == 0) || args.epoch > kServiceGangEpochMask)
         return hipErrorInvalidValue;
     if (reset_box) {

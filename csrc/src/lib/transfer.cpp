@@ -327,6 +327,7 @@ int service_start(unsigned long long first_seq) {
     ka.direct_wgs = std::min(s.svc_direct, s.svc_blocks);
     ka.checkin_base = l.checkins;
     ka.epoch = s.svc_epoch;
+    ka.blocks = s.svc_blocks;
     ka.degraded_idle_ticks = s.svc_degraded_idle_ticks;
     ka.lone_ticks = l.aql ? s.svc_lone_ticks : 0;
     const uint64_t tl = now_ns();
