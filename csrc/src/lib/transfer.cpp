@@ -144,8 +144,10 @@ static bool lane_idle(State::SvcLane &l) {
 }
 
 // Wait until every workgroup of the lane's last instance has left. 0: drained;
-// -1: not within timeout_ns.
-static int lane_drain(State::SvcLane &l, uint64_t timeout_ns) {
+// -1: not within timeout_ns. `site` names the caller in the health counters
+// (the longest drain and where it happened).
+enum DrainSite : unsigned { kDrainStart = 1, kDrainPark, kDrainStop, kDrainAbort, kDrainRepost };
+static int lane_drain_timed(State::SvcLane &l, uint64_t timeout_ns) {
     if (l.aql) return aql_lane_wait(&l.q, timeout_ns);
     const uint64_t t0 = now_ns();
     hipError_t e;
@@ -155,6 +157,17 @@ static int lane_drain(State::SvcLane &l, uint64_t timeout_ns) {
     }
     (void)hipGetLastError();
     return 0;
+}
+static int lane_drain(State::SvcLane &l, uint64_t timeout_ns, DrainSite site) {
+    State &s = S();
+    const uint64_t t0 = now_ns();
+    const int rc = lane_drain_timed(l, timeout_ns);
+    const uint64_t dt = now_ns() - t0;
+    if (dt > s.svc_drain_max_ns) {
+        s.svc_drain_max_ns = dt;
+        s.svc_drain_max_site = site;
+    }
+    return rc;
 }
 
 // The current instance's tagged status words (ocm/xfer.h): 0 unless it wrote them.
@@ -291,7 +304,7 @@ int service_start(unsigned long long first_seq) {
                              __ATOMIC_RELEASE);
             __builtin_ia32_sfence();
         }
-        if (lane_drain(s.svc_lanes[(size_t)pick], s.svc_drain_ns) != 0) {
+        if (lane_drain(s.svc_lanes[(size_t)pick], s.svc_drain_ns, kDrainStart) != 0) {
             s.svc_wedged = true;
             s.svc_max = 0;
             OCM_FAIL(-1, "copy service: no lane drained within OCM_SERVICE_DRAIN_MS");
@@ -377,7 +390,7 @@ void service_park() {
     if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
     State::SvcLane &l = s.svc_lanes[(size_t)s.svc_lane];
     if (l.aql) {
-        if (lane_drain(l, s.svc_drain_ns) != 0) {
+        if (lane_drain(l, s.svc_drain_ns, kDrainPark) != 0) {
             s.svc_wedged = true;
             s.svc_max = 0;
             OCM_WARN("copy service did not leave on STOP within OCM_SERVICE_DRAIN_MS; the service is off");
@@ -397,7 +410,7 @@ void service_stop() {
     s.svc_running = false;
     for (State::SvcLane &l : s.svc_lanes) {  // every lane drained before its box goes
         if (l.aql) {
-            if (lane_drain(l, s.svc_drain_ns) != 0) {
+            if (lane_drain(l, s.svc_drain_ns, kDrainStop) != 0) {
                 // never free what a kernel that did not leave may still touch
                 OCM_WARN("copy service: a lane did not drain at shutdown; its queue and box are leaked");
                 continue;
@@ -451,7 +464,7 @@ static int service_abort(unsigned long long seq, unsigned long long active, cons
     service_store_seq(s.svc_req, kServiceStop);
     if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
     s.svc_aborts++;
-    if (lane_drain(s.svc_lanes[(size_t)s.svc_lane], s.svc_drain_ns) != 0) {
+    if (lane_drain(s.svc_lanes[(size_t)s.svc_lane], s.svc_drain_ns, kDrainAbort) != 0) {
         s.svc_wedged = true;
         s.svc_max = 0;
         OCM_FAIL(-2, "copy service %s (seq %llu, %llu members, %llu done words, roster %llu, exited %llu) "
@@ -558,7 +571,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
                     service_store_seq(s.svc_req, kServiceStop);
                     if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
                 }
-                if (lane_drain(s.svc_lanes[(size_t)s.svc_lane], s.svc_drain_ns) != 0)
+                if (lane_drain(s.svc_lanes[(size_t)s.svc_lane], s.svc_drain_ns, kDrainRepost) != 0)
                     return service_abort(seq, active, "left part of a request behind and did not drain");
                 s.svc_running = false;
                 s.svc_relaunches++;

@@ -394,8 +394,9 @@ def service_health() -> dict:
     synchronize never waits for it, and its lead may stay resident alone between
     bursts, OCM_SERVICE_LONE_US), "hip" on HIP streams; `promotions`: gang ops that
     replaced a lone lead with a full instance; `lone`: the running instance's lead
-    is alone."""
-    out = (ctypes.c_uint64 * 14)()
+    is alone; `drain_max_ms` / `drain_max_site`: the longest wait for a lane's
+    workgroups to leave and where it happened."""
+    out = (ctypes.c_uint64 * 16)()
     load().ocm_x_service_health(out)
     n, k = int(out[6]), int(out[10])
     return {"degraded": int(out[0]), "incomplete_exits": int(out[1]), "aborts": int(out[2]),
@@ -404,7 +405,10 @@ def service_health() -> dict:
             # every start, split: choosing a lane (runtime stream queries) / the launch call itself
             "start_pick_us_mean": round(out[8] / k / 1e3, 2) if k else None,
             "start_launch_us_mean": round(out[9] / k / 1e3, 2) if k else None,
-            "queue": "aql" if out[11] else "hip", "promotions": int(out[12]), "lone": bool(out[13])}
+            "queue": "aql" if out[11] else "hip", "promotions": int(out[12]), "lone": bool(out[13]),
+            # the longest wait for a lane's workgroups to leave, and where
+            "drain_max_ms": round(out[14] / 1e6, 3),
+            "drain_max_site": {0: None, 1: "start", 2: "park", 3: "stop", 4: "abort", 5: "repost"}.get(int(out[15]))}
 
 
 def tick_stats() -> dict | None:
