@@ -25,12 +25,16 @@ struct AqlKernel {
     uint32_t private_bytes = 0;  // scratch per work-item
 };
 
-// One queue with one dispatch in flight at a time, its completion signal and
-// kernarg buffer (reused only once the previous dispatch has completed).
+// One queue, its completion signal (the dispatches still running: every
+// dispatch adds one, the packet processor subtracts one when it completes) and
+// two kernarg slots used in turn, so a dispatch may follow one that is still
+// running (the packets carry no barrier bit: the second starts as soon as every
+// workgroup of the first has been dispatched).
 struct AqlLane {
     void *queue = nullptr;  // hsa_queue_t *
-    uint64_t signal = 0;    // hsa_signal_t handle: 1 while a dispatch runs, 0 once it completed
+    uint64_t signal = 0;    // hsa_signal_t handle
     void *kernarg = nullptr;
+    unsigned slot = 0;      // kernarg slot of the last dispatch
     bool busy = false;      // a dispatch was issued and not yet seen complete
 };
 
@@ -43,10 +47,16 @@ int aql_lane_create(AqlLane *l, bool high_priority);
 void aql_lane_destroy(AqlLane *l);
 // One 1-D dispatch of `blocks` x `threads`: `args` (the explicit kernel
 // arguments, `nargs` bytes) followed by the hidden arguments the code object
-// reads (block count, group size, grid dimensions). The lane must be idle.
-int aql_dispatch(AqlLane *l, const AqlKernel &k, const void *args, size_t nargs, unsigned blocks, unsigned threads);
-// Whether the lane's dispatch has completed (a load of its signal).
+// reads (block count, group size, grid dimensions). The lane must be idle unless
+// `overlap`: then at most one dispatch may still run (its kernel must have read
+// its arguments already), and the new one starts once all of its workgroups
+// have been dispatched.
+int aql_dispatch(AqlLane *l, const AqlKernel &k, const void *args, size_t nargs, unsigned blocks, unsigned threads,
+                 bool overlap = false);
+// Whether the lane's dispatches have completed (a load of its signal).
 bool aql_lane_idle(AqlLane *l);
+// Dispatches of the lane still running.
+long aql_lane_inflight(AqlLane *l);
 // Wait up to timeout_ns for the lane's dispatch to complete. 0: idle.
 int aql_lane_wait(AqlLane *l, uint64_t timeout_ns);
 

@@ -73,6 +73,8 @@ hsa_status_t find_kernarg_pool(hsa_amd_memory_pool_t pool, void *p) {
     return HSA_STATUS_SUCCESS;
 }
 
+constexpr size_t kKernargSlot = 2048;
+
 uint64_t mono_ns() {
     timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -176,7 +178,7 @@ int aql_lane_create(AqlLane *l, bool high_priority) {
         return -1;
     }
     void *ka = nullptr;
-    if (hsa_amd_memory_pool_allocate(s.kernarg_pool, 4096, 0, &ka) != HSA_STATUS_SUCCESS ||
+    if (hsa_amd_memory_pool_allocate(s.kernarg_pool, 2 * kKernargSlot, 0, &ka) != HSA_STATUS_SUCCESS ||
         hsa_amd_agents_allow_access(1, &s.gpu, nullptr, ka) != HSA_STATUS_SUCCESS) {
         if (ka) (void)hsa_amd_memory_pool_free(ka);
         (void)hsa_signal_destroy(sig);
@@ -198,15 +200,22 @@ void aql_lane_destroy(AqlLane *l) {
     *l = AqlLane{};
 }
 
-int aql_dispatch(AqlLane *l, const AqlKernel &k, const void *args, size_t nargs, unsigned blocks, unsigned threads) {
+int aql_dispatch(AqlLane *l, const AqlKernel &k, const void *args, size_t nargs, unsigned blocks, unsigned threads,
+                 bool overlap) {
     hsa_queue_t *q = static_cast<hsa_queue_t *>(l->queue);
     const size_t hidden = (nargs + 7) & ~size_t(7);
     // COv5 hidden arguments read by the kernel: block count x/y/z at +0, group
     // size x/y/z at +12, remainders at +18, global offsets at +40, dims at +64.
-    if (!q || l->busy || blocks == 0 || threads == 0 || threads > 1024 || k.kernarg_bytes > 4096 ||
+    if (!q || blocks == 0 || threads == 0 || threads > 1024 || k.kernarg_bytes > kKernargSlot ||
         nargs > k.kernarg_bytes || (k.kernarg_bytes > nargs && hidden + 66 > k.kernarg_bytes))
         return -1;
-    char *ka = static_cast<char *>(l->kernarg);
+    hsa_signal_t sig{l->signal};
+    if (l->busy && !aql_lane_idle(l)) {
+        // one dispatch still running: only when asked, and never a third
+        if (!overlap || hsa_signal_load_scacquire(sig) > 1) return -1;
+    }
+    l->slot ^= 1u;
+    char *ka = static_cast<char *>(l->kernarg) + (size_t)l->slot * kKernargSlot;
     std::memset(ka, 0, k.kernarg_bytes);
     std::memcpy(ka, args, nargs);
     if (k.kernarg_bytes > nargs) {
@@ -217,8 +226,7 @@ int aql_dispatch(AqlLane *l, const AqlKernel &k, const void *args, size_t nargs,
         std::memcpy(ka + hidden + 12, gs, sizeof(gs));
         std::memcpy(ka + hidden + 64, &dims, sizeof(dims));
     }
-    hsa_signal_t sig{l->signal};
-    hsa_signal_store_relaxed(sig, 1);
+    hsa_signal_add_relaxed(sig, 1);
     const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
     const uint64_t t0 = mono_ns();
     while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
@@ -254,6 +262,13 @@ bool aql_lane_idle(AqlLane *l) {
     if (hsa_signal_load_scacquire(hsa_signal_t{l->signal}) != 0) return false;
     l->busy = false;
     return true;
+}
+
+long aql_lane_inflight(AqlLane *l) {
+    if (!l->busy) return 0;
+    const long v = (long)hsa_signal_load_scacquire(hsa_signal_t{l->signal});
+    if (v == 0) l->busy = false;
+    return v;
 }
 
 int aql_lane_wait(AqlLane *l, uint64_t timeout_ns) {

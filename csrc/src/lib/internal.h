@@ -238,6 +238,7 @@ struct State {
     // members left (OCM_SERVICE_LONE_US; AQL lanes only, 100 MHz ticks).
     unsigned long long svc_lone_ticks = 100ull * 200000;
     uint64_t svc_promotions = 0;  // gang ops that replaced a lone lead with a full instance
+    uint64_t svc_overlaps = 0;    // instances dispatched on a lane whose previous lead had not left yet
     uint64_t svc_drain_max_ns = 0;   // the longest wait for a lane to drain (health)
     unsigned svc_drain_max_site = 0; // where: 1 start, 2 park, 3 stop, 4 abort, 5 re-post
     int svc_lane = -1;

@@ -972,8 +972,9 @@ void ocm_x_service_stats(uint64_t out[5]) {
 // gang ops that replaced a lone lead with a full instance, 1 if the running
 // instance's lead is alone (its members left), and the lanes created.
 // Then the longest wait for a lane to drain (ns) and where it happened
-// (1 lane pick at a start, 2 park, 3 shutdown, 4 abort, 5 re-post after an exit).
-void ocm_x_service_health(uint64_t out[16]) {
+// (1 lane pick at a start, 2 park, 3 shutdown, 4 abort, 5 re-post after an exit),
+// and the instances dispatched beside a previous lead that had not left yet.
+void ocm_x_service_health(uint64_t out[17]) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     const bool run = s.svc && s.svc_running;
@@ -993,6 +994,7 @@ void ocm_x_service_health(uint64_t out[16]) {
     out[13] = (run && service_untag(s.svc_epoch, __atomic_load_n(&s.svc->lone, __ATOMIC_ACQUIRE)) != 0) ? 1 : 0;
     out[14] = s.svc_drain_max_ns;
     out[15] = s.svc_drain_max_site;
+    out[16] = s.svc_overlaps;
 }
 
 // Copy-service phase stamps of the last request (OCM_SERVICE_PROTO with the

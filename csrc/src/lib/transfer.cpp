@@ -286,11 +286,24 @@ int service_start(unsigned long long first_seq) {
     // lane without a runtime query (stream order starts the new instance after them;
     // they ignore the new epoch meanwhile). A stream query costs ~10 us of host
     // time; an AQL lane's is one load of its completion signal.
+    // AQL lanes: when the last instance had its whole grid resident (a lone lead
+    // included: only such an instance goes lone), the new one goes on the same
+    // queue right away, beside a lead that has not left yet (it leaves on the new
+    // epoch; the packet starts once the old one's workgroups have all been
+    // dispatched, which they have): no new queue, no wait.
     const uint64_t tq = now_ns();
     int pick = -1;
+    bool overlap = false;
     const int n = (int)s.svc_lanes.size();
-    if (!s.svc_aql && s.svc_lane >= 0 && !s.svc_relaunch_query && svc_word(&s.svc->roster) >= s.svc_blocks)
-        pick = s.svc_lane;
+    const bool whole = s.svc_lane >= 0 && svc_word(&s.svc->roster) >= s.svc_blocks;
+    if (whole && !s.svc_aql && !s.svc_relaunch_query) pick = s.svc_lane;
+    if (whole && s.svc_aql && !s.svc_lanes[(size_t)s.svc_lane].dirty) {
+        const long run = aql_lane_inflight(&s.svc_lanes[(size_t)s.svc_lane].q);
+        if (run <= 1) {
+            pick = s.svc_lane;
+            overlap = run == 1;
+        }
+    }
     for (int k = 0; k < n && pick < 0; k++) {
         const int i = (s.svc_lane + k) % n;
         if (lane_idle(s.svc_lanes[(size_t)i])) pick = i;
@@ -353,10 +366,11 @@ int service_start(unsigned long long first_seq) {
             s.svc_max = 0;
             OCM_FAIL(-1, "copy service: clearing the gang box failed");
         }
-        if (aql_dispatch(&l.q, s.svc_kernel, &ka, sizeof(ka), s.svc_blocks, 256) != 0) {
+        if (aql_dispatch(&l.q, s.svc_kernel, &ka, sizeof(ka), s.svc_blocks, 256, overlap) != 0) {
             s.svc_max = 0;
             OCM_FAIL(-1, "copy service dispatch failed");
         }
+        if (overlap) s.svc_overlaps++;
     } else if (service_launch(ka, s.svc_blocks, reset, l.stream) != hipSuccess) {
         (void)hipGetLastError();
         s.svc_max = 0;

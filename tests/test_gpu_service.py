@@ -429,8 +429,9 @@ def test_gang_ops_complete_while_another_process_holds_most_cus(mesh_factory):
             a.fill(seed=1, nbytes=size)
             a.put(0, 0, size)
         before = api.service_health()
-        time.sleep(0.002)  # past the idle exit: the next op relaunches the service under the hog
+        time.sleep(0.002)  # past the idle window: the next gang op starts an instance under the hog
         hog, resident, grid = _start_hog(4, 5000)
+        print(f"before the hog: {before}")
         try:
             worst = 0.0
             for i in range(2 * len(plan)):
