@@ -596,10 +596,7 @@ def main() -> int:
         if not args.no_characterize:
             ig = ph.run("idle_gap", lambda: wl.idle_gap_latency(pair, 4096))
             igs = gather_obj(dist, ig, world)
-            for gap in ig:
-                row = {k: (max(x[gap][k] for x in igs) if k.endswith("_us") else sum(x[gap][k] for x in igs))
-                       for k in ig[gap]}
-                idle_gap[gap] = row
+            idle_gap.update(wl.merge_idle_gap_rows(igs))
             # the headline small-op rows run pinned (OCM_PIN=1, set above for GPU runs);
             # the library default leaves apps unpinned, so time 4 KiB ops unpinned too
             def unpinned():

@@ -120,6 +120,22 @@ def idle_gap_latency(alloc: api.Allocation, nbytes: int = 4096, gaps=IDLE_GAPS, 
     return out
 
 
+def merge_idle_gap_rows(per_rank: list) -> dict:
+    """Merge every rank's idle_gap_latency() result: per gap, times (keys ending in
+    `_us`) are the slowest rank's, counts the sum over ranks. Every rank's keys count
+    (relaunch timings exist only on ranks that relaunched), so every rank computes the
+    same table from the same gathered list and raises nothing another rank would not."""
+    out = {}
+    for gap in sorted({g for r in per_rank for g in r}, key=lambda g: int(g)):
+        rows = [r[gap] for r in per_rank if gap in r]
+        row = {}
+        for k in sorted({k for x in rows for k in x}):
+            vals = [x[k] for x in rows if x.get(k) is not None]
+            row[k] = (max(vals) if k.endswith("_us") else sum(vals)) if vals else None
+        out[gap] = row
+    return out
+
+
 # Configurations an autotune chooses from: (variant 0 auto / 1 register kernel /
 # 2 LDS-DMA kernel / 3 the runtime's copy engines / 4 PCIe streaming kernel /
 # 5 push-based get (kernels on the owners' GPUs write into the local half; puts

@@ -294,3 +294,19 @@ def test_push_candidates_are_opt_in(monkeypatch):
     assert not any(v[0] == 5 for v in wl.default_candidates().values())
     monkeypatch.setenv("OCM_AUTOTUNE_PUSH", "1")
     assert {"push", "push_b1024"} <= set(wl.default_candidates())
+
+
+def test_idle_gap_rows_merge_ragged_ranks():
+    # Relaunch timings exist only on ranks that relaunched: a merge keyed on one rank's
+    # row raised on some ranks and not others, which then waited in different
+    # collectives (found in the 8-rank one-GPU rehearsal with HIP lanes).
+    from oncilla_amd.models import workloads as wl
+
+    a = {"0": {"get_p50_us": 5.0, "get_relaunches": 0}, "1000": {"get_p50_us": 6.0, "get_relaunches": 2,
+                                                              "get_relaunch_host_us": 3.0}}
+    b = {"0": {"get_p50_us": 5.5, "get_relaunches": 0}, "1000": {"get_p50_us": 6.5, "get_relaunches": 0}}
+    for order in ([a, b], [b, a]):
+        m = wl.merge_idle_gap_rows(order)
+        assert m["0"] == {"get_p50_us": 5.5, "get_relaunches": 0}
+        assert m["1000"] == {"get_p50_us": 6.5, "get_relaunches": 2, "get_relaunch_host_us": 3.0}
+        assert list(m) == ["0", "1000"]

@@ -6,5 +6,5 @@
 set -o pipefail
 OUT=${OUT:-gpurun_out/share8}
 mkdir -p $OUT
-timeout -k 10 900 env OCM_BENCH_SHARE_GPU=1 RANKLOG_DIR=$OUT bash tools/launch_ranks.sh 8 29551 bench.py --gpus 8 --steps 3 --warmup 1 --json-out $OUT/bench_share8.json > $OUT/share8.log 2>&1
+timeout -k 10 900 env OCM_BENCH_SHARE_GPU=1 RANKLOG_DIR=$OUT bash tools/launch_ranks.sh 8 ${PORT:-29551} bench.py --gpus 8 --steps 3 --warmup 1 --json-out $OUT/bench_share8.json > $OUT/share8.log 2>&1
 rc=$?; tail -c 400 $OUT/share8.log; echo; grep -c "\[ocm W" $OUT/share8.log $OUT/rank*.log; exit $rc
