@@ -169,10 +169,22 @@ int ocm_init(void) {
     return 0;
 }
 
+// An application that exits without ocm_tini may leave the copy service's lone
+// lead resident on the library's AQL queue: tell it to leave (a store to the
+// host record; nothing waits, the process is going away).
+__attribute__((destructor)) static void ocm_lib_exit() {
+    State &s = S();
+    if (s.svc && s.svc_req) {
+        service_store_seq(s.svc_req, kServiceStop);
+        if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
+    }
+}
+
 int ocm_tini(void) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (!s.inited) return -1;
+    service_stop();  // no copy-service instance may outlive the mappings below
     std::vector<lib_alloc *> left(s.allocs.begin(), s.allocs.end());
     for (auto *a : left) ocm_free(a);
     Msg d = new_msg(MSG_DISCONNECT);
@@ -191,7 +203,6 @@ int ocm_tini(void) {
         if (m.hbase) munmap(m.hbase, m.bytes);
     }
     s.imports.clear();
-    service_stop();
     net_close_all();
     close_fd_chans();
     for (auto st : s.lanes) {
