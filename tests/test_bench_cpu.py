@@ -310,3 +310,18 @@ def test_idle_gap_rows_merge_ragged_ranks():
         assert m["0"] == {"get_p50_us": 5.5, "get_relaunches": 0}
         assert m["1000"] == {"get_p50_us": 6.5, "get_relaunches": 2, "get_relaunch_host_us": 3.0}
         assert list(m) == ["0", "1000"]
+
+
+def test_bench_ranks_started_without_torchrun(native, tmp_path):
+    # tools/launch_ranks.sh: the one-GPU 8-rank rehearsal starts its ranks from a
+    # shell loop (no Python parent with the GPU open); the env:// rendezvous and the
+    # JSON line on rank 0's stdout must be the same as under torchrun.
+    r = subprocess.run(["bash", os.path.join(REPO, "tools", "launch_ranks.sh"), "2", "29597",
+                        os.path.join(REPO, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "1", "--warmup",
+                        "1", "--max-bytes", str(1 << 20), "--alloc-samples", "10", "--no-ctrl-extra"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp",
+                       env=dict(os.environ, RANKLOG_DIR=str(tmp_path)))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-1500:] + (tmp_path / "rank1.log").read_text()[-1500:]
+    res = _last_json(r.stdout)
+    assert res["n_gpus"] == 2 and res["value"] > 0 and len(res["ranks"]) == 2, res
+    assert (tmp_path / "rank1.log").exists()
