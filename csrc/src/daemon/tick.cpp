@@ -380,7 +380,11 @@ public:
             const hipError_t de = tick_done_launch(done_dev_, sl.seq, st);
             if (de != hipSuccess) return why(std::string("done launch: ") + hipGetErrorString(de));
         }
-        if (ring_.size() == 1) return 0;
+        // Completion is read from the gathered slots' tick numbers and tags; the
+        // runtime is only the backstop (errors, and a done kernel's absence), for
+        // which a stream query serves: no event per tick (host time per start()).
+        // Two streams keep per-tick events (a tick on one stream says nothing of the other).
+        if (ring_.size() == 1 || (nstreams_ == 1 && !done_kernel_)) return 0;
         return hipEventRecord(sl.ev, st) == hipSuccess ? 0 : -1;
     }
     int test(int i) override {
@@ -400,7 +404,9 @@ public:
         // One tick in flight: the stream is exactly that tick, and a stream query
         // measured cheaper than an event query (profiles/ctrl_probe_r02c.json).
         // (graph ticks record no events: a drained stream has finished them all)
-        const hipError_t q = (ring_.size() == 1 || graph_k_) ? hipStreamQuery(stream_) : hipEventQuery(ring_[(size_t)i].ev);
+        const hipError_t q = (ring_.size() == 1 || graph_k_ || (nstreams_ == 1 && !done_kernel_))
+                                 ? hipStreamQuery(stream_)  // drained: every queued tick is done
+                                 : hipEventQuery(ring_[(size_t)i].ev);
         if (q == hipSuccess) return 1;
         if (q != hipErrorNotReady) return why(std::string("tick completion: ") + hipGetErrorString(q));
         {
