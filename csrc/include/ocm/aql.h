@@ -50,9 +50,10 @@ void aql_lane_destroy(AqlLane *l);
 // reads (block count, group size, grid dimensions). The lane must be idle unless
 // `overlap`: then at most one dispatch may still run (its kernel must have read
 // its arguments already), and the new one starts once all of its workgroups
-// have been dispatched.
+// have been dispatched. `barrier`: the new one starts only once every earlier
+// dispatch of the lane has completed (the packet's barrier bit).
 int aql_dispatch(AqlLane *l, const AqlKernel &k, const void *args, size_t nargs, unsigned blocks, unsigned threads,
-                 bool overlap = false);
+                 bool overlap = false, bool barrier = false);
 // Whether the lane's dispatches have completed (a load of its signal).
 bool aql_lane_idle(AqlLane *l);
 // Dispatches of the lane still running.

@@ -323,6 +323,8 @@ static_assert(sizeof(ServiceKernelArgs) == 88, "service kernel argument layout")
 hipError_t service_launch(const ServiceKernelArgs &args, unsigned blocks, bool reset_box, hipStream_t stream);
 // The service kernel's symbol in the device code object embedded in libocm (AQL dispatch).
 constexpr const char *kServiceKernelSymbol = "ocm_service_kernel";
+// ... and the kernel that zeroes a gang box (one workgroup, ServiceBox * argument).
+constexpr const char *kServiceBoxClearSymbol = "ocm_service_box_clear";
 
 // Deterministic 32-bit word pattern (word i of a buffer) for data verification.
 hipError_t pattern_fill(void *p, uint64_t words, uint64_t first_word, uint32_t seed, hipStream_t stream);

@@ -1002,6 +1002,13 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
     }
 }
 
+// Zero a lane's gang box on the lane's own AQL queue (one workgroup), ahead of an
+// instance dispatched with the barrier bit: no host memset and stream sync.
+extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_box_clear(ServiceBox *box) {
+    unsigned long long *w = reinterpret_cast<unsigned long long *>(box);
+    for (unsigned i = threadIdx.x; i < sizeof(ServiceBox) / 8; i += kThreads) w[i] = 0ull;
+}
+
 uint32_t service_gang_size(const XferArgs &a, unsigned blocks, unsigned solo_tiles) {
     const uint64_t tile_mask = (1ull << a.tile_shift) - 1;
     const uint64_t ntiles = (((a.rem_off + a.len + tile_mask) & ~tile_mask) - (a.rem_off & ~tile_mask)) >> a.tile_shift;

@@ -201,7 +201,7 @@ void aql_lane_destroy(AqlLane *l) {
 }
 
 int aql_dispatch(AqlLane *l, const AqlKernel &k, const void *args, size_t nargs, unsigned blocks, unsigned threads,
-                 bool overlap) {
+                 bool overlap, bool barrier) {
     hsa_queue_t *q = static_cast<hsa_queue_t *>(l->queue);
     const size_t hidden = (nargs + 7) & ~size_t(7);
     // COv5 hidden arguments read by the kernel: block count x/y/z at +0, group
@@ -248,6 +248,7 @@ int aql_dispatch(AqlLane *l, const AqlKernel &k, const void *args, size_t nargs,
     p->completion_signal = sig;
     // system-scope acquire at the start and release at the end, as HIP's own launches
     const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                            ((barrier ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
                             (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                             (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
     const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;

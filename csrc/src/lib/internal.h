@@ -234,6 +234,7 @@ struct State {
     // object loads (svc_aql), =hip: HIP streams.
     bool svc_queue_aql = true, svc_aql = false;
     AqlKernel svc_kernel;
+    AqlKernel svc_clear_kernel;     // ocm_service_box_clear (object 0: clear with a host memset)
     // Lone lead (ocm/xfer.h): the lead stays resident alone this long after the
     // members left (OCM_SERVICE_LONE_US; AQL lanes only, 100 MHz ticks).
     unsigned long long svc_lone_ticks = 100ull * 200000;

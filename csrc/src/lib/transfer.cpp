@@ -229,6 +229,8 @@ int service_start(unsigned long long first_seq) {
                 OCM_INFO("copy service on HIP streams: no usable %s in the embedded code object", kServiceKernelSymbol);
             else
                 s.svc_aql = true;
+            if (s.svc_aql && aql_kernel(kServiceBoxClearSymbol, &s.svc_clear_kernel) != 0)
+                s.svc_clear_kernel = AqlKernel{};
         }
         if (!s.svc_aql) s.svc_lone_ticks = 0;
         // Streams of their own priority: HIP shares its few hardware queues
@@ -297,7 +299,8 @@ int service_start(unsigned long long first_seq) {
     const int n = (int)s.svc_lanes.size();
     const bool whole = s.svc_lane >= 0 && svc_word(&s.svc->roster) >= s.svc_blocks;
     if (whole && !s.svc_aql && !s.svc_relaunch_query) pick = s.svc_lane;
-    if (whole && s.svc_aql && !s.svc_lanes[(size_t)s.svc_lane].dirty) {
+    if (whole && s.svc_aql && !s.svc_lanes[(size_t)s.svc_lane].dirty && !s.svc_box_reset_always &&
+        s.svc_lanes[(size_t)s.svc_lane].gang_total <= (1ull << 30)) {  // a box clear would make a third dispatch
         const long run = aql_lane_inflight(&s.svc_lanes[(size_t)s.svc_lane].q);
         if (run <= 1) {
             pick = s.svc_lane;
@@ -359,18 +362,27 @@ int service_start(unsigned long long first_seq) {
     const uint64_t tl = now_ns();
     s.svc_ns_pick += tl - tq;
     if (l.aql) {
-        // the box is cleared before the dispatch (the queue is not a HIP stream)
-        if (reset && (hipMemsetAsync(l.box, 0, sizeof(ServiceBox), s.stream) != hipSuccess ||
-                      hipStreamSynchronize(s.stream) != hipSuccess)) {
+        // The box is cleared first: on the lane itself, the instance behind it with the
+        // barrier bit (the queue is not a HIP stream); a host memset if that kernel is missing.
+        bool barrier = false;
+        if (reset && s.svc_clear_kernel.object && !overlap) {
+            ServiceBox *bx = l.box;
+            if (aql_dispatch(&l.q, s.svc_clear_kernel, &bx, sizeof(bx), 1, 256) != 0) {
+                s.svc_max = 0;
+                OCM_FAIL(-1, "copy service: gang box clear dispatch failed");
+            }
+            barrier = overlap = true;
+        } else if (reset && (hipMemsetAsync(l.box, 0, sizeof(ServiceBox), s.stream) != hipSuccess ||
+                             hipStreamSynchronize(s.stream) != hipSuccess)) {
             (void)hipGetLastError();
             s.svc_max = 0;
             OCM_FAIL(-1, "copy service: clearing the gang box failed");
         }
-        if (aql_dispatch(&l.q, s.svc_kernel, &ka, sizeof(ka), s.svc_blocks, 256, overlap) != 0) {
+        if (aql_dispatch(&l.q, s.svc_kernel, &ka, sizeof(ka), s.svc_blocks, 256, overlap, barrier) != 0) {
             s.svc_max = 0;
             OCM_FAIL(-1, "copy service dispatch failed");
         }
-        if (overlap) s.svc_overlaps++;
+        if (overlap && !barrier) s.svc_overlaps++;
     } else if (service_launch(ka, s.svc_blocks, reset, l.stream) != hipSuccess) {
         (void)hipGetLastError();
         s.svc_max = 0;
