@@ -217,7 +217,7 @@ struct alignas(128) ServiceSlot {
     ServiceReq req;                   // the request record
     unsigned long long done;          // device -> host (own cache line)
     unsigned long long exited;        // device -> host, tagged: first seq NOT served when it left
-    unsigned long long gpu_ticks;     // device -> host: sum of request-seen -> done ticks of workgroup 0 (100 MHz)
+    unsigned long long gpu_ticks;     // device -> host: this instance's sum of request-seen -> done ticks of its lead (100 MHz)
     // device -> host, tagged: gang members resident so far (workgroup 0 included);
     // the host sizes every gang to at most this many.
     unsigned long long roster;

@@ -852,8 +852,9 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
     bool served = false;
     bool lone = false;        // the lead alone: the members have left (lone_ticks)
     bool superseded = false;  // the lead saw a newer instance: it leaves without touching the slot
-    unsigned long long ticks_sum =
-        lead ? __hip_atomic_load(&slot->gpu_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+    // This instance's own sum (the host folds each instance's into its total when it
+    // starts the next): no read across PCIe before the first poll.
+    unsigned long long ticks_sum = 0;
     for (;;) {
         int base = 0;  // first lane of the record being served (wave-uniform)
         if (tid < 64) {

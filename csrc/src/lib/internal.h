@@ -63,6 +63,7 @@ constexpr unsigned kServiceGangHostDefault = 32;
 constexpr uint64_t kServiceMaxLocalDefault = 64ull << 20;
 constexpr int kServiceSoloTilesDefault = 2;
 constexpr int kServiceIdleUsDefault = 50;
+constexpr int kServiceLoneUsDefault = 2000;
 // Write-through hand-offs, the records in write-combined memory, and gang
 // requests polled directly by the first 16 workgroups: small ops -0.1/-0.2 us,
 // host-tier 128 KiB-4 MiB and HBM 256 KiB-1 MiB gangs 1-1.5 us faster than the
@@ -236,8 +237,12 @@ struct State {
     AqlKernel svc_kernel;
     AqlKernel svc_clear_kernel;     // ocm_service_box_clear (object 0: clear with a host memset)
     // Lone lead (ocm/xfer.h): the lead stays resident alone this long after the
-    // members left (OCM_SERVICE_LONE_US; AQL lanes only, 100 MHz ticks).
-    unsigned long long svc_lone_ticks = 100ull * 200000;
+    // members left (OCM_SERVICE_LONE_US; AQL lanes only, 100 MHz ticks). 2 ms: a
+    // 4 KiB op after a 1 ms pause stays hot (6.4-6.8 us against 17 us through a
+    // relaunch), while any resident workgroup delays a full-GPU GEMM launched
+    // meanwhile by ~45% (bf16 8192^3: 0.93 -> 1.38 ms: the CU it holds runs its
+    // tile late), so the window stays short (profiles/lone_sweep_r04.json).
+    unsigned long long svc_lone_ticks = 100ull * kServiceLoneUsDefault;
     uint64_t svc_promotions = 0;  // gang ops that replaced a lone lead with a full instance
     uint64_t svc_overlaps = 0;    // instances dispatched on a lane whose previous lead had not left yet
     uint64_t svc_drain_max_ns = 0;   // the longest wait for a lane to drain (health)
@@ -269,6 +274,7 @@ struct State {
     bool svc_park_kernel = false;  // park the service during kernel transfers above svc_max (OCM_SERVICE_PARK_KERNEL)
     unsigned long long svc_seq = 0;
     uint64_t svc_ops = 0, svc_ns_post = 0, svc_ns_wait = 0;  // service diagnostics (ocm_x_service_stats)
+    uint64_t svc_gpu_ticks_done = 0;  // GPU ticks of the instances before the current one
     uint64_t svc_max = kServiceMaxDefault;           // 0: the service is off (or failed)
     uint64_t svc_max_host = kServiceMaxHostDefault;  // the same bound for host-tier-only pairs
     // Largest blocking op the service takes for a pair with (`hbm`) or without HBM extents.

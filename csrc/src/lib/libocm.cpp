@@ -155,7 +155,7 @@ int ocm_init(void) {
         const char *v = std::getenv("OCM_SERVICE_QUEUE");  // State outlives ocm_tini: set it on every init
         s.svc_queue_aql = !(v && std::strcmp(v, "hip") == 0);
     }
-    s.svc_lone_ticks = 100ull * (unsigned long long)std::max(0, env_int("OCM_SERVICE_LONE_US", 200000));
+    s.svc_lone_ticks = 100ull * (unsigned long long)std::max(0, env_int("OCM_SERVICE_LONE_US", kServiceLoneUsDefault));
     const char *lfm = std::getenv("OCM_LAUNCH_FLAG_MAX");
     s.launch_flag_max = lfm && *lfm ? std::strtoull(lfm, nullptr, 0) : kLaunchFlagMaxDefault;
     s.tuning = xfer_tuning_from_env();
@@ -968,7 +968,7 @@ void ocm_x_service_stats(uint64_t out[5]) {
     out[0] = s.svc_ops;
     out[1] = s.svc_ns_post;
     out[2] = s.svc_ns_wait;
-    out[3] = s.svc ? __atomic_load_n(&s.svc->gpu_ticks, __ATOMIC_ACQUIRE) : 0;
+    out[3] = s.svc_gpu_ticks_done + (s.svc ? __atomic_load_n(&s.svc->gpu_ticks, __ATOMIC_ACQUIRE) : 0);
     out[4] = s.svc_relaunches;  // instances started because the previous one left idle
 }
 
@@ -984,8 +984,9 @@ void ocm_x_service_stats(uint64_t out[5]) {
 // instance's lead is alone (its members left), and the lanes created.
 // Then the longest wait for a lane to drain (ns) and where it happened
 // (1 lane pick at a start, 2 park, 3 shutdown, 4 abort, 5 re-post after an exit),
-// and the instances dispatched beside a previous lead that had not left yet.
-void ocm_x_service_health(uint64_t out[17]) {
+// the instances dispatched beside a previous lead that had not left yet, and 1
+// while an instance is resident (started and not yet left).
+void ocm_x_service_health(uint64_t out[18]) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     const bool run = s.svc && s.svc_running;
@@ -1006,6 +1007,7 @@ void ocm_x_service_health(uint64_t out[17]) {
     out[14] = s.svc_drain_max_ns;
     out[15] = s.svc_drain_max_site;
     out[16] = s.svc_overlaps;
+    out[17] = (run && service_untag(s.svc_epoch, __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE)) == 0) ? 1 : 0;
 }
 
 // Copy-service phase stamps of the last request (OCM_SERVICE_PROTO with the

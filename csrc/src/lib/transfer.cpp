@@ -331,6 +331,9 @@ int service_start(unsigned long long first_seq) {
     s.svc_stream = l.stream;
     s.svc_box = l.box;
     s.svc_epoch = (s.svc_epoch + 1) & (unsigned)kServiceGangEpochMask;
+    // the last instance's GPU time (diagnostic) joins the total; a lead that is still
+    // leaving serves nothing more, so it writes no more ticks
+    s.svc_gpu_ticks_done += __atomic_exchange_n(&s.svc->gpu_ticks, 0ull, __ATOMIC_ACQ_REL);
     __atomic_store_n(&s.svc->exited, 0ull, __ATOMIC_RELEASE);
     __atomic_store_n(&s.svc->roster, 0ull, __ATOMIC_RELEASE);  // the new lead publishes its own
     __atomic_store_n(&s.svc->lone, 0ull, __ATOMIC_RELEASE);

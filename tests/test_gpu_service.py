@@ -82,6 +82,7 @@ def test_service_restarts_after_idle_exit(mesh_factory, monkeypatch, queue):
     # (lone) and serves solo ops itself, and a gang op replaces it with a full
     # instance (a promotion). Alternate gang-sized and solo ops across idle gaps.
     monkeypatch.setenv("OCM_SERVICE_QUEUE", queue)
+    monkeypatch.setenv("OCM_SERVICE_LONE_US", "200000")  # the lead outlasts every 5 ms sleep
     m = mesh_factory(1, gpus=[0])
     with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
         n = 1 << 20
@@ -99,7 +100,7 @@ def test_service_restarts_after_idle_exit(mesh_factory, monkeypatch, queue):
         assert st["ops"] - st0["ops"] >= 24
         if h["queue"] == "aql":
             assert h["promotions"] - h0["promotions"] >= 5, h  # every gang op after a gap replaced the lone lead
-            assert st["relaunches"] == st0["relaunches"], st  # the lone lead never left (200 ms window)
+            assert st["relaunches"] == st0["relaunches"], st  # the lone lead never left (200 ms window here)
         else:
             assert queue == "hip", f"the AQL queue did not come up: {h}"
             assert st["relaunches"] - st0["relaunches"] >= 10, st  # every 5 ms sleep outlasted the idle exit
@@ -119,6 +120,30 @@ def test_service_lanes_are_aql_queues(mesh_factory):
         assert a.check(seed=5, nbytes=4096) == 0
         h = api.service_health()
         assert h["queue"] == "aql", h
+        a.free()
+
+
+@pytest.mark.parametrize("lone_us", ["0", "2000"])
+def test_lone_window_bounds_the_lead_residency(mesh_factory, monkeypatch, lone_us):
+    # A resident workgroup delays full-GPU kernels (profiles/lone_sweep_r04.json), so the
+    # lone lead must be gone once its window has passed: 5 ms after an op, nothing of the
+    # service is resident, and the next small op relaunches it and still moves the right bytes.
+    monkeypatch.setenv("OCM_SERVICE_LONE_US", lone_us)
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 4096
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_HOST_TIER)
+        for i in range(5):
+            a.fill(seed=20 + i, nbytes=n)
+            a.put(0, 0, n)
+            r0 = api.service_stats()["relaunches"]
+            _busy_wait(0.005)
+            h = api.service_health()
+            assert not h["resident"], h  # the instance has left
+            a.fill(seed=0, nbytes=n)
+            a.get(0, 0, n)
+            assert a.check(seed=20 + i, nbytes=n) == 0
+            assert api.service_stats()["relaunches"] == r0 + 1
         a.free()
 
 
