@@ -229,7 +229,9 @@ int service_start(unsigned long long first_seq) {
                 OCM_INFO("copy service on HIP streams: no usable %s in the embedded code object", kServiceKernelSymbol);
             else
                 s.svc_aql = true;
-            if (s.svc_aql && aql_kernel(kServiceBoxClearSymbol, &s.svc_clear_kernel) != 0)
+            // OCM_SERVICE_CLEAR_KERNEL=0: clear gang boxes with a host memset (A/B)
+            if (s.svc_aql && (env_int("OCM_SERVICE_CLEAR_KERNEL", 1) == 0 ||
+                              aql_kernel(kServiceBoxClearSymbol, &s.svc_clear_kernel) != 0))
                 s.svc_clear_kernel = AqlKernel{};
         }
         if (!s.svc_aql) s.svc_lone_ticks = 0;

@@ -20,6 +20,8 @@ VARIANTS = {
     "reset": {"OCM_SERVICE_BOX_RESET": "1", "OCM_SERVICE_RELAUNCH_QUERY": "1"},  # + clear the box (round 3)
     "idle200": {"OCM_SERVICE_IDLE_US": "200"},
     "hip": {"OCM_SERVICE_QUEUE": "hip"},  # round-4 start: HIP stream lanes, no lone lead
+    "lone0": {"OCM_SERVICE_LONE_US": "0"},  # AQL lanes, the lead leaves with the members
+    "memsetclear": {"OCM_SERVICE_CLEAR_KERNEL": "0"},  # gang box cleared by a host memset
 }
 
 
