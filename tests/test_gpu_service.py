@@ -459,6 +459,7 @@ def test_gang_ops_complete_while_another_process_holds_most_cus(mesh_factory):
         print(f"before the hog: {before}")
         try:
             worst = 0.0
+            trail = []  # per op pair: ms, roster, lone, promotions, relaunches, degraded
             for i in range(2 * len(plan)):
                 a, size = plan[i % len(plan)]
                 a.fill(seed=500 + i, nbytes=size)
@@ -466,7 +467,11 @@ def test_gang_ops_complete_while_another_process_holds_most_cus(mesh_factory):
                 a.put(0, 0, size)
                 a.fill(seed=0, nbytes=size)
                 a.get(0, 0, size)
-                worst = max(worst, time.perf_counter() - t0)
+                dt = time.perf_counter() - t0
+                worst = max(worst, dt)
+                hh = api.service_health()
+                trail.append((size >> 10, round(dt * 1e3, 2), hh["roster"], hh["lone"], hh["promotions"],
+                              hh["relaunches"], hh["degraded"], hh["roster_min"]))
                 assert a.check(seed=500 + i, nbytes=size) == 0, f"op pair {i} ({size} B)"
                 if i % 3 == 2:
                     time.sleep(0.001)  # another relaunch under the hog
@@ -475,6 +480,7 @@ def test_gang_ops_complete_while_another_process_holds_most_cus(mesh_factory):
             _finish_hog(hog)
         h = api.service_health()
         print(f"hog {resident}/{grid} workgroups; service health {h}; worst op pair {worst * 1e3:.2f} ms")
+        print("per op pair (KiB, ms, roster, lone, promotions, relaunches, degraded, roster_min):", trail)
         assert still_held, "the hog left before the ops ran: the test proved nothing"
         assert h["aborts"] == before["aborts"] and not h["wedged"], h
         assert h["incomplete_exits"] == 0, h
