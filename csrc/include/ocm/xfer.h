@@ -223,7 +223,8 @@ struct alignas(128) ServiceSlot {
     unsigned long long roster;
     unsigned long long lone;          // device -> host, tagged: first seq after which the members left
     unsigned long long epoch_now;     // host -> device: the current instance's epoch (a lone lead of another leaves)
-    unsigned long long pad[10];
+    unsigned long long lead_xcd;      // device -> host, tagged: 1 + the XCD the current lead runs on (diagnostic)
+    unsigned long long pad[9];
     // WGDONE: gang member i stores the seq it finished here (device -> host)
     unsigned long long wg_done[kServiceWgDoneMax];
 };

@@ -985,8 +985,9 @@ void ocm_x_service_stats(uint64_t out[5]) {
 // Then the longest wait for a lane to drain (ns) and where it happened
 // (1 lane pick at a start, 2 park, 3 shutdown, 4 abort, 5 re-post after an exit),
 // the instances dispatched beside a previous lead that had not left yet, and 1
-// while an instance is resident (started and not yet left).
-void ocm_x_service_health(uint64_t out[18]) {
+// while an instance is resident (started and not yet left), and 1 + the XCD of
+// the running instance's lead (0: unknown).
+void ocm_x_service_health(uint64_t out[19]) {
     State &s = S();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     const bool run = s.svc && s.svc_running;
@@ -1008,6 +1009,7 @@ void ocm_x_service_health(uint64_t out[18]) {
     out[15] = s.svc_drain_max_site;
     out[16] = s.svc_overlaps;
     out[17] = (run && service_untag(s.svc_epoch, __atomic_load_n(&s.svc->exited, __ATOMIC_ACQUIRE)) == 0) ? 1 : 0;
+    out[18] = run ? service_untag(s.svc_epoch, __atomic_load_n(&s.svc->lead_xcd, __ATOMIC_ACQUIRE)) : 0;
 }
 
 // Copy-service phase stamps of the last request (OCM_SERVICE_PROTO with the

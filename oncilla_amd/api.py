@@ -396,7 +396,7 @@ def service_health() -> dict:
     replaced a lone lead with a full instance; `lone`: the running instance's lead
     is alone; `drain_max_ms` / `drain_max_site`: the longest wait for a lane's
     workgroups to leave and where it happened."""
-    out = (ctypes.c_uint64 * 18)()
+    out = (ctypes.c_uint64 * 19)()
     load().ocm_x_service_health(out)
     n, k = int(out[6]), int(out[10])
     return {"degraded": int(out[0]), "incomplete_exits": int(out[1]), "aborts": int(out[2]),
@@ -409,7 +409,8 @@ def service_health() -> dict:
             # the longest wait for a lane's workgroups to leave, and where
             "drain_max_ms": round(out[14] / 1e6, 3),
             "drain_max_site": {0: None, 1: "start", 2: "park", 3: "stop", 4: "abort", 5: "repost"}.get(int(out[15])),
-            "overlaps": int(out[16]), "resident": bool(out[17])}
+            "overlaps": int(out[16]), "resident": bool(out[17]),
+            "lead_xcd": int(out[18]) - 1 if out[18] else None}
 
 
 def tick_stats() -> dict | None:
