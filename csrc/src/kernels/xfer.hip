@@ -855,10 +855,14 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
     // This instance's own sum (the host folds each instance's into its total when it
     // starts the next): no read across PCIe before the first poll.
     unsigned long long ticks_sum = 0;
-    if (lead && tid == 0)  // which XCD leads (HW_REG_XCC_ID[3:0]); a posted write, nothing waits for it
-        __hip_atomic_store(&slot->lead_xcd,
-                           service_tag(epoch, 1ull + (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xFu)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lead && tid == 0) {
+        // where the lead runs (diagnostic; a posted write, nothing waits for it): 1 + its XCD
+        // (HW_REG_XCC_ID[3:0]) in bits 0..7, its HW_REG_HW_ID (CU, shader array, engine) above
+        const unsigned long long xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xFu;
+        const unsigned long long hwid = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+        __hip_atomic_store(&slot->lead_xcd, service_tag(epoch, (1ull + xcc) | (hwid << 8)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     for (;;) {
         int base = 0;  // first lane of the record being served (wave-uniform)
         if (tid < 64) {

@@ -410,7 +410,9 @@ def service_health() -> dict:
             "drain_max_ms": round(out[14] / 1e6, 3),
             "drain_max_site": {0: None, 1: "start", 2: "park", 3: "stop", 4: "abort", 5: "repost"}.get(int(out[15])),
             "overlaps": int(out[16]), "resident": bool(out[17]),
-            "lead_xcd": int(out[18]) - 1 if out[18] else None}
+            "lead_xcd": (int(out[18]) & 0xFF) - 1 if out[18] else None,
+            # the lead's HW_REG_HW_ID: CU bits 8..11, shader array 12, engine 13..15 (gfx9 layout)
+            "lead_hw_id": int(out[18]) >> 8 if out[18] else None}
 
 
 def tick_stats() -> dict | None:

@@ -32,7 +32,10 @@ def main():
                 for _ in range(a.instances):
                     api.quiesce()
                     p.get(0, 0, 4096)  # relaunch
-                    x = api.service_health()["lead_xcd"]
+                    h = api.service_health()
+                    hw = h["lead_hw_id"] or 0
+                    # XCD / engine / array / CU of the lead
+                    x = f'{h["lead_xcd"]}/se{(hw >> 13) & 7}/sh{(hw >> 12) & 1}/cu{(hw >> 8) & 15}' 
                     g, _ = p.time_onesided_samples(0, 4096, 200, cap_s=0.2)
                     u, _ = p.time_onesided_samples(1, 4096, 200, cap_s=0.2)
                     res[tier].setdefault(str(x), []).append((round(wl.percentile(g, 50) * 1e6, 2),
