@@ -36,6 +36,7 @@ struct AqlLane {
     void *kernarg = nullptr;
     unsigned slot = 0;      // kernarg slot of the last dispatch
     bool busy = false;      // a dispatch was issued and not yet seen complete
+    bool kernarg_wc = false;  // kernarg buffer in write-combined host memory (else the runtime's pool)
 };
 
 // Load the embedded code object for HIP device `hip_device` (idempotent per

@@ -177,9 +177,24 @@ int aql_lane_create(AqlLane *l, bool high_priority) {
         (void)hsa_queue_destroy(q);
         return -1;
     }
+    // Kernel arguments in write-combined host memory (OCM_AQL_KERNARG=wc, the default):
+    // the kernel's first scalar loads then skip the snoop of the CPU's caches that the
+    // coherent kernarg pool costs (a GPU load of coherent host memory: ~3.5 us,
+    // profiles/xcd_latency_r04.json). The host only ever writes them, and fences
+    // before the doorbell. =pool: the runtime's kernarg pool.
     void *ka = nullptr;
-    if (hsa_amd_memory_pool_allocate(s.kernarg_pool, 2 * kKernargSlot, 0, &ka) != HSA_STATUS_SUCCESS ||
-        hsa_amd_agents_allow_access(1, &s.gpu, nullptr, ka) != HSA_STATUS_SUCCESS) {
+    bool wc = false;
+    const char *km = std::getenv("OCM_AQL_KERNARG");
+    if (!(km && std::strcmp(km, "pool") == 0)) {
+        if (hipHostMalloc(&ka, 2 * kKernargSlot, hipHostMallocWriteCombined | hipHostMallocMapped) == hipSuccess) {
+            wc = true;
+        } else {
+            (void)hipGetLastError();
+            ka = nullptr;
+        }
+    }
+    if (!wc && (hsa_amd_memory_pool_allocate(s.kernarg_pool, 2 * kKernargSlot, 0, &ka) != HSA_STATUS_SUCCESS ||
+                hsa_amd_agents_allow_access(1, &s.gpu, nullptr, ka) != HSA_STATUS_SUCCESS)) {
         if (ka) (void)hsa_amd_memory_pool_free(ka);
         (void)hsa_signal_destroy(sig);
         (void)hsa_queue_destroy(q);
@@ -188,13 +203,17 @@ int aql_lane_create(AqlLane *l, bool high_priority) {
     l->queue = q;
     l->signal = sig.handle;
     l->kernarg = ka;
+    l->kernarg_wc = wc;
     l->busy = false;
     return 0;
 }
 
 void aql_lane_destroy(AqlLane *l) {
     if (!l->queue) return;
-    (void)hsa_amd_memory_pool_free(l->kernarg);
+    if (l->kernarg_wc)
+        (void)hipHostFree(l->kernarg);
+    else
+        (void)hsa_amd_memory_pool_free(l->kernarg);
     (void)hsa_signal_destroy(hsa_signal_t{l->signal});
     (void)hsa_queue_destroy(static_cast<hsa_queue_t *>(l->queue));
     *l = AqlLane{};
@@ -226,6 +245,8 @@ int aql_dispatch(AqlLane *l, const AqlKernel &k, const void *args, size_t nargs,
         std::memcpy(ka + hidden + 12, gs, sizeof(gs));
         std::memcpy(ka + hidden + 64, &dims, sizeof(dims));
     }
+    // write-combined kernargs leave the CPU's buffers before the packet names them
+    if (l->kernarg_wc) __builtin_ia32_sfence();
     hsa_signal_add_relaxed(sig, 1);
     const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
     const uint64_t t0 = mono_ns();
