@@ -177,15 +177,15 @@ int aql_lane_create(AqlLane *l, bool high_priority) {
         (void)hsa_queue_destroy(q);
         return -1;
     }
-    // Kernel arguments in write-combined host memory (OCM_AQL_KERNARG=wc, the default):
-    // the kernel's first scalar loads then skip the snoop of the CPU's caches that the
-    // coherent kernarg pool costs (a GPU load of coherent host memory: ~3.5 us,
-    // profiles/xcd_latency_r04.json). The host only ever writes them, and fences
-    // before the doorbell. =pool: the runtime's kernarg pool.
+    // Kernel arguments in the runtime's kernarg pool (coherent host memory), or with
+    // OCM_AQL_KERNARG=wc in write-combined host memory (no snoop of the CPU's caches on
+    // the kernel's first loads; the host fences before the doorbell). Measured equal:
+    // a relaunch costs 11.5 us after 100 us idle and 16.6-17.8 us after 1 ms either way
+    // (profiles/idle_gap_r04_kernarg.json), the GPU's wake-up, not the argument fetch.
     void *ka = nullptr;
     bool wc = false;
     const char *km = std::getenv("OCM_AQL_KERNARG");
-    if (!(km && std::strcmp(km, "pool") == 0)) {
+    if (km && std::strcmp(km, "wc") == 0) {
         if (hipHostMalloc(&ka, 2 * kKernargSlot, hipHostMallocWriteCombined | hipHostMallocMapped) == hipSuccess) {
             wc = true;
         } else {

@@ -22,7 +22,7 @@ VARIANTS = {
     "hip": {"OCM_SERVICE_QUEUE": "hip"},  # round-4 start: HIP stream lanes, no lone lead
     "lone0": {"OCM_SERVICE_LONE_US": "0"},  # AQL lanes, the lead leaves with the members
     "memsetclear": {"OCM_SERVICE_CLEAR_KERNEL": "0"},  # gang box cleared by a host memset
-    "lone0_kpool": {"OCM_SERVICE_LONE_US": "0", "OCM_AQL_KERNARG": "pool"},  # kernargs in the coherent pool
+    "lone0_kwc": {"OCM_SERVICE_LONE_US": "0", "OCM_AQL_KERNARG": "wc"},  # kernargs in write-combined memory
 }
 
 
