@@ -117,9 +117,15 @@ int open_locked(AqlState &s, int hip_device) {
         return -1;
     }
     if (hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &s.exe) !=
-            HSA_STATUS_SUCCESS ||
-        hsa_executable_load_agent_code_object(s.exe, s.gpu, s.reader, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        HSA_STATUS_SUCCESS) {
+        (void)hsa_code_object_reader_destroy(s.reader);
+        s.why = "creating an HSA executable";
+        return -1;
+    }
+    if (hsa_executable_load_agent_code_object(s.exe, s.gpu, s.reader, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
         hsa_executable_freeze(s.exe, nullptr) != HSA_STATUS_SUCCESS) {
+        (void)hsa_executable_destroy(s.exe);
+        (void)hsa_code_object_reader_destroy(s.reader);
         s.why = "loading the embedded code object (not gfx950?)";
         return -1;
     }
