@@ -189,7 +189,14 @@ public:
              hipHostGetDevicePointer(reinterpret_cast<void **>(&done_dev_), done_, 0) == hipSuccess;
         if (ok) __atomic_store_n(done_, 0ull, __ATOMIC_RELAXED);
         if (ok && sealed_) {
-            ok = hipHostMalloc(reinterpret_cast<void **>(&out_), sizeof(TickRing), fl) == hipSuccess &&
+            // The outbox in write-combined host memory (OCM_TICK_OUTBOX_WC, default 1): the
+            // host only writes it (TickTransport::flush_ring never reads it back), and the
+            // seal's one round trip then skips the snoop of the CPU's caches that coherent
+            // host memory costs a GPU read (profiles/xcd_latency_r04.json).
+            const unsigned ofl = flag("OCM_TICK_OUTBOX_WC", true)
+                                     ? (hipHostMallocMapped | hipHostMallocWriteCombined | hipHostMallocPortable)
+                                     : fl;
+            ok = hipHostMalloc(reinterpret_cast<void **>(&out_), sizeof(TickRing), ofl) == hipSuccess &&
                  hipHostGetDevicePointer(reinterpret_cast<void **>(&out_dev_), out_, 0) == hipSuccess &&
                  hipMalloc(reinterpret_cast<void **>(&consumed_), sizeof(uint64_t)) == hipSuccess &&
                  hipMemset(consumed_, 0, sizeof(uint64_t)) == hipSuccess;
@@ -818,10 +825,11 @@ void TickTransport::flush_ring() {
     if (!ring_ || out_.empty()) return;
     uint64_t pub = ring_pub_;  // never read back: the ring may sit behind a write-combined BAR
     while (!out_.empty() && pub - ring_sent_ < kTickRing) {
-        TickRecord &r = ring_->rec[pub & (kTickRing - 1)];
-        r = out_.front();
+        const TickRecord &src = out_.front();
+        ring_->rec[pub & (kTickRing - 1)] = src;
         post_ns_[pub & (kTickRing - 1)] = out_ns_.front();  // when it was posted (it may have waited for room)
-        ring_->tag[pub & (kTickRing - 1)] = tick_record_tag(reinterpret_cast<const uint64_t *>(&r), pub);
+        // the tag from the private copy: the ring is never read back (write-combined memory)
+        ring_->tag[pub & (kTickRing - 1)] = tick_record_tag(reinterpret_cast<const uint64_t *>(&src), pub);
         out_.pop_front();
         out_ns_.pop_front();
         pub++;
