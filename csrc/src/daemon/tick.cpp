@@ -189,11 +189,11 @@ public:
              hipHostGetDevicePointer(reinterpret_cast<void **>(&done_dev_), done_, 0) == hipSuccess;
         if (ok) __atomic_store_n(done_, 0ull, __ATOMIC_RELAXED);
         if (ok && sealed_) {
-            // The outbox in write-combined host memory (OCM_TICK_OUTBOX_WC, default 1): the
-            // host only writes it (TickTransport::flush_ring never reads it back), and the
-            // seal's one round trip then skips the snoop of the CPU's caches that coherent
-            // host memory costs a GPU read (profiles/xcd_latency_r04.json).
-            const unsigned ofl = flag("OCM_TICK_OUTBOX_WC", true)
+            // OCM_TICK_OUTBOX_WC=1: the outbox in write-combined host memory (the host only
+            // writes it; TickTransport::flush_ring never reads it back), so the seal's read
+            // skips the snoop of the CPU's caches. Measured no faster (alloc p50 29.8-38.0 us
+            // against 29.0-32.7 coherent, profiles/ctrl_probe_r04_outbox_wc.json): off.
+            const unsigned ofl = flag("OCM_TICK_OUTBOX_WC", false)
                                      ? (hipHostMallocMapped | hipHostMallocWriteCombined | hipHostMallocPortable)
                                      : fl;
             ok = hipHostMalloc(reinterpret_cast<void **>(&out_), sizeof(TickRing), ofl) == hipSuccess &&
