@@ -490,9 +490,9 @@ public:
         const char *tf = std::getenv("OCM_TICK_FAULT");
         // fail_after_do_alloc / fail_after_do_free: see test()
         if (tf && bytes == sizeof(TickSlot))
-            fault_type_ = std::strcmp(tf, "fail_after_do_alloc") == 0  ? MSG_DO_ALLOC
-                          : std::strcmp(tf, "fail_after_do_free") == 0 ? MSG_DO_FREE
-                                                                        : 0;
+            fault_type_ = std::strcmp(tf, "fail_after_do_alloc") == 0  ? (uint32_t)MSG_DO_ALLOC
+                          : std::strcmp(tf, "fail_after_do_free") == 0 ? (uint32_t)MSG_DO_FREE
+                                                                        : 0u;
         // stall_after=N: from tick N on this rank stops taking part, without an error
         // (a wedged collective): the peers' watchdogs must end the transport.
         if (tf && std::strncmp(tf, "stall_after=", 12) == 0) stall_after_ = std::atoll(tf + 12);
