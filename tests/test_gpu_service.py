@@ -539,3 +539,36 @@ def test_timed_out_op_is_redone_only_after_the_service_drains(mesh_factory, monk
             a.get(0, 0, n)
             assert a.check(seed=40 + i, nbytes=n) == 0
         a.free()
+
+
+def test_process_exit_without_tini_while_the_lead_is_resident(mesh_factory):
+    # An application that exits without ocm_tini while the copy service's lead is
+    # resident on the library's AQL queue: the process must end at once (a library
+    # destructor tells the lead to leave), and the GPU must serve the next process.
+    import subprocess
+    import sys
+
+    m = mesh_factory(1, gpus=[0])
+    code = (
+        "import os, time\n"
+        "from oncilla_amd import api\n"
+        f"c = api.Client(daemon_rank=0, gpu=0, ns={m.ns!r}); c.init()\n"
+        "a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=4096, flags=api.OCM_ALLOC_HOST_TIER)\n"
+        "a.get(0, 0, 4096); time.sleep(0.001)\n"
+        "h = api.service_health(); print('resident', h['resident'], h['lone'], h['queue'], flush=True)\n"
+        "os._exit(0)\n")
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=dict(__import__("os").environ))
+    took = time.perf_counter() - t0
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "resident True True aql" in r.stdout, r.stdout
+    assert took < 30, took
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=4096, flags=api.OCM_ALLOC_HOST_TIER)
+        a.fill(seed=4, nbytes=4096)
+        a.put(0, 0, 4096)
+        a.fill(seed=0, nbytes=4096)
+        a.get(0, 0, 4096)
+        assert a.check(seed=4, nbytes=4096) == 0
+        a.free()
