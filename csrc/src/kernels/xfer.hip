@@ -852,6 +852,12 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
     bool served = false;
     bool lone = false;        // the lead alone: the members have left (lone_ticks)
     bool superseded = false;  // the lead saw a newer instance: it leaves without touching the slot
+    // The last gang request was already seen complete by an earlier idle check. The idle
+    // window runs from the lead's own share, and a PCIe-bound gang op of 8-16 MiB ends up
+    // to ~50 us later on its slowest member: leaving at the first check that finds it
+    // complete raced the host's next post (12-15 % of those ops relaunched,
+    // profiles/bench_n1_r04_final_b.json). A gang op gets one more window from then.
+    bool gang_drained = false;
     // This instance's own sum (the host folds each instance's into its total when it
     // starts the next): no read across PCIe before the first poll.
     unsigned long long ticks_sum = 0;
@@ -943,7 +949,8 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
                     (served || __builtin_amdgcn_s_memrealtime() - started > 2000000ull)) {
                     // Leave only once every member the last request named is done
                     // with it: a member that saw the STOP first would never serve it.
-                    if (service_last_complete(slot, box, proto, last, last_gang)) {
+                    const bool complete = service_last_complete(slot, box, proto, last, last_gang);
+                    if (complete && (gang_drained || (last_gang & 0xFFFFull) <= 1 || !served)) {
                         // Only an instance whose whole grid has started goes lone: one with
                         // workgroups still waiting for a CU leaves whole, as its lane drains
                         // only once they have started (and left at once), and the full
@@ -960,6 +967,8 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
                             __hip_atomic_store(&slot->lone, service_tag(epoch, last + 1), __ATOMIC_RELEASE,
                                                __HIP_MEMORY_SCOPE_SYSTEM);
                         }
+                    } else if (complete) {
+                        gang_drained = true;  // complete only now: the host gets a whole window to post
                     }
                     idle_start = __builtin_amdgcn_s_memrealtime();
                 }
@@ -993,6 +1002,7 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
         last = s;
         last_gang = sh[1];
         served = true;
+        gang_drained = false;
         idle_start = __builtin_amdgcn_s_memrealtime();  // every lane: the idle test must stay wave-uniform
         if (lead) {
             // Diagnostic, after `done` so it never delays it: a running sum in a
