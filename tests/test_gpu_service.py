@@ -572,3 +572,25 @@ def test_process_exit_without_tini_while_the_lead_is_resident(mesh_factory):
         a.get(0, 0, 4096)
         assert a.check(seed=4, nbytes=4096) == 0
         a.free()
+
+
+@pytest.mark.parametrize("idle_us", ["50", "20"])
+def test_back_to_back_gang_ops_never_relaunch(mesh_factory, monkeypatch, idle_us):
+    # The lead's idle window runs from the end of its own share, and a PCIe-bound
+    # 8 MiB gang op ends later on its slowest member. The lead gives the host one
+    # more window after it first sees the op complete, so back-to-back gang ops keep
+    # the instance (before: 25 of 200 8 MiB gets relaunched in one driver-shaped run,
+    # profiles/bench_n1_r04_final_b.json). Timed in the library's own loop.
+    monkeypatch.setenv("OCM_SERVICE_IDLE_US", idle_us)
+    m = mesh_factory(1, gpus=[0])
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        n = 8 << 20
+        a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_HOST_TIER)
+        for op, size in ((0, n), (1, n), (0, 2 << 20), (1, 2 << 20)):
+            a.time_onesided_samples(op, size, 2, cap_s=0.0, min_iters=2)  # a resident instance
+            xs, rel = a.time_onesided_samples(op, size, 100, cap_s=2.0, min_iters=100)
+            xs.sort()
+            print(f"idle {idle_us} us op {op} {size} B: p50 {xs[len(xs) // 2] * 1e6:.1f} us "
+                  f"max {xs[-1] * 1e6:.1f} us relaunches {rel}")
+            assert rel == 0, (op, size, rel)
+        a.free()
