@@ -265,10 +265,20 @@ struct State {
     // default), so a direct gang spreads them over more CUs' miss queues. Gets use
     // 16 KiB tiles there: 64/128/256 KiB 6.9/7.75/9.86 vs 7.6/8.3/10.4 us; 8 and 4 KiB
     // tiles lose, and so do puts and a 32 KiB get as a gang of two
-    // (profiles/svc_host_tile_ab_r02.json).
-    unsigned svc_host_tile_shift_get = 14, svc_host_tile_shift_put = 0;  // OCM_SERVICE_HOST_TILE_SHIFT_GET/_PUT
+    // (profiles/svc_host_tile_ab_r02.json). Puts take 16 KiB tiles there too since round 4:
+    // with WGDONE completion and the roster a 64 KiB put as a gang of four beats it solo,
+    // 64/128/256 KiB 6.2-6.4/6.9-7.3/9.2-9.3 vs 7.5-7.6/7.2-7.5/9.6-9.7 us in six interleaved
+    // runs (profiles/host_mid_ab_r04p.json, profiles/host_put_ab_r04q.json).
+    unsigned svc_host_tile_shift_get = 14, svc_host_tile_shift_put = 14;  // OCM_SERVICE_HOST_TILE_SHIFT_GET/_PUT
     uint64_t svc_host_tile_min = 64ull << 10;                             // OCM_SERVICE_HOST_TILE_MIN
     uint64_t svc_host_tile_max = 256ull << 10;                            // OCM_SERVICE_HOST_TILE_MAX
+    // Host-tier gets of at least svc_host_get_narrow_min bytes go to at most
+    // svc_host_get_width members: fewer reads in flight over PCIe end closer together.
+    // 1/2/4 MiB gets 24.5-24.6/43.3/79.9 us with 12 members against 25.8-26.1/44.7-45.1/
+    // 81.8-82.1 with 16; 512 KiB keeps 16 (14.9-15.0 against 15.2-15.4 with 12), and 8 or
+    // 4 members lose (profiles/host_wide_ab_r04q.json).
+    uint64_t svc_host_get_narrow_min = 1ull << 20;  // OCM_SERVICE_HOST_GET_NARROW_MIN
+    unsigned svc_host_get_width = 12;               // OCM_SERVICE_HOST_GET_WIDTH
     bool svc_running = false;
     bool svc_shared_queue = false;  // no priority stream for the service: it may share a launch stream's hardware queue
     bool svc_park_kernel = false;  // park the service during kernel transfers above svc_max (OCM_SERVICE_PARK_KERNEL)

@@ -141,6 +141,9 @@ int ocm_init(void) {
     s.svc_host_tile_shift_put = (unsigned)std::max(0, env_int("OCM_SERVICE_HOST_TILE_SHIFT_PUT", (int)s.svc_host_tile_shift_put));
     if (const char *v = std::getenv("OCM_SERVICE_HOST_TILE_MAX"); v && *v) s.svc_host_tile_max = std::strtoull(v, nullptr, 0);
     if (const char *v = std::getenv("OCM_SERVICE_HOST_TILE_MIN"); v && *v) s.svc_host_tile_min = std::strtoull(v, nullptr, 0);
+    if (const char *v = std::getenv("OCM_SERVICE_HOST_GET_NARROW_MIN"); v && *v)
+        s.svc_host_get_narrow_min = std::strtoull(v, nullptr, 0);
+    s.svc_host_get_width = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_HOST_GET_WIDTH", 12), 1024));
     s.launch_flags = env_int("OCM_LAUNCH_FLAG", 1) != 0;
     s.svc_park_kernel = env_int("OCM_SERVICE_PARK_KERNEL", 0) != 0;
     s.svc_idle_ticks = 100ull * (unsigned long long)std::max(1, env_int("OCM_SERVICE_IDLE_US", kServiceIdleUsDefault));  // 100 MHz clock

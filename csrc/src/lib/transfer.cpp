@@ -543,6 +543,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
     auto size_and_post = [&]() -> int {
         unsigned width = direct ? std::min(s.svc_direct, s.svc_blocks)
                                 : (hbm ? s.svc_blocks : std::min(s.svc_gang_host, s.svc_blocks));
+        if (!hbm && !x.put && x.len >= s.svc_host_get_narrow_min) width = std::min(width, s.svc_host_get_width);
         if (service_gang_size(x, width, solo_tiles) > 1) {
             // A lone lead takes no gang: a full instance replaces it (the lead leaves
             // on the new epoch by itself; it holds no request of ours).

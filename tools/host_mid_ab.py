@@ -28,11 +28,13 @@ def child():
     from oncilla_amd.models import workloads as wl
     from oncilla_amd.parallel.mesh import Mesh
 
+    sizes = [int(x) for x in os.environ.get("HOST_MID_SIZES", "").split(",") if x] or SIZES
     out = {}
     with Mesh(1, gpus=[0]) as m:
         with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
-            a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=1 << 20, remote_bytes=1 << 20, flags=api.OCM_ALLOC_HOST_TIER)
-            for s in SIZES:
+            n = max(sizes)
+            a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_HOST_TIER)
+            for s in sizes:
                 a.time_onesided(0, s, 3)
                 for op, key in ((0, "get"), (1, "put")):
                     t0 = api.service_totals()
@@ -55,6 +57,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default=DEFAULT_VARIANTS)
+    ap.add_argument("--sizes", default="", help="comma-separated bytes (default: 4 KiB - 1 MiB)")
     ap.add_argument("--out", default="")
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
@@ -71,7 +74,8 @@ def main():
     res = {}
     for k in range(a.rounds):
         for name, env in variants:
-            r = subprocess.run([sys.executable, "-u", __file__, "--child"], env=dict(os.environ, **env),
+            r = subprocess.run([sys.executable, "-u", __file__, "--child"],
+                               env=dict(os.environ, HOST_MID_SIZES=a.sizes, **env),
                                capture_output=True, text=True, timeout=240)
             line = [x for x in r.stdout.splitlines() if x.startswith("{")]
             row = json.loads(line[-1]) if line else {"error": r.stderr[-1500:]}
