@@ -4,6 +4,7 @@
 // system-scope loads, each from a new 4 KiB page, with s_memrealtime (100 MHz).
 // Each kind is measured twice: after a GPU kernel wrote the buffer (no CPU cache holds
 // its lines, as for data a put left) and after a CPU memset (lines dirty in CPU caches).
+// A third pass reads one line over and over (a poller's pattern).
 // Prints one JSON object of medians in ns. Bounded: 200 loads per launch, 8 MiB buffers.
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
@@ -22,12 +23,13 @@ __global__ void gpu_fill(unsigned long long *p, size_t words) {
     __threadfence_system();
 }
 
-__global__ __launch_bounds__(64) void chase(const unsigned long long *p, unsigned long long *out) {
+// stride 0: every load reads the same line, as a poller of one record does
+__global__ __launch_bounds__(64) void chase(const unsigned long long *p, unsigned long long *out, size_t stride) {
     if (threadIdx.x != 0) return;
     unsigned long long v = 0;
     for (int i = 0; i < kIters; i++) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        v += __hip_atomic_load(p + (size_t)i * kStride + (v & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        v += __hip_atomic_load(p + (size_t)i * stride + (v & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         out[i] = __builtin_amdgcn_s_memrealtime() - t0;
     }
@@ -76,17 +78,19 @@ int main() {
                 }
             }
         }
-        unsigned long long gpu_last = 0, cpu_last = 0;
+        unsigned long long gpu_last = 0, cpu_last = 0, same_line = 0;
         if (h) {
             void *d = nullptr;
             if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess) {
                 unsigned long long *dp = static_cast<unsigned long long *>(d);
                 hipLaunchKernelGGL(gpu_fill, dim3(64), dim3(256), 0, nullptr, dp, kBytes / 8);
-                hipLaunchKernelGGL(chase, dim3(1), dim3(64), 0, nullptr, dp, out);
+                hipLaunchKernelGGL(chase, dim3(1), dim3(64), 0, nullptr, dp, out, kStride);
                 if (hipDeviceSynchronize() == hipSuccess) gpu_last = median_ns(out);
                 std::memset(h, 0, kBytes);
-                hipLaunchKernelGGL(chase, dim3(1), dim3(64), 0, nullptr, dp, out);
+                hipLaunchKernelGGL(chase, dim3(1), dim3(64), 0, nullptr, dp, out, kStride);
                 if (hipDeviceSynchronize() == hipSuccess) cpu_last = median_ns(out);
+                hipLaunchKernelGGL(chase, dim3(1), dim3(64), 0, nullptr, dp, out, (size_t)0);
+                if (hipDeviceSynchronize() == hipSuccess) same_line = median_ns(out);
             }
             if (mapped) {
                 (void)hipHostUnregister(h);
@@ -95,8 +99,8 @@ int main() {
                 (void)hipHostFree(h);
             }
         }
-        std::printf("%s\"%s\": {\"gpu_written_ns_p50\": %llu, \"cpu_written_ns_p50\": %llu}", first ? "" : ", ", k.name,
-                    gpu_last, cpu_last);
+        std::printf("%s\"%s\": {\"gpu_written_ns_p50\": %llu, \"cpu_written_ns_p50\": %llu, \"same_line_ns_p50\": %llu}",
+                    first ? "" : ", ", k.name, gpu_last, cpu_last, same_line);
         first = false;
     }
     std::printf("}\n");
