@@ -106,6 +106,11 @@ struct Extent {
 
 }  // namespace ocmlib
 
+// lib_alloc is the public opaque handle (oncillamem.h), so it keeps default visibility
+// while the ocmlib types it holds are hidden; g++ warns about that (-Wattributes), clang
+// does not. Hiding lib_alloc instead would hide every C entry point taking it.
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Wattributes"
 struct lib_alloc {
     enum ocm_kind kind;
     uint64_t alloc_id = 0;
@@ -134,6 +139,7 @@ struct lib_alloc {
     bool dep_pending = false;
     int plans = 0;                  // ocm_plan stages that reference this allocation
 };
+#pragma GCC diagnostic pop
 
 struct ocm_plan {
     struct Stage {
