@@ -253,11 +253,12 @@ struct alignas(128) ServiceBox {
 // `solo_tiles` tiles or the gang has one workgroup, else min(tiles, blocks).
 // `blocks` is the host's wanted width, already capped at the roster.
 uint32_t service_gang_size(const XferArgs &a, unsigned blocks, unsigned solo_tiles);
-// Post one request (words, sum, then seq with release) and flush the CPU's
-// write-combining buffers. gang = active | target << 16.
-void service_post(ServiceReq *req, const XferArgs &a, unsigned long long gang, unsigned long long seq);
-// Store one word of the record (seq: 0 to re-arm, kServiceStop) and flush.
-void service_store_seq(ServiceReq *req, unsigned long long seq);
+// Post one request (words, sum, then seq with release) to `copies` adjacent records
+// and flush the CPU's write-combining buffers. gang = active | target << 16.
+void service_post(ServiceReq *req, const XferArgs &a, unsigned long long gang, unsigned long long seq,
+                  unsigned copies = 1);
+// Store one word of the record(s) (seq: 0 to re-arm, kServiceStop) and flush.
+void service_store_seq(ServiceReq *req, unsigned long long seq, unsigned copies = 1);
 
 // Hand-off protocol bits of the service (OCM_SERVICE_PROTO):
 //   WT        copied bytes are loaded sc1 and stored write-through (sc1), and
@@ -288,8 +289,16 @@ void service_store_seq(ServiceReq *req, unsigned long long seq);
 //             copy write-through (sc1 stores drop their lines from L2 and write
 //             through) and drain, instead of a plain copy and a system release
 //             (an L2 writeback) before `done`
+//   COPIES    (with GANGREC) the gang record is written once per direct poller,
+//             128-byte copies side by side on the gang page, and member i polls
+//             copy i (the lead copy 0): GPU reads of one host line from many
+//             workgroups at once are served one after another (16 pollers: 2.8 us
+//             per read against 1.2 us with a line each; 64: 10.4 us,
+//             profiles/host_mem_latency_r04.json)
 constexpr unsigned kServiceProtoWT = 1u, kServiceProtoGangRec = 2u, kServiceProtoWCReq = 4u, kServiceProtoWgDone = 8u,
-                   kServiceProtoTrace = 16u, kServiceProtoStrictWT = 32u;
+                   kServiceProtoTrace = 16u, kServiceProtoStrictWT = 32u, kServiceProtoCopies = 64u;
+constexpr unsigned kServiceProtoMask = 127u;
+constexpr int kServiceGangCopiesMax = 4096 / 128;  // copies on the gang page
 // Whether a gang of `active` workgroups completes through ServiceSlot::wg_done.
 constexpr bool service_wg_done(unsigned proto, unsigned long long active) {
     return (proto & kServiceProtoWgDone) && active > 1 && active <= (unsigned long long)kServiceWgDoneMax;

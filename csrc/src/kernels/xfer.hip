@@ -837,8 +837,10 @@ extern "C" __global__ __launch_bounds__(kThreads) void ocm_service_kernel(Servic
     const bool lead = id == 0;
     const bool direct = grq != nullptr && id < direct_wgs;  // polls the host gang record itself
     const unsigned long long relay_above = grq != nullptr ? direct_wgs : 1;  // gangs wider than this are relayed
+    // COPIES: direct member i polls copy i of the gang record (the lead, member 0, copy 0)
+    const ServiceReq *gmine = grq + ((proto & kServiceProtoCopies) && direct ? id : 0u);
     const unsigned long long *req = reinterpret_cast<const unsigned long long *>(
-        lead ? static_cast<const void *>(rq) : direct ? static_cast<const void *>(grq) : static_cast<const void *>(box->rec));
+        lead ? static_cast<const void *>(rq) : direct ? static_cast<const void *>(gmine) : static_cast<const void *>(box->rec));
     const unsigned long long *greq = reinterpret_cast<const unsigned long long *>(grq);
     unsigned long long last = first_seq - 1;  // requests carry strictly increasing seqs
     unsigned long long last_gang = 0;          // gang word of request `last` (workgroup 0's idle-exit test)
@@ -1035,23 +1037,28 @@ uint32_t service_gang_size(const XferArgs &a, unsigned blocks, unsigned solo_til
     return (uint32_t)(ntiles < blocks ? ntiles : blocks);
 }
 
-void service_post(ServiceReq *req, const XferArgs &a, unsigned long long gang, unsigned long long seq) {
+void service_post(ServiceReq *req, const XferArgs &a, unsigned long long gang, unsigned long long seq,
+                  unsigned copies) {
     unsigned long long w[kServiceReqGang + 1] = {};
     std::memcpy(w, &a, sizeof(a));
     w[kServiceReqGang] = gang;
     const unsigned long long h = service_sum(seq, w);
-    // Line 0 (words 0..7) first and fenced, then line 1 (words 8..13, sum, seq):
-    // a poll that saw seq ahead of the rest fails the hash and reads again.
-    for (int i = 0; i < 8; i++) __atomic_store_n(&req->args[i], w[i], __ATOMIC_RELAXED);
+    // Line 0 (words 0..7) of every copy first and fenced, then line 1 (words 8..13,
+    // sum, seq): a poll that saw seq ahead of the rest fails the hash and reads again.
+    // The last copy first: copy 0 is the lead's.
+    for (unsigned c = copies; c-- > 0;)
+        for (int i = 0; i < 8; i++) __atomic_store_n(&req[c].args[i], w[i], __ATOMIC_RELAXED);
     __builtin_ia32_sfence();
-    for (int i = 8; i <= kServiceReqGang; i++) __atomic_store_n(&req->args[i], w[i], __ATOMIC_RELAXED);
-    __atomic_store_n(&req->sum, h, __ATOMIC_RELAXED);
-    __atomic_store_n(&req->seq, seq, __ATOMIC_RELEASE);
+    for (unsigned c = copies; c-- > 0;) {
+        for (int i = 8; i <= kServiceReqGang; i++) __atomic_store_n(&req[c].args[i], w[i], __ATOMIC_RELAXED);
+        __atomic_store_n(&req[c].sum, h, __ATOMIC_RELAXED);
+        __atomic_store_n(&req[c].seq, seq, __ATOMIC_RELEASE);
+    }
     __builtin_ia32_sfence();
 }
 
-void service_store_seq(ServiceReq *req, unsigned long long seq) {
-    __atomic_store_n(&req->seq, seq, __ATOMIC_RELEASE);
+void service_store_seq(ServiceReq *req, unsigned long long seq, unsigned copies) {
+    for (unsigned c = 0; c < copies; c++) __atomic_store_n(&req[c].seq, seq, __ATOMIC_RELEASE);
     __builtin_ia32_sfence();
 }
 

@@ -218,6 +218,7 @@ struct State {
     ServiceSlot *svc = nullptr;
     ServiceReq *svc_req = nullptr;   // request record (&svc->req)
     ServiceReq *svc_greq = nullptr;  // GANGREC: gang requests' record, a page of its own
+    unsigned svc_greq_copies = 1;    // COPIES: one gang record per direct poller on that page
     char *svc_rec_pages = nullptr;   // separately allocated record pages (GANGREC / WCREQ), freed at stop
     ServiceBox *svc_box = nullptr;   // device-memory mailbox of the gang (the current lane's)
     unsigned long long *pattern_bad = nullptr;  // device counter of ocm_x_pattern checks

@@ -128,13 +128,14 @@ int ocm_init(void) {
     s.svc_blocks = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_BLOCKS", kServiceBlocksDefault), 1024));
     s.svc_solo_tiles = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES", kServiceSoloTilesDefault));
     s.svc_solo_tiles_host_get = (unsigned)std::max(0, env_int("OCM_SERVICE_SOLO_TILES_HOST_GET", 1));
-    s.svc_proto = (unsigned)env_int("OCM_SERVICE_PROTO", (int)kServiceProtoDefault) & 63u;
+    s.svc_proto = (unsigned)env_int("OCM_SERVICE_PROTO", (int)kServiceProtoDefault) & kServiceProtoMask;
     // OCM_SERVICE_STRICT=1 (measurements, tests): every request takes the STRICT
     // (peer-HBM) hand-off, so its cost shows on a one-GPU box
     s.svc_force_strict = env_int("OCM_SERVICE_STRICT", 0) != 0;
     if (const char *v = std::getenv("OCM_SERVICE_MAX_LOCAL"); v && *v) s.svc_max_local = std::strtoull(v, nullptr, 0);
     s.svc_gang_host = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_GANG_HOST", (int)s.svc_gang_host), 1024));
     s.svc_direct = (unsigned)std::max(1, std::min(env_int("OCM_SERVICE_DIRECT", kServiceDirectDefault), 1024));
+    if (s.svc_direct > (unsigned)kServiceGangCopiesMax) s.svc_proto &= ~kServiceProtoCopies;  // one page of copies
     if (const char *v = std::getenv("OCM_SERVICE_DIRECT_MAX_HOST"); v && *v) s.svc_direct_max_host = std::strtoull(v, nullptr, 0);
     if (const char *v = std::getenv("OCM_SERVICE_DIRECT_MAX_HBM"); v && *v) s.svc_direct_max_hbm = std::strtoull(v, nullptr, 0);
     s.svc_host_tile_shift_get = (unsigned)std::max(0, env_int("OCM_SERVICE_HOST_TILE_SHIFT_GET", (int)s.svc_host_tile_shift_get));
@@ -179,7 +180,7 @@ __attribute__((destructor)) static void ocm_lib_exit() {
     State &s = S();
     if (s.svc && s.svc_req) {
         service_store_seq(s.svc_req, kServiceStop);
-        if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
+        if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop, s.svc_greq_copies);
     }
 }
 

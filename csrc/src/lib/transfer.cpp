@@ -276,7 +276,13 @@ int service_start(unsigned long long first_seq) {
                 for (int i = 0; i < 8192 / 8; i++) __atomic_store_n(reinterpret_cast<unsigned long long *>(s.svc_rec_pages) + i, 0ull, __ATOMIC_RELAXED);
                 __builtin_ia32_sfence();
                 if (wc) s.svc_req = reinterpret_cast<ServiceReq *>(s.svc_rec_pages);
-                if (gangrec) s.svc_greq = reinterpret_cast<ServiceReq *>(s.svc_rec_pages + 4096);
+                if (gangrec) {
+                    s.svc_greq = reinterpret_cast<ServiceReq *>(s.svc_rec_pages + 4096);
+                    s.svc_greq_copies = (s.svc_proto & kServiceProtoCopies)
+                                            ? std::max(1u, std::min(std::min(s.svc_direct, s.svc_blocks),
+                                                                    (unsigned)kServiceGangCopiesMax))
+                                            : 1u;
+                }
             }
         }
     }
@@ -342,7 +348,7 @@ int service_start(unsigned long long first_seq) {
     // A lone lead of an earlier instance (another lane) leaves when it sees this.
     __atomic_store_n(&s.svc->epoch_now, (unsigned long long)s.svc_epoch, __ATOMIC_RELEASE);
     service_store_seq(s.svc_req, 0ull);  // clear a STOP left by a parked instance
-    if (s.svc_greq) service_store_seq(s.svc_greq, 0ull);
+    if (s.svc_greq) service_store_seq(s.svc_greq, 0ull, s.svc_greq_copies);
     // the gang counter mirror stays below the 31-bit target field (ocm/xfer.h)
     const bool reset = l.dirty || s.svc_box_reset_always || l.gang_total > (1ull << 30);
     if (reset) {
@@ -418,7 +424,7 @@ void service_park() {
     if (!s.svc || !s.svc_running) return;
     DeviceGuard g(s.device);
     service_store_seq(s.svc_req, kServiceStop);
-    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
+    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop, s.svc_greq_copies);
     State::SvcLane &l = s.svc_lanes[(size_t)s.svc_lane];
     if (l.aql) {
         if (lane_drain(l, s.svc_drain_ns, kDrainPark) != 0) {
@@ -437,7 +443,7 @@ void service_stop() {
     if (!s.svc) return;
     DeviceGuard g(s.device);
     service_store_seq(s.svc_req, kServiceStop);
-    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
+    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop, s.svc_greq_copies);
     s.svc_running = false;
     for (State::SvcLane &l : s.svc_lanes) {  // every lane drained before its box goes
         if (l.aql) {
@@ -493,7 +499,7 @@ static int service_abort(unsigned long long seq, unsigned long long active, cons
     const unsigned long long ex = svc_word(&s.svc->exited);
     const unsigned long long roster = svc_word(&s.svc->roster);
     service_store_seq(s.svc_req, kServiceStop);
-    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
+    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop, s.svc_greq_copies);
     s.svc_aborts++;
     if (lane_drain(s.svc_lanes[(size_t)s.svc_lane], s.svc_drain_ns, kDrainAbort) != 0) {
         s.svc_wedged = true;
@@ -565,7 +571,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
                (strict ? kServiceGangStrict : 0ull);
         // GANGREC: gang requests go to the record the whole gang polls.
         rq = (active > 1 && s.svc_greq) ? s.svc_greq : s.svc_req;
-        service_post(rq, x, gang, seq);
+        service_post(rq, x, gang, seq, rq == s.svc_greq ? s.svc_greq_copies : 1u);
         return 0;
     };
     // Completed: `done` (a solo op or the gang's last member), or under WGDONE
@@ -601,7 +607,7 @@ int service_xfer(XferArgs x, unsigned solo_tiles, bool hbm, bool strict) {
                 DeviceGuard g(s.device);
                 if (!ex) {
                     service_store_seq(s.svc_req, kServiceStop);
-                    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop);
+                    if (s.svc_greq) service_store_seq(s.svc_greq, kServiceStop, s.svc_greq_copies);
                 }
                 if (lane_drain(s.svc_lanes[(size_t)s.svc_lane], s.svc_drain_ns, kDrainRepost) != 0)
                     return service_abort(seq, active, "left part of a request behind and did not drain");

@@ -4,6 +4,7 @@ service's own split of each op (post, lead GPU time, crossings). VERDICT r03 ite
 asks for 64 KiB get <= 6 us, 256 KiB >= 28 GiB/s, 1 MiB >= 45 GiB/s.
 
     python tools/host_mid_ab.py [--rounds 3] [--variants name:K=V,K=V;name2:...] [--out ...]
+    (HOST_MID_TIER=hbm: the remote half in this GPU's HBM instead of the host tier)
 """
 import argparse
 import json
@@ -33,7 +34,8 @@ def child():
     with Mesh(1, gpus=[0]) as m:
         with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
             n = max(sizes)
-            a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=api.OCM_ALLOC_HOST_TIER)
+            tier = api.OCM_ALLOC_LOOPBACK if os.environ.get("HOST_MID_TIER") == "hbm" else api.OCM_ALLOC_HOST_TIER
+            a = c.alloc(api.OCM_REMOTE_GPU, local_bytes=n, remote_bytes=n, flags=tier)
             for s in sizes:
                 a.time_onesided(0, s, 3)
                 for op, key in ((0, "get"), (1, "put")):
