@@ -202,6 +202,11 @@ public:
     // (take_announce never fires). `bell`: the host-wide doorbell every daemon of the
     // host rings (futex word, shared memory) when it posts into an idle mesh, so the
     // idle tick ends at once on every rank; nullptr: idle ticks run their full length.
+    // An RCCL idle tick's seal waits for the bell on the GPU, which keeps one workgroup
+    // resident; that delays a full-GPU GEMM by ~45 % (profiles/resident_cost_r04.json).
+    // So the seal waits on the GPU only within OCM_TICK_IDLE_DEVICE_US (2 ms) of the
+    // last tick that carried traffic; later idle ticks wait on the host (the bell's
+    // futex) and then run as plain ticks. 0: always on the host; -1: always on the GPU.
     void set_idle(uint32_t idle_us, uint32_t *bell) {
         idle_us_ = idle_us;
         bell_ = bell;
@@ -262,6 +267,8 @@ private:
     void ring_bell();                        // bump the doorbell and wake its futex waiters
     uint32_t idle_us_ = 0;
     uint32_t *bell_ = nullptr;
+    uint64_t idle_dev_window_ns_ = 2000ull * 1000;  // OCM_TICK_IDLE_DEVICE_US (UINT64_MAX: always)
+    uint64_t idle_dev_ticks_ = 0, idle_host_ticks_ = 0;  // idle ticks that waited on the GPU / the host
     std::atomic<bool> lazy_{false};          // the mesh is ticking idle: posts ring the bell
     uint64_t lazy_ticks_ = 0;
     // hop breakdown (TickStatsWire): per own record, post -> its tick queued / -> completion;

@@ -789,6 +789,9 @@ void TickTransport::stop() {
                  st.periods ? st.period_sum_ns / 1e3 / (double)st.periods : 0.0,
                  st.starts ? st.start_sum_ns / 1e3 / (double)st.starts : 0.0, st.start_max_ns / 1e3,
                  (unsigned long long)st.starts);
+    if (stats_ && st.lazy_ticks && !stats_logged_)
+        OCM_INFO("rank %d: idle ticks: %llu waited on the GPU, %llu on the host (OCM_TICK_IDLE_DEVICE_US)", rank_,
+                 (unsigned long long)idle_dev_ticks_, (unsigned long long)idle_host_ticks_);
     stats_logged_ = true;
 }
 
@@ -925,6 +928,11 @@ void TickTransport::run() {
     // Idle ticks: the seal waits on the GPU (RCCL), or this thread waits on the
     // bell before starting the tick (the socket ring, graph-captured ticks).
     const bool dev_idle = idle_us_ && coll->device_idle_wait();
+    if (const char *v = std::getenv("OCM_TICK_IDLE_DEVICE_US"); v && *v) {
+        const long long us = std::atoll(v);
+        idle_dev_window_ns_ = us < 0 ? UINT64_MAX : (uint64_t)us * 1000ull;
+    }
+    uint64_t last_traffic_ns = 0;  // completion of the last tick that carried records (0: none yet)
     uint64_t idle_tick = 0;     // number of the idle tick in flight (0: none)
     uint32_t idle_bell = 0;     // the bell when it was queued
     const uint64_t depth = (uint64_t)std::max(1, coll->depth());
@@ -969,15 +977,18 @@ void TickTransport::run() {
     while (!stop_) {
         {
             std::unique_lock<std::mutex> lk(mu_);
-            bool idle_now = false;
+            bool idle_now = false, idle_dev = false;
             if (done == issued && issued >= target && idle_us_) {
+                // the seal waits on the GPU only shortly after traffic (see set_idle)
+                idle_dev = dev_idle && last_traffic_ns &&
+                           (idle_dev_window_ns_ == UINT64_MAX || mono_ns() - last_traffic_ns < idle_dev_window_ns_);
                 // Idle mesh, idle ticks: every rank issues the next tick anyway (each
                 // decides from the same gathered ticks), so nobody needs waking over
                 // TCP. Its seal (or this thread, below) waits up to idle_us for a
                 // record of ours or the host-wide bell.
                 lazy_ = true;
                 if (unsent() > 0) ring_bell();  // posted before lazy_ was set: tell the peers
-                if (!dev_idle) {
+                if (!idle_dev) {
                     const uint64_t t_end = mono_ns() + (uint64_t)idle_us_ * 1000ull;
                     const uint32_t b0 = bell_ ? __atomic_load_n(bell_, __ATOMIC_ACQUIRE) : 0u;
                     while (!stop_ && unsent() == 0 && (!bell_ || __atomic_load_n(bell_, __ATOMIC_ACQUIRE) == b0)) {
@@ -998,6 +1009,7 @@ void TickTransport::run() {
                 target = issued + 1;
                 idle_now = true;
                 lazy_ticks_++;
+                (idle_dev ? idle_dev_ticks_ : idle_host_ticks_)++;
             } else if (done == issued && issued >= target) {
                 // Idle: sleep until there is something to send or a peer calls a tick.
                 cv_.wait(lk, [&] { return stop_.load() || unsent() > 0 || wake_upto_.load() > target; });
@@ -1029,7 +1041,7 @@ void TickTransport::run() {
                     slot->busy = out_.empty() ? 0 : 1;
                 }
                 if (announce_.load()) signal();  // let the event loop wake the peers first
-                const bool idle_start = idle_now && dev_idle;
+                const bool idle_start = idle_now && idle_dev;
                 if (idle_start) {
                     idle_tick = issued + 1;
                     idle_bell = bell_ ? __atomic_load_n(bell_, __ATOMIC_ACQUIRE) : 0u;
@@ -1155,6 +1167,7 @@ void TickTransport::run() {
         ticks_ = done;
         if (idle_tick && done >= idle_tick) idle_tick = 0;
         if (traffic) {
+            last_traffic_ns = mono_ns();
             target = std::max(target, done + kBusyTicks);
             lazy_ = false;  // a burst: ticks run back to back, posts need no bell
         }

@@ -1030,6 +1030,18 @@ int ocm_x_service_trace(uint64_t *out, int n_wgs) {
     return 0;
 }
 
+// Host addresses behind the copy service's hand-off (diagnostics: which NUMA node
+// holds them): the request record pages, the status slot, and extent 0's host
+// mapping of `a` (0 where there is none).
+int ocm_x_service_pages(ocm_alloc_t a, uint64_t out[3]) {
+    State &s = S();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    out[0] = reinterpret_cast<uint64_t>(s.svc_rec_pages);
+    out[1] = reinterpret_cast<uint64_t>(s.svc);
+    out[2] = (a && !a->ext.empty()) ? reinterpret_cast<uint64_t>(a->ext[0].hptr) : 0;
+    return s.svc ? 0 : -1;
+}
+
 // Transfer tuning at runtime (benchmarks): variant 0 auto / 1 reg / 2 lds,
 // blocks 0 = per-path default, nt = nontemporal destination stores.
 void ocm_x_set_tuning(int variant, int blocks, int nt) {

@@ -189,6 +189,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             "ocm_x_tick_stats": (ctypes.c_int, [ctypes.POINTER(u64)]),
             "ocm_x_quiesce": (None, []),
             "ocm_x_service_trace": (i32, [ctypes.POINTER(u64), i32]),
+            "ocm_x_service_pages": (i32, [ctypes.c_void_p, ctypes.POINTER(u64)]),
             "ocm_x_adam": (i32, [vp, vp, vp, u64, u64, u64, ctypes.POINTER(ctypes.c_float), vp]),
             "ocm_x_adam_multi": (i32, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(u64),
                                        ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64),
