@@ -980,8 +980,8 @@ void TickTransport::run() {
             bool idle_now = false, idle_dev = false;
             if (done == issued && issued >= target && idle_us_) {
                 // the seal waits on the GPU only shortly after traffic (see set_idle)
-                idle_dev = dev_idle && last_traffic_ns &&
-                           (idle_dev_window_ns_ == UINT64_MAX || mono_ns() - last_traffic_ns < idle_dev_window_ns_);
+                idle_dev = dev_idle && (idle_dev_window_ns_ == UINT64_MAX ||
+                                        (last_traffic_ns && mono_ns() - last_traffic_ns < idle_dev_window_ns_));
                 // Idle mesh, idle ticks: every rank issues the next tick anyway (each
                 // decides from the same gathered ticks), so nobody needs waking over
                 // TCP. Its seal (or this thread, below) waits up to idle_us for a

@@ -235,6 +235,43 @@ def test_rccl_tick_single_gpu(mesh_factory, monkeypatch, mode):
         assert "ticks per captured graph" in logs and "rccl tick graphs unavailable" not in logs, logs
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("window_us", ["2000", "-1", "0"])
+def test_rccl_idle_seals_wait_on_the_gpu_only_after_traffic(mesh_factory, monkeypatch, window_us):
+    """An idle RCCL mesh keeps ticking (OCM_TICK_IDLE_US, 1 ms). An idle seal that waits
+    for the doorbell on the GPU keeps a workgroup resident, which delays full-GPU GEMMs,
+    so it waits there only within OCM_TICK_IDLE_DEVICE_US (2 ms) of the last tick that
+    carried records, and later idle ticks wait on the host (-1: always on the GPU, the
+    first cut; 0: always on the host). The daemon logs the split when it stops; records
+    posted after the idle stretch still go through."""
+    import re
+    import time
+
+    monkeypatch.delenv("OCM_NO_GPU", raising=False)
+    m = mesh_factory(1, gpus=[0], extra_args=["--ctrl", "rccl"],
+                     env={"OCM_TICK_SELF": "1", "OCM_TICK_STATS": "1", "OCM_LEASE_BYTES": "0",
+                          "OCM_TICK_IDLE_DEVICE_US": window_us})
+    with api.Client(daemon_rank=0, gpu=0, ns=m.ns) as c:
+        _wait_tick_up(c, 1)
+        for _ in range(10):
+            c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=4096).free()
+        time.sleep(0.1)  # ~100 idle ticks
+        c.alloc(api.OCM_REMOTE_GPU, local_bytes=4096, remote_bytes=4096).free()
+        assert c.stats(0)["ctrl"] == "rccl"
+    m.stop()
+    logs = m.logs()
+    found = re.search(r"idle ticks: (\d+) waited on the GPU, (\d+) on the host", logs)
+    assert found, logs[-3000:]
+    dev, host = int(found.group(1)), int(found.group(2))
+    print(f"window {window_us} us: {dev} idle ticks waited on the GPU, {host} on the host")
+    if window_us == "-1":
+        assert host == 0 and dev >= 20, (dev, host)
+    elif window_us == "0":
+        assert dev == 0 and host >= 20, (dev, host)
+    else:
+        assert dev >= 1 and host >= 20, (dev, host)
+
+
 def _ctrl(c, n):
     return [c.stats(r)["ctrl"] for r in range(n)]
 
