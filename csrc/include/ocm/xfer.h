@@ -217,18 +217,24 @@ struct alignas(128) ServiceSlot {
     ServiceReq req;                   // the request record
     unsigned long long done;          // device -> host (own cache line)
     unsigned long long exited;        // device -> host, tagged: first seq NOT served when it left
-    unsigned long long gpu_ticks;     // device -> host: this instance's sum of request-seen -> done ticks of its lead (100 MHz)
     // device -> host, tagged: gang members resident so far (workgroup 0 included);
     // the host sizes every gang to at most this many.
     unsigned long long roster;
     unsigned long long lone;          // device -> host, tagged: first seq after which the members left
     unsigned long long epoch_now;     // host -> device: the current instance's epoch (a lone lead of another leaves)
     unsigned long long lead_xcd;      // device -> host, tagged: 1 + the XCD the current lead runs on (diagnostic)
-    unsigned long long pad[9];
+    unsigned long long pad0[2];
+    // device -> host: this instance's sum of request-seen -> done ticks of its lead (100 MHz).
+    // Written after every op, so it sits on the next cache line, away from `done`, which the
+    // host spins on.
+    unsigned long long gpu_ticks;
+    unsigned long long pad[7];
     // WGDONE: gang member i stores the seq it finished here (device -> host)
     unsigned long long wg_done[kServiceWgDoneMax];
 };
 static_assert(sizeof(ServiceSlot) == 256 + 8 * kServiceWgDoneMax, "service slot layout");
+static_assert(__builtin_offsetof(ServiceSlot, gpu_ticks) / 64 != __builtin_offsetof(ServiceSlot, done) / 64,
+              "gpu_ticks on a cache line of its own");
 
 constexpr int kServiceTraceWgs = 64;
 // Device-memory state of the gang. Zeroed only at the first launch and after an

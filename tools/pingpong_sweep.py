@@ -11,22 +11,29 @@ import subprocess
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VARIANTS = (("wc", "plain"), ("coh", "plain"), ("wc", "pause"), ("wc", "flush"))
+DATA_VARIANTS = (("wc", "plain", "none"), ("wc", "plain", "get"), ("wc", "plain", "put"))
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--out", default="")
+    ap.add_argument("--data", action="store_true", help="none/get/put with a 4 KiB copy per answer")
+    ap.add_argument("--cpus", default="", help="comma-separated CPUs (default: every allowed one)")
+    ap.add_argument("--n", type=int, default=3000)
     a = ap.parse_args()
     exe = os.path.join(REPO, "build", "bin", "pingpong_probe")
-    cpus = sorted(os.sched_getaffinity(0))
+    cpus = [int(x) for x in a.cpus.split(",") if x] or sorted(os.sched_getaffinity(0))
+    variants = DATA_VARIANTS if a.data else tuple(v + ("none",) for v in VARIANTS)
     rows = []
     for k in range(a.rounds):
         for cpu in cpus:
-            for bell, spin in VARIANTS:
-                r = subprocess.run([exe, str(cpu), bell, spin], capture_output=True, text=True, timeout=30)
+            for bell, spin, data in variants:
+                r = subprocess.run([exe, str(cpu), bell, spin, data, str(a.n)], capture_output=True, text=True,
+                                   timeout=60)
                 line = [x for x in r.stdout.splitlines() if x.startswith("{")]
-                row = json.loads(line[-1]) if line else {"cpu": cpu, "bell": bell, "spin": spin, "rc": r.returncode,
+                row = json.loads(line[-1]) if line else {"cpu": cpu, "bell": bell, "spin": spin, "data": data,
+                                                         "rc": r.returncode,
                                                          "err": r.stderr[-300:]}
                 row["round"] = k
                 rows.append(row)
