@@ -25,6 +25,20 @@ def _seal_env(sealed):
     return {"OCM_TICK_SOCKET_SEAL": sealed}
 
 
+def _wait_ticking(c, n):
+    """Wait until every rank has completed a tick, without posting anything: idle ticks
+    keep an idle mesh ticking, and the join is the first traffic. The fault-injection
+    tests use this, so the first DO_ALLOC / DO_FREE is the test's own."""
+    import time
+
+    deadline = time.time() + 20
+    while time.time() < deadline:
+        if all(c.stats(r)["ctrl_ticks"] > 0 for r in range(n)):
+            return
+        time.sleep(0.02)
+    raise AssertionError("the tick transport never ticked on every rank")
+
+
 def _wait_tick_up(c, n):
     import time
 
@@ -152,7 +166,7 @@ def test_tick_failure_after_do_free_frees_once(mesh_factory, sealed):
                      env={"OCM_TICK_SOCKET_SEAL": sealed, "OCM_TICK_FAULT": "fail_after_do_free",
                           "OCM_LEASE_BYTES": "0"})
     with api.Client(daemon_rank=0, ns=m.ns) as c:
-        _wait_tick_up(c, 3)
+        _wait_ticking(c, 3)
         held = [c.alloc(api.OCM_REMOTE_RDMA, local_bytes=1 << 20, remote_bytes=1 << 20) for _ in range(4)]
         for a in held:  # the first DO_FREE trips the fault; the rest ride TCP
             a.free()
